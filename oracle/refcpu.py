@@ -1,0 +1,286 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+CPU (torch fp32) restatement of the reference hot path. Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this
+module, and only as the checker / CPU baseline. The product path
+(``weatherforecast_stgcn_maml_amd``) never imports it.
+
+Pinned against golden vectors produced by running the reference modules themselves
+(``tests/golden/make_fixtures.py``; see ``tests/test_oracle_golden.py``). The PyG
+``GCNConv`` arithmetic is third-party (torch_geometric, unvendored, version unpinned,
+absent from this image): it is restated from PyG 2.x's published ``gcn_norm`` +
+``propagate`` and is "parity unpinned" at that boundary.
+
+What each function follows:
+  * ``gcn_conv``            PyG 2.x GCNConv (called at model.py:23-26, hybrid_model.py:65-74)
+  * ``stgcn_features``      hybrid_model.py:60-78 (no_grad GCN x4 + ReLU, dropout p=0)
+  * ``lstm_stack``          nn.LSTM(batch_first) semantics, gates [i,f,g,o] (hybrid_model.py:42-49,93-102)
+  * ``hybrid_forward``      hybrid_model.py:80-117 (F3, F4 layouts)
+  * ``mse``                 nn.MSELoss on the F4-permuted rows (train_hybrid_maml_v5.py:119,133)
+  * ``clip_coef``           torch.nn.utils.clip_grad_norm_ (train_hybrid_maml_v5.py:135-138)
+  * ``inner_loop``          train_hybrid_maml_v5.py:110-141 (SGD lr 0.01, batch of B samples)
+  * ``meta_step``           train_hybrid_maml_v5.py:144-184 (+ FO / second-order meta-grad)
+  * ``ReferencePort``       op-for-op mirror (per-node nn.LSTM loop, batch 1) for CPU timing
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+# ----------------------------------------------------------------------------- GCN
+def gcn_conv(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor,
+             bias: torch.Tensor) -> torch.Tensor:
+    """PyG 2.x GCNConv: add_remaining_self_loops over all x rows, deg at target,
+    norm = d_s^-1/2 d_t^-1/2, out = index_add(target, (x W^T)[source] * norm) + bias."""
+    n = x.shape[0]
+    ei = edge_index.to(torch.long)
+    keep = ei[0] != ei[1]
+    loop = torch.arange(n, dtype=torch.long)
+    row = torch.cat([ei[0][keep], loop])
+    col = torch.cat([ei[1][keep], loop])
+    w = torch.ones(row.numel(), dtype=x.dtype)
+    deg = torch.zeros(n, dtype=x.dtype).scatter_add_(0, col, w)
+    dinv = deg.pow(-0.5)
+    dinv = dinv.masked_fill(torch.isinf(dinv), 0.0)
+    norm = dinv[row] * w * dinv[col]
+    xw = x @ weight.t()
+    out = torch.zeros(n, weight.shape[0], dtype=x.dtype).index_add_(0, col, xw[row] * norm[:, None])
+    return out + bias
+
+
+def stgcn_features(x: torch.Tensor, edge_index: torch.Tensor, P: Dict[str, torch.Tensor]):
+    h = x
+    for k in range(1, 5):
+        h = F.relu(gcn_conv(h, edge_index, P[f"base_stgcn.conv{k}.lin.weight"],
+                            P[f"base_stgcn.conv{k}.bias"]))
+    return h
+
+
+# ----------------------------------------------------------------------------- LSTM
+def lstm_stack(seq: torch.Tensor, P: Dict[str, torch.Tensor], layers: int):
+    """seq [B, T, C] -> top-layer h_T [B, H]; h0 = c0 = 0."""
+    Bn, T, _ = seq.shape
+    inp = seq
+    for l in range(layers):
+        Wih, Whh = P[f"lstm.weight_ih_l{l}"], P[f"lstm.weight_hh_l{l}"]
+        b = P[f"lstm.bias_ih_l{l}"] + P[f"lstm.bias_hh_l{l}"]
+        H = Whh.shape[1]
+        xp = inp @ Wih.t()
+        h = torch.zeros(Bn, H, dtype=seq.dtype)
+        c = torch.zeros(Bn, H, dtype=seq.dtype)
+        outs = []
+        for t in range(T):
+            g = xp[:, t] + h @ Whh.t() + b
+            i, f, gg, o = g.chunk(4, dim=1)
+            i, f, gg, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(gg), torch.sigmoid(o)
+            c = f * c + i * gg
+            h = o * torch.tanh(c)
+            outs.append(h)
+        inp = torch.stack(outs, dim=1)
+    return inp[:, -1]
+
+
+def hybrid_forward(P: Dict[str, torch.Tensor], x: torch.Tensor, edge_index: torch.Tensor,
+                   dims, feats: torch.Tensor = None) -> torch.Tensor:
+    """x [T*N, 24] (time-major rows) -> pred [N*Hf, C] (rows n*Hf + h)."""
+    T, N = dims.window_size, dims.num_nodes
+    if feats is None:
+        with torch.no_grad():
+            feats = stgcn_features(x, edge_index, P)
+    seq = feats.view(T, N, -1).permute(1, 0, 2)
+    hT = lstm_stack(seq, P, dims.lstm_num_layers)
+    pred = hT @ P["output_layer.weight"].t() + P["output_layer.bias"]
+    return pred.view(N, dims.forecast_horizon, dims.output_channels).reshape(-1, dims.output_channels)
+
+
+def batched_forward(P, feats_list: Sequence[torch.Tensor], dims) -> List[torch.Tensor]:
+    """Same as ``hybrid_forward`` for several samples at once (sequences stacked)."""
+    T, N = dims.window_size, dims.num_nodes
+    seq = torch.cat([f.view(T, N, -1).permute(1, 0, 2) for f in feats_list], dim=0)
+    hT = lstm_stack(seq, P, dims.lstm_num_layers)
+    pred = hT @ P["output_layer.weight"].t() + P["output_layer.bias"]
+    pred = pred.view(len(feats_list), N * dims.forecast_horizon, dims.output_channels)
+    return list(pred)
+
+
+def mse(pred: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """nn.MSELoss (mean) row by row; pred rows are [node][horizon], y rows
+    [horizon][node] (F4) -- compared as they stand, exactly as the reference does."""
+    return ((pred - y) ** 2).mean()
+
+
+def clip_coef(grads: Sequence[torch.Tensor], max_norm: float):
+    norms = torch.stack([g.norm(2) for g in grads])
+    total = norms.norm(2)
+    return torch.clamp(max_norm / (total + 1e-6), max=1.0), total
+
+
+# ----------------------------------------------------------------------------- MAML
+TRAINABLE_PREFIXES = ("lstm.", "output_layer.")
+
+
+def trainable_names(P) -> List[str]:
+    return [k for k in P if k.startswith(TRAINABLE_PREFIXES)]
+
+
+def to_torch(P: Dict[str, np.ndarray]) -> Dict[str, torch.Tensor]:
+    return {k: torch.from_numpy(np.ascontiguousarray(v)).clone() for k, v in P.items()}
+
+
+class TaskData:
+    """A task's feature stream and graph; samples are windows (dataset.py:30-48)."""
+
+    def __init__(self, features: np.ndarray, edge_index: np.ndarray, dims):
+        self.features = torch.from_numpy(np.ascontiguousarray(features))
+        self.edge_index = torch.from_numpy(np.ascontiguousarray(edge_index)).long()
+        self.dims = dims
+        self._feat_cache = {}
+
+    def xy(self, i: int):
+        W, Hf, N = self.dims.window_size, self.dims.forecast_horizon, self.dims.num_nodes
+        x = self.features[i:i + W].reshape(W * N, -1)
+        y = self.features[i + W + 1:i + W + 1 + Hf, :, :12].reshape(Hf * N, 12)
+        return x, y
+
+    def gcn(self, i: int, P):
+        if i not in self._feat_cache:
+            x, _ = self.xy(i)
+            with torch.no_grad():
+                self._feat_cache[i] = stgcn_features(x, self.edge_index, P)
+        return self._feat_cache[i]
+
+
+def batch_loss(Pt: Dict[str, torch.Tensor], Pg: Dict[str, torch.Tensor], task: TaskData,
+               idx: Sequence[int]):
+    """Mean over the B samples of the per-sample MSE (SURVEY F9 definition)."""
+    P = dict(Pg)
+    P.update(Pt)
+    feats = [task.gcn(i, Pg) for i in idx]
+    preds = batched_forward(P, feats, task.dims)
+    losses = torch.stack([mse(p, task.xy(i)[1]) for p, i in zip(preds, idx)])
+    return losses.mean(), preds
+
+
+def support_schedule(step: int, batch: int, support: int) -> List[int]:
+    """Samples used by inner step ``step``: ``(step*B + b) mod S``. With B=1, S=15 this
+    is the reference's 6 epochs x first 15 support samples (train_hybrid_maml_v5.py:124-127)."""
+    return [(step * batch + b) % support for b in range(batch)]
+
+
+def inner_loop(Pt, Pg, task: TaskData, steps: int, batch: int, support: int, lr: float,
+               max_norm: float, create_graph: bool = False, record=None):
+    names = list(Pt.keys())
+    params = [Pt[k] for k in names]
+    for k in range(steps):
+        idx = support_schedule(k, batch, support)
+        cur = dict(zip(names, params))
+        loss, _ = batch_loss(cur, Pg, task, idx)
+        grads = torch.autograd.grad(loss, params, create_graph=create_graph)
+        coef, total = clip_coef(grads, max_norm)
+        if record is not None:
+            record.append((float(loss.detach()), float(total.detach()), float(coef.detach())))
+        params = [p - lr * coef * g for p, g in zip(params, grads)]
+        if not create_graph:
+            params = [p.detach().requires_grad_(True) for p in params]
+    return dict(zip(names, params))
+
+
+def meta_step(Pt0: Dict[str, torch.Tensor], Pg, tasks: Sequence[TaskData], query_idx,
+              steps: int, batch: int, support: int, lr: float, max_norm: float,
+              order: int, query_scale: float = 0.5):
+    """Returns dict(meta_loss, query_losses, meta_grad (per name, summed over tasks),
+    step_records, adapted (per task))."""
+    names = list(Pt0.keys())
+    meta_grad = {k: torch.zeros_like(v) for k, v in Pt0.items()}
+    qlosses, records, adapted_all = [], [], []
+    for task in tasks:
+        theta0 = [Pt0[k].detach().clone().requires_grad_(True) for k in names]
+        rec = []
+        adapted = inner_loop(dict(zip(names, theta0)), Pg, task, steps, batch, support, lr,
+                             max_norm, create_graph=(order == 2), record=rec)
+        qloss, _ = batch_loss(adapted, Pg, task, query_idx)
+        scaled = qloss * query_scale
+        if order == 2:
+            g = torch.autograd.grad(scaled, theta0)
+        elif order == 1:
+            g = torch.autograd.grad(scaled, [adapted[k] for k in names])
+        else:
+            g = [torch.zeros_like(t) for t in theta0]
+        for k, gi in zip(names, g):
+            meta_grad[k] += gi.detach()
+        qlosses.append(float(qloss))
+        records.append(rec)
+        adapted_all.append({k: v.detach() for k, v in adapted.items()})
+    meta_loss = sum(q * query_scale for q in qlosses)
+    return dict(meta_loss=meta_loss, query_losses=qlosses, meta_grad=meta_grad,
+                step_records=records, adapted=adapted_all)
+
+
+def adamw_step(params, grads, state, lr, betas=(0.9, 0.999), eps=1e-8, wd=1e-4,
+               max_norm=1.0):
+    """clip_grad_norm_ then torch.optim.AdamW (decoupled wd), in place; fp32."""
+    names = list(grads.keys())
+    coef, _ = clip_coef([grads[k] for k in names], max_norm)
+    b1, b2 = betas
+    state["step"] = state.get("step", 0) + 1
+    t = state["step"]
+    for k in names:
+        g = grads[k] * coef
+        m = state.setdefault("m_" + k, torch.zeros_like(g))
+        v = state.setdefault("v_" + k, torch.zeros_like(g))
+        params[k].mul_(1 - lr * wd)
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        params[k].addcdiv_(m, denom, value=-lr / bc1)
+    return params
+
+
+# ----------------------------------------------------------------------------- CPU port
+class ReferencePort:
+    """Op-for-op mirror of the reference's inner step for CPU timing: PyG-semantics GCN x4
+    under no_grad, a per-node ``nn.LSTM`` loop (hybrid_model.py:93-102), Linear head,
+    MSELoss, backward, clip_grad_norm_(1.0), SGD(lr=0.01) -- batch 1."""
+
+    def __init__(self, P: Dict[str, np.ndarray], dims, edge_index: np.ndarray):
+        self.dims = dims
+        H, L = dims.lstm_hidden_size, dims.lstm_num_layers
+        self.lstm = torch.nn.LSTM(dims.hidden_channels, H, L, batch_first=True)
+        self.head = torch.nn.Linear(H, dims.head_out)
+        with torch.no_grad():
+            for name, p in self.lstm.named_parameters():
+                p.copy_(torch.from_numpy(P["lstm." + name]))
+            self.head.weight.copy_(torch.from_numpy(P["output_layer.weight"]))
+            self.head.bias.copy_(torch.from_numpy(P["output_layer.bias"]))
+        self.Pg = {k: torch.from_numpy(v) for k, v in P.items() if k.startswith("base_stgcn")}
+        self.edge_index = torch.from_numpy(np.asarray(edge_index)).long()
+        params = list(self.lstm.parameters()) + list(self.head.parameters())
+        self.params = params
+        self.opt = torch.optim.SGD(params, lr=0.01)
+        self.crit = torch.nn.MSELoss()
+
+    def step(self, x: torch.Tensor, y: torch.Tensor) -> float:
+        d = self.dims
+        self.opt.zero_grad()
+        with torch.no_grad():
+            feats = stgcn_features(x, self.edge_index, self.Pg)
+        N = feats.shape[0] // d.window_size
+        seq = feats.view(d.window_size, N, -1).permute(1, 0, 2)
+        outs = []
+        for n in range(N):
+            o, _ = self.lstm(seq[n:n + 1])
+            outs.append(o[0, -1, :])
+        pred = self.head(torch.stack(outs, 0))
+        pred = pred.view(N, d.forecast_horizon, d.output_channels).reshape(-1, d.output_channels)
+        loss = self.crit(pred, y)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=1.0)
+        self.opt.step()
+        return float(loss)
