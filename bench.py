@@ -1,0 +1,205 @@
+"""Benchmark: MAML meta-steps/sec on BASELINE config 2 (15 tasks x B=32 x T=24 x N=441,
+Hc=256, LSTM 4x128, K=5 inner steps) on 1..8 MI355X, plus the reference's CPU path.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 launched by
+torch.distributed.run (one rank per GPU, RCCL). Prints ONE JSON line on rank 0.
+
+One "step" = one meta-step over the 15-task meta-batch: every task runs K inner steps of
+B samples (GCN x4 fwd, LSTM fwd, head + loss, BPTT, clip + SGD) and one B-sample query
+batch (+ backward for the meta-gradient), then one RCCL all-reduce of the 606,304-float
+meta-gradient and a replicated clip + AdamW. Tasks are sharded round-robin over ranks:
+the meta-batch is fixed, so scaling is "strong". Inputs are synthetic ERA5-shaped
+feature streams (portable numpy seeds 1000+j) resident in HBM before the timed region;
+weights are random-init with the reference's distributions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--tasks", type=int, default=15)
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--inner-steps", type=int, default=5)
+    p.add_argument("--nodes", type=int, default=441)
+    p.add_argument("--order", type=int, default=1)
+    p.add_argument("--cpu-sample-steps", type=int, default=6,
+                   help="reference-port CPU sample-steps to time (0 = skip)")
+    p.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
+    return p.parse_args()
+
+
+def algorithmic_flops(d, tasks, K, B, order):
+    """SURVEY §8(d) convention: per-sample FO step = GCN + LSTM_fwd + head + bwd."""
+    T, N, Cin, Hc, H, L = d.window_size, d.num_nodes, d.input_channels, d.hidden_channels, d.lstm_hidden_size, d.lstm_num_layers
+    HfC = d.forecast_horizon * d.output_channels
+    gcn = 2 * T * N * (Cin * Hc + 3 * Hc * Hc)
+    lstm = 2 * T * N * 4 * H * (Hc + H) + 2 * T * N * 4 * H * 2 * H * (L - 1)
+    head = 2 * N * H * HfC
+    bwd = lstm + (lstm - 2 * T * N * 4 * H * Hc) + 2 * head
+    per = gcn + lstm + head + bwd
+    fo = tasks * (K + 1) * B * per
+    if order == 2:
+        return fo + tasks * K * B * 2 * (lstm + head + bwd)
+    return fo
+
+
+def cpu_baseline(d, n_steps, P, ei, feats):
+    """Reference CPU path restated op for op (oracle.refcpu.ReferencePort: per-node nn.LSTM
+    loop, batch 1, MKLDNN), timed on this host's cores over a bounded sample."""
+    import torch
+    from oracle import refcpu
+    from weatherforecast_stgcn_maml_amd import synth
+
+    port = refcpu.ReferencePort(P, d, ei)
+    x, y = synth.sample_xy(feats, 0)
+    x = torch.from_numpy(np.ascontiguousarray(x))
+    y = torch.from_numpy(np.ascontiguousarray(y))
+    port.step(x, y)  # warm
+    t0 = time.perf_counter()
+    for i in range(n_steps):
+        xi, yi = synth.sample_xy(feats, i % 8)
+        port.step(torch.from_numpy(np.ascontiguousarray(xi)), torch.from_numpy(np.ascontiguousarray(yi)))
+    return (time.perf_counter() - t0) / n_steps, torch.get_num_threads()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from weatherforecast_stgcn_maml_amd import synth
+    from weatherforecast_stgcn_maml_amd.config import SEED, MamlConfig, ModelDims
+    from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
+    from weatherforecast_stgcn_maml_amd.maml import MetaLearner, shard_tasks, stream_len_for
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    d = ModelDims(num_nodes=args.nodes)
+    cfg = MamlConfig(inner_steps=args.inner_steps, batch=args.batch, order=args.order)
+    side = int(round(d.num_nodes ** 0.5))
+    lats, lons = synth.region_grid(n_lat=side, n_lon=side)
+    ei, _, _ = build_spatial_graph(lats, lons, 4)
+    P = synth.init_params(SEED, d)
+    names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
+    mine = shard_tasks(args.tasks, rank, world)
+    T_total = stream_len_for(cfg, d)
+    feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T_total) for j in mine]
+    ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
+                     ei, device=f"cuda:{local}")
+    ml.set_tasks(feats)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ml.meta_step(sync=False)
+    if not args.no_timing:
+        ml.ctx.timing_collect()  # drop warmup records
+        ml.ctx.timing(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = ml.meta_step(sync=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern = None
+    if not args.no_timing:
+        ml.ctx.timing(False)
+        kern = ml.ctx.timing_collect()
+    qmse = float(res.losses[-1].mean().item())
+    if world > 1:
+        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        q = torch.tensor([qmse * len(mine)], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(q)
+        qmse = float(q.item()) / args.tasks
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = args.steps / elapsed
+    flops_meta = algorithmic_flops(d, args.tasks, cfg.inner_steps, cfg.batch, 1)
+    out = {
+        "metric": "MAML meta-steps/sec (15-task batch, N=441, T=24)",
+        "value": value,
+        "unit": "meta-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic ERA5-shaped feature streams (numpy PCG64 seeds 1000+j), random-init weights",
+        "config": {
+            "workload": f"BASELINE config 2: {args.tasks} tasks x B={cfg.batch} x T={d.window_size} x "
+                        f"N={d.num_nodes} x C={d.input_channels}, Hc={d.hidden_channels}, "
+                        f"LSTM {d.lstm_num_layers}x{d.lstm_hidden_size}, K={cfg.inner_steps} inner steps",
+            "tasks": args.tasks, "batch": cfg.batch, "inner_steps": cfg.inner_steps,
+            "maml_order": cfg.order, "parallelism": f"task-sharded x{world} + RCCL all-reduce",
+            "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
+        },
+        "meta_step_tflop": flops_meta / 1e12,
+        "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,
+        "query_mse": qmse,
+    }
+    if world == 1 and cfg.order == 2:
+        out["meta_step_tflop_so"] = algorithmic_flops(d, args.tasks, cfg.inner_steps, cfg.batch, 2) / 1e12
+    if kern is not None:
+        dom = max((k for k in kern if k != "misc"), key=lambda k: kern[k]["ms"])
+        kd = kern[dom]
+        ach = kd["flops"] / (kd["ms"] * 1e-3) / 1e12 if kd["ms"] > 0 else 0.0
+        out["roofline"] = {
+            "kernel": dom, "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS,
+            "unit": "TFLOP/s", "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+            "avg_launch_us": kd["ms"] * 1e3 / max(kd["launches"], 1),
+            "flops_per_launch": kd["flops"] / max(kd["launches"], 1),
+        }
+        out["kernels"] = {k: {"ms_per_step": v["ms"] / args.steps,
+                              "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
+                              "launches_per_step": v["launches"] / args.steps}
+                          for k, v in kern.items()}
+    if rank == 0 and world == 1 and args.cpu_sample_steps > 0:
+        t_step, cores = cpu_baseline(d, args.cpu_sample_steps, P, ei, feats[0])
+        sample_steps = args.tasks * (cfg.inner_steps + 1) * cfg.batch
+        out["cpu_baseline"] = {
+            "value": 1.0 / (sample_steps * t_step), "unit": "meta-steps/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{args.cpu_sample_steps} batch-1 sample-steps (fwd+bwd+clip+SGD) of the reference's "
+                      f"per-node nn.LSTM CPU path at N={d.num_nodes}, {t_step:.3f} s each; meta-steps/s = "
+                      f"1/({sample_steps} sample-steps x t)",
+        }
+        out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

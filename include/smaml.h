@@ -1,0 +1,146 @@
+/*
+ * smaml.h -- C ABI of libsmaml.so, the MI355X (gfx950) STGCN-LSTM MAML hot path.
+ *
+ * The reference (Yalt8826/WeatherForecast_STGCN_MAML) is pure Python with no FFI layer;
+ * its boundary for this path is the module API of model.py / hybrid_model.py and the
+ * train loop entry points of train_hybrid_maml_v5.py. Each entry point below names the
+ * reference interface it replaces. The Python host package
+ * (weatherforecast_stgcn_maml_amd/_capi.py) binds these with ctypes; INTEGRATION.md
+ * shows the binding.
+ *
+ * Conventions
+ *  - Every function returns an int status: 0 = OK, else an SMAML_E* code;
+ *    smaml_last_error() returns the message of the calling thread's last failure.
+ *  - Device buffers are caller-owned device pointers (e.g. torch tensors' data_ptr()),
+ *    fp32, contiguous. Host arrays are marked _host.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream). All work is
+ *    enqueued on it; no call synchronises the device unless documented.
+ *  - A context is bound to one GPU, is not thread-safe, and is driven by one host thread.
+ *  - Trainable parameters (LSTM + head, the only tensors that receive gradients: SURVEY
+ *    F2) live in one flat "theta" vector in state_dict order; smaml_param_layout gives
+ *    each tensor's offset (offsets are padded to 64 floats; pads must be zero).
+ */
+#ifndef SMAML_H
+#define SMAML_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMAML_OK 0
+#define SMAML_EINVAL 1   /* bad argument / shape */
+#define SMAML_EHIP 2     /* HIP runtime error */
+#define SMAML_ENOMEM 3   /* device allocation failed */
+#define SMAML_ESTATE 4   /* missing set_graph / set_gcn_params / reserve / set_tasks */
+#define SMAML_ENOTIMPL 5 /* requested mode not built */
+
+typedef struct smaml_ctx smaml_ctx;
+
+/* Model shapes: model.STGCN(...) (model.py:8-28) + HybridSTGCN_LSTM(...) (hybrid_model.py:16-58). */
+typedef struct smaml_dims {
+  int32_t num_nodes;         /* N: grid nodes per region (441 = 21x21) */
+  int32_t window_size;       /* T (24) */
+  int32_t input_channels;    /* 24 */
+  int32_t hidden_channels;   /* GCN hidden (256) */
+  int32_t lstm_hidden_size;  /* 128 (multiple of 32) */
+  int32_t lstm_num_layers;   /* 4 */
+  int32_t forecast_horizon;  /* 8 */
+  int32_t output_channels;   /* 12 */
+} smaml_dims;
+
+const char* smaml_last_error(void);
+int32_t smaml_abi_version(void);
+
+/* ---- host-only helpers (no GPU needed) ------------------------------------------ */
+
+/* Flat layout of the trainable vector (which=0: lstm.* then output_layer.*, the order of
+ * HybridSTGCN_LSTM.get_trainable_parameters(), hybrid_model.py:119-124) or of the frozen
+ * GCN vector (which=1: base_stgcn.conv{1..4}.{bias,lin.weight}). Writes up to `cap`
+ * offsets/sizes, *count tensors and *total padded floats. */
+int smaml_param_layout(const smaml_dims* dims, int32_t which, int64_t* offsets, int64_t* sizes,
+                       int32_t cap, int32_t* count, int64_t* total);
+
+/* Normalised t=0 adjacency of PyG gcn_norm as ELL (width 8): replaces the
+ * add_remaining_self_loops + degree + norm part of GCNConv (model.py:23-26) for the
+ * edge_index of graphBuilder.build_spatial_graph (graphBuilder.py:9-47). */
+int smaml_graph_ell(const int64_t* edge_index_host, int64_t num_edges, int32_t num_nodes,
+                    int32_t* cols_host, float* vals_host);
+
+/* ---- context ----------------------------------------------------------------------- */
+int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out);
+int smaml_destroy(smaml_ctx* ctx);
+
+/* Upload the graph (edge_index [2, E] int64, host). */
+int smaml_set_graph(smaml_ctx* ctx, const int64_t* edge_index_host, int64_t num_edges);
+
+/* Frozen GCN parameters (flat, layout which=1), device pointer kept by reference. */
+int smaml_set_gcn_params(smaml_ctx* ctx, const float* gcn_flat);
+
+/* Size the workspace for `tasks` x `batch` samples per step (grows, never shrinks). */
+int smaml_reserve(smaml_ctx* ctx, int32_t tasks, int32_t batch);
+
+/* Bytes of device workspace currently held. */
+int64_t smaml_workspace_bytes(const smaml_ctx* ctx);
+
+/* ---- forward (module API) ----------------------------------------------------------- */
+
+/* GCNConv.forward(x, edge_index) (PyG semantics, F3): x [rows, cin] -> out [rows, cout].
+ * Rows < num_nodes aggregate over the graph, the rest see only their self loop. */
+int smaml_gcn_conv(smaml_ctx* ctx, void* stream, const float* x, int32_t rows, int32_t cin,
+                   const float* weight, const float* bias, int32_t cout, float* out);
+
+/* HybridSTGCN_LSTM.forward(x, edge_index) (hybrid_model.py:80-117) for `nsamples` samples:
+ * x_host[s] = device pointer to sample s's x [T*N, input_channels] (time-major rows);
+ * pred [nsamples][N*Hf][C] (rows n*Hf + h); feats (optional) [nsamples][T*N][Hc] = the
+ * extract_base_features output (hybrid_model.py:60-78). */
+int smaml_forward(smaml_ctx* ctx, void* stream, const float* theta, const float* const* x_host,
+                  int32_t nsamples, float* pred, float* feats);
+
+/* ---- training ------------------------------------------------------------------------ */
+
+/* Register the tasks' feature streams: features_host[j] = device pointer to a
+ * [t_total[j], N, input_channels] stream (WeatherGraphDataset.features, dataset.py:6-25).
+ * A sample is addressed by its window start w: x = stream[w:w+T], targets
+ * stream[w+T+1 .. w+T+Hf, :, :C] (dataset.py:30-48, F5). */
+int smaml_set_tasks(smaml_ctx* ctx, int32_t ntasks, const float* const* features_host,
+                    const int32_t* t_total_host);
+
+/* One meta-step over all registered tasks (meta_update_v4, train_hybrid_maml_v5.py:144-184,
+ * wrapping inner_loop_v4, :110-141):
+ *   per task: fast = theta; for k < steps: B-sample support step (mean MSE, backward,
+ *   clip_grad_norm_(max_norm), SGD(inner_lr)); then one B-sample query batch.
+ * windows_host: int32 [(steps+1)][ntasks][batch] window starts (row `steps` = query).
+ * order 0: reference semantics (the reference's outer step is a no-op):
+ *          query loss only; order 1: first-order MAML meta-gradient; order 2: second-order.
+ * meta_grad [P]: sum over tasks of d(query_scale * query_mse)/d(theta) (order >= 1).
+ * losses [(steps+1)][ntasks]: per-step support MSE; last row = query MSE (unscaled).
+ * norms [steps][ntasks] (optional): pre-clip gradient norms. fast_out [ntasks][P]
+ * (optional): adapted parameters. */
+int smaml_meta_step(smaml_ctx* ctx, void* stream, const float* theta, int32_t order, int32_t steps,
+                    int32_t batch, const int32_t* windows_host, float inner_lr, float max_norm,
+                    float query_scale, float* meta_grad, float* losses, float* norms, float* fast_out);
+
+/* Outer update (train_hybrid_maml_v5.py:174-179, 245-249): clip_grad_norm_(max_norm) of
+ * `grad` then torch.optim.AdamW step `step` (1-based) on theta, m, v (n floats).
+ * norm_out (optional, device float): pre-clip norm. */
+int smaml_adamw_step(smaml_ctx* ctx, void* stream, float* theta, const float* grad, float* m, float* v,
+                     int64_t n, int32_t step, float lr, float beta1, float beta2, float eps,
+                     float weight_decay, float max_norm, float* norm_out);
+
+/* ---- measurement (no reference counterpart; bench / profiling only) ------------------ */
+
+/* Enable/disable per-kernel-category HIP-event timing of the launches this context
+ * enqueues (events recorded on the launch stream around each kernel). */
+int smaml_timing(smaml_ctx* ctx, int32_t enable);
+
+/* Synchronise, then report and reset per category: summed kernel milliseconds, summed
+ * algorithmic FLOPs, launch counts. Categories (index): 0 gcn_layer, 1 lstm_fwd_step,
+ * 2 head_loss, 3 head_dh, 4 lstm_bwd_step, 5 wgrad (split-K + reduce), 6 dx, 7 misc. */
+int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* count, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMAML_H */

@@ -1,0 +1,219 @@
+"""ctypes binding of ``libsmaml.so`` (C ABI declared in ``include/smaml.h``).
+
+The product path has no CPU fallback: if the library is missing or no HIP device is
+present, every compute entry point raises ``SmamlError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsmaml.so")
+
+# every function include/smaml.h declares (checked by tests/test_capi_cpu.py)
+EXPORTS = (
+    "smaml_last_error", "smaml_abi_version", "smaml_param_layout", "smaml_graph_ell",
+    "smaml_create", "smaml_destroy", "smaml_set_graph", "smaml_set_gcn_params", "smaml_reserve",
+    "smaml_workspace_bytes", "smaml_gcn_conv", "smaml_forward", "smaml_set_tasks",
+    "smaml_meta_step", "smaml_adamw_step", "smaml_timing", "smaml_timing_collect",
+)
+
+TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "head_loss", "head_dh", "lstm_bwd_step",
+                     "wgrad", "dx", "misc")
+
+ERRORS = {1: "EINVAL", 2: "EHIP", 3: "ENOMEM", 4: "ESTATE", 5: "ENOTIMPL"}
+
+
+class SmamlError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"smaml error {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "num_nodes", "window_size", "input_channels", "hidden_channels", "lstm_hidden_size",
+        "lstm_num_layers", "forecast_horizon", "output_channels")]
+
+    @classmethod
+    def from_model(cls, d):
+        return cls(d.num_nodes, d.window_size, d.input_channels, d.hidden_channels,
+                   d.lstm_hidden_size, d.lstm_num_layers, d.forecast_horizon, d.output_channels)
+
+
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+PI64 = ctypes.POINTER(ctypes.c_int64)
+PI32 = ctypes.POINTER(ctypes.c_int32)
+PF32 = ctypes.POINTER(ctypes.c_float)
+PDIMS = ctypes.POINTER(Dims)
+
+_SIGS = {
+    "smaml_last_error": ([], ctypes.c_char_p),
+    "smaml_abi_version": ([], I32),
+    "smaml_param_layout": ([PDIMS, I32, PI64, PI64, I32, PI32, PI64], I32),
+    "smaml_graph_ell": ([PI64, I64, I32, PI32, PF32], I32),
+    "smaml_create": ([PDIMS, I32, ctypes.POINTER(P)], I32),
+    "smaml_destroy": ([P], I32),
+    "smaml_set_graph": ([P, PI64, I64], I32),
+    "smaml_set_gcn_params": ([P, P], I32),
+    "smaml_reserve": ([P, I32, I32], I32),
+    "smaml_workspace_bytes": ([P], I64),
+    "smaml_gcn_conv": ([P, P, P, I32, I32, P, P, I32, P], I32),
+    "smaml_forward": ([P, P, P, ctypes.POINTER(P), I32, P, P], I32),
+    "smaml_set_tasks": ([P, I32, ctypes.POINTER(P), PI32], I32),
+    "smaml_meta_step": ([P, P, P, I32, I32, I32, PI32, F32, F32, F32, P, P, P, P], I32),
+    "smaml_adamw_step": ([P, P, P, P, P, P, I64, I32, F32, F32, F32, F32, F32, F32, P], I32),
+    "smaml_timing": ([P, I32], I32),
+    "smaml_timing_collect": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                              PI64, I32], I32),
+}
+
+
+def lib():
+    """Load libsmaml.so (raises SmamlError if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise SmamlError(-1, f"{LIB_PATH} not built; run __graft_entry__.build()")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (args, res) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise SmamlError(rc, lib().smaml_last_error().decode(errors="replace"))
+
+
+def param_layout(dims, which: int):
+    """[(offset, size)] of the flat trainable (which=0) or GCN (which=1) vector + total."""
+    L = lib()
+    d = Dims.from_model(dims)
+    cap = 64
+    offs = (ctypes.c_int64 * cap)()
+    sizes = (ctypes.c_int64 * cap)()
+    cnt = ctypes.c_int32()
+    tot = ctypes.c_int64()
+    check(L.smaml_param_layout(ctypes.byref(d), which, offs, sizes, cap, ctypes.byref(cnt),
+                               ctypes.byref(tot)))
+    return [(offs[i], sizes[i]) for i in range(cnt.value)], tot.value
+
+
+def graph_ell(edge_index: np.ndarray, num_nodes: int):
+    L = lib()
+    ei = np.ascontiguousarray(edge_index, dtype=np.int64)
+    E = ei.shape[1]
+    cols = np.zeros((num_nodes, 8), np.int32)
+    vals = np.zeros((num_nodes, 8), np.float32)
+    check(L.smaml_graph_ell(ei.ctypes.data_as(PI64), E, num_nodes, cols.ctypes.data_as(PI32),
+                            vals.ctypes.data_as(PF32)))
+    return cols, vals
+
+
+def ptr(t) -> int:
+    return t.data_ptr()
+
+
+def stream_ptr(torch_mod):
+    return torch_mod.cuda.current_stream().cuda_stream
+
+
+class Context:
+    """Owns one ``smaml_ctx`` (one GPU, one host thread)."""
+
+    def __init__(self, dims, device: int = 0):
+        self.dims = dims
+        self._L = lib()
+        self._h = P()
+        self._d = Dims.from_model(dims)
+        check(self._L.smaml_create(ctypes.byref(self._d), int(device), ctypes.byref(self._h)))
+        self.device = device
+        self._keep = []
+        self.graph_key = None
+
+    def close(self):
+        if self._h:
+            self._L.smaml_destroy(self._h)
+            self._h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- setup
+    def set_graph(self, edge_index: np.ndarray):
+        ei = np.ascontiguousarray(edge_index, dtype=np.int64)
+        check(self._L.smaml_set_graph(self._h, ei.ctypes.data_as(PI64), ei.shape[1]))
+        self.graph_key = ei.tobytes()
+
+    def set_gcn_params(self, flat):
+        self._gcn = flat
+        check(self._L.smaml_set_gcn_params(self._h, ptr(flat)))
+
+    def reserve(self, tasks, batch):
+        check(self._L.smaml_reserve(self._h, int(tasks), int(batch)))
+
+    def workspace_bytes(self):
+        return int(self._L.smaml_workspace_bytes(self._h))
+
+    # --- compute
+    def gcn_conv(self, stream, x, weight, bias, out):
+        check(self._L.smaml_gcn_conv(self._h, stream, ptr(x), x.shape[0], x.shape[1], ptr(weight),
+                                     ptr(bias), weight.shape[0], ptr(out)))
+
+    def forward(self, stream, theta, xs, pred, feats=None):
+        arr = (P * len(xs))(*[ptr(x) for x in xs])
+        check(self._L.smaml_forward(self._h, stream, ptr(theta), arr, len(xs), ptr(pred),
+                                    ptr(feats) if feats is not None else None))
+
+    def set_tasks(self, feats):
+        arr = (P * len(feats))(*[ptr(f) for f in feats])
+        tt = (ctypes.c_int32 * len(feats))(*[int(f.shape[0]) for f in feats])
+        self._tasks = list(feats)
+        check(self._L.smaml_set_tasks(self._h, len(feats), arr, tt))
+
+    def meta_step(self, stream, theta, order, steps, batch, windows: np.ndarray, inner_lr, max_norm,
+                  query_scale, meta_grad=None, losses=None, norms=None, fast_out=None):
+        w = np.ascontiguousarray(windows, dtype=np.int32)
+        check(self._L.smaml_meta_step(
+            self._h, stream, ptr(theta), int(order), int(steps), int(batch), w.ctypes.data_as(PI32),
+            float(inner_lr), float(max_norm), float(query_scale),
+            ptr(meta_grad) if meta_grad is not None else None,
+            ptr(losses) if losses is not None else None,
+            ptr(norms) if norms is not None else None,
+            ptr(fast_out) if fast_out is not None else None))
+
+    def timing(self, enable: bool):
+        check(self._L.smaml_timing(self._h, 1 if enable else 0))
+
+    def timing_collect(self):
+        n = len(TIMING_CATEGORIES)
+        ms = (ctypes.c_double * n)()
+        fl = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        check(self._L.smaml_timing_collect(self._h, ms, fl, cnt, n))
+        return {name: {"ms": ms[i], "flops": fl[i], "launches": cnt[i]}
+                for i, name in enumerate(TIMING_CATEGORIES)}
+
+    def adamw_step(self, stream, theta, grad, m, v, step, lr, betas, eps, wd, max_norm, norm_out=None):
+        check(self._L.smaml_adamw_step(self._h, stream, ptr(theta), ptr(grad), ptr(m), ptr(v),
+                                       theta.numel(), int(step), float(lr), float(betas[0]),
+                                       float(betas[1]), float(eps), float(wd), float(max_norm),
+                                       ptr(norm_out) if norm_out is not None else None))

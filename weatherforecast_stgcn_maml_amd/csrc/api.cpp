@@ -1,0 +1,672 @@
+// C ABI (include/smaml.h) and the host-side driver of the STGCN-LSTM MAML hot path.
+//
+// The inner loop (train_hybrid_maml_v5.py:110-141) and the meta-step
+// (train_hybrid_maml_v5.py:144-184) run here in C++: Python calls one entry point per
+// meta-step and never sees an inner step. Everything for all tasks of the meta-batch
+// is batched into each launch (blockIdx.z = task, per-task fast weights).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "smaml.h"
+
+using namespace smaml;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(x)                                                                              \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) return fail(SMAML_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define TRY(x)                \
+  do {                        \
+    int r_ = (x);             \
+    if (r_ != SMAML_OK) return r_; \
+  } while (0)
+
+constexpr int64_t PAD = 64;  // floats: every tensor offset is 256-B aligned
+
+int64_t pad_up(int64_t x) { return (x + PAD - 1) / PAD * PAD; }
+
+struct Spec {
+  int64_t off, size;
+};
+
+int check_dims(const smaml_dims* d) {
+  if (!d) return fail(SMAML_EINVAL, "dims is NULL");
+  if (d->num_nodes <= 0 || d->window_size <= 0 || d->lstm_num_layers <= 0 ||
+      d->lstm_num_layers > MAX_LAYERS || d->forecast_horizon <= 0 || d->output_channels <= 0)
+    return fail(SMAML_EINVAL, "non-positive dimension");
+  if (d->input_channels % 4 || d->hidden_channels % 4)
+    return fail(SMAML_EINVAL, "input/hidden channels must be multiples of 4");
+  if (d->lstm_hidden_size % 32) return fail(SMAML_EINVAL, "lstm_hidden_size must be a multiple of 32");
+  if (d->forecast_horizon * d->output_channels > 128)
+    return fail(SMAML_EINVAL, "forecast_horizon*output_channels must be <= 128");
+  if (d->output_channels > d->input_channels)
+    return fail(SMAML_EINVAL, "output_channels must not exceed input_channels (targets come from inputs)");
+  return SMAML_OK;
+}
+
+void layout(const smaml_dims& d, int which, std::vector<Spec>& specs, int64_t& total) {
+  specs.clear();
+  int64_t off = 0;
+  auto add = [&](int64_t n) {
+    specs.push_back({off, n});
+    off = pad_up(off + n);
+  };
+  const int64_t H = d.lstm_hidden_size, G = 4 * H;
+  if (which == 0) {
+    for (int l = 0; l < d.lstm_num_layers; ++l) {
+      const int64_t cin = l == 0 ? d.hidden_channels : H;
+      add(G * cin);  // weight_ih_l
+      add(G * H);    // weight_hh_l
+      add(G);        // bias_ih_l
+      add(G);        // bias_hh_l
+    }
+    add((int64_t)d.forecast_horizon * d.output_channels * H);  // output_layer.weight
+    add((int64_t)d.forecast_horizon * d.output_channels);      // output_layer.bias
+  } else {
+    int64_t cin = d.input_channels;
+    for (int k = 0; k < 4; ++k) {
+      add(d.hidden_channels);        // convK.bias
+      add(d.hidden_channels * cin);  // convK.lin.weight
+      cin = d.hidden_channels;
+    }
+  }
+  total = off;
+}
+
+int build_ell(const int64_t* ei, int64_t E, int N, std::vector<int32_t>& cols, std::vector<float>& vals) {
+  cols.assign((size_t)N * ELLW, 0);
+  vals.assign((size_t)N * ELLW, 0.f);
+  std::vector<float> deg(N, 1.f);  // self loop (add_remaining_self_loops, fill 1)
+  const int64_t* src = ei;
+  const int64_t* dst = ei + E;
+  for (int64_t e = 0; e < E; ++e) {
+    if (src[e] < 0 || src[e] >= N || dst[e] < 0 || dst[e] >= N)
+      return fail(SMAML_EINVAL, "edge_index references a node outside [0, num_nodes)");
+    if (src[e] != dst[e]) deg[dst[e]] += 1.f;
+  }
+  std::vector<float> dinv(N);
+  for (int i = 0; i < N; ++i) dinv[i] = 1.f / std::sqrt(deg[i]);
+  std::vector<int> fill(N, 0);
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t s = src[e], t = dst[e];
+    if (s == t) continue;
+    if (fill[t] >= ELLW - 1) return fail(SMAML_EINVAL, "node in-degree exceeds the ELL width (7)");
+    cols[(size_t)t * ELLW + fill[t]] = (int32_t)s;
+    vals[(size_t)t * ELLW + fill[t]] = dinv[s] * dinv[t];
+    ++fill[t];
+  }
+  for (int i = 0; i < N; ++i) {
+    for (int j = fill[i]; j < ELLW; ++j) cols[(size_t)i * ELLW + j] = i;
+    vals[(size_t)i * ELLW + fill[i]] = dinv[i] * dinv[i];
+  }
+  return SMAML_OK;
+}
+
+enum Cat { C_GCN = 0, C_FWD, C_HEAD, C_HEAD_DH, C_BWD, C_WGRAD, C_DX, C_MISC, NCAT };
+
+// Live per-category kernel timing with HIP events on the launch stream (bench roofline).
+struct Timer {
+  bool on = false;
+  struct Rec {
+    int cat;
+    hipEvent_t a, b;
+    double flops;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  double ms[NCAT] = {};
+  double flops[NCAT] = {};
+  int64_t count[NCAT] = {};
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+};
+
+}  // namespace
+
+struct smaml_ctx {
+  smaml_dims dims{};
+  Dims d{};
+  ParamOff po{};
+  GcnOff go{};
+  int device = 0;
+  int32_t* ell_c = nullptr;
+  float* ell_v = nullptr;
+  const float* gcn = nullptr;
+  // workspace
+  char* arena = nullptr;
+  int64_t arena_bytes = 0;
+  int zb_cap = 0, z_cap = 0;
+  Work w{};
+  float* fast = nullptr;
+  float* grad = nullptr;
+  float* scratch_loss = nullptr;  // [(steps+1)*Z] fallback when the caller passes no buffer
+  int64_t scratch_loss_cap = 0;
+  // device pointer table for sample windows + pinned staging
+  const float** xtab = nullptr;
+  const float** xtab_pinned = nullptr;
+  int64_t xtab_cap = 0;
+  hipEvent_t xtab_evt = nullptr;
+  // tasks
+  std::vector<const float*> feats;
+  std::vector<int> t_total;
+  Timer tm;
+};
+
+namespace {
+
+int ensure_device(smaml_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  return SMAML_OK;
+}
+
+int reserve(smaml_ctx* c, int Z, int B) {
+  const int zb = Z * B;
+  if (zb <= c->zb_cap && Z <= c->z_cap) return SMAML_OK;
+  const int zbc = std::max(zb, c->zb_cap), zc = std::max(Z, c->z_cap);
+  const Dims& d = c->d;
+  const int64_t rows = (int64_t)zbc * d.T * d.N;
+  const int64_t G = 4 * d.H;
+  const int64_t seq = (int64_t)zbc * d.N;
+  int max_cin = std::max(d.Hc, d.H);
+  const int64_t wpart = std::max<int64_t>((int64_t)zc * G * (max_cin + d.H + 1) * 32, 1 << 24);
+  const int64_t lblk = (int64_t)zc * ((seq + 127) / 128 + 1);
+  const bool alias_gcn = G >= 2 * d.Hc;
+  std::vector<std::pair<void**, int64_t>> parts;  // (dst, bytes)
+  Work w{};
+  float* dummy = nullptr;
+  parts.push_back({(void**)&w.F, rows * d.Hc * 4});
+  parts.push_back({(void**)&w.Hs, rows * d.L * d.H * 4});
+  parts.push_back({(void**)&w.Cs, rows * d.L * d.H * 4});
+  parts.push_back({(void**)&w.Gs, rows * d.L * G * 4});
+  parts.push_back({(void**)&w.dG, rows * G * 4});
+  parts.push_back({(void**)&w.dH, rows * d.H * 4});
+  parts.push_back({(void**)&w.dc, seq * d.H * 4});
+  parts.push_back({(void**)&w.pred, seq * d.HfC * 4});
+  parts.push_back({(void**)&w.dpred, seq * d.HfC * 4});
+  parts.push_back({(void**)&w.wpart, wpart * 4});
+  parts.push_back({(void**)&w.lpart, lblk * 4});
+  parts.push_back({(void**)&w.sqpart, (int64_t)(zc + 1) * SQB * 8});
+  float *fast = nullptr, *grad = nullptr;
+  parts.push_back({(void**)&fast, (int64_t)zc * c->po.P * 4});
+  parts.push_back({(void**)&grad, (int64_t)zc * c->po.P * 4});
+  if (!alias_gcn) {
+    parts.push_back({(void**)&w.gcnA, rows * d.Hc * 4});
+    parts.push_back({(void**)&w.gcnB, rows * d.Hc * 4});
+  }
+  (void)dummy;
+  int64_t total = 0;
+  for (auto& p : parts) total += (p.second + 255) / 256 * 256;
+  if (c->arena) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree(c->arena));
+    c->arena = nullptr;
+    c->arena_bytes = 0;
+  }
+  char* arena = nullptr;
+  if (hipMalloc((void**)&arena, total) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMAML_ENOMEM, "hipMalloc of " + std::to_string(total) + " B workspace failed");
+  }
+  int64_t off = 0;
+  for (auto& p : parts) {
+    *p.first = arena + off;
+    off += (p.second + 255) / 256 * 256;
+  }
+  if (alias_gcn) {
+    w.gcnA = w.dG;
+    w.gcnB = w.dG + rows * d.Hc;
+  }
+  w.wpart_floats = wpart;
+  HIP_TRY(hipMemset(grad, 0, (size_t)zc * c->po.P * 4));
+  HIP_TRY(hipMemset(fast, 0, (size_t)zc * c->po.P * 4));
+  c->arena = arena;
+  c->arena_bytes = total;
+  c->w = w;
+  c->fast = fast;
+  c->grad = grad;
+  c->zb_cap = zbc;
+  c->z_cap = zc;
+  return SMAML_OK;
+}
+
+int ensure_xtab(smaml_ctx* c, int64_t n) {
+  if (n <= c->xtab_cap) return SMAML_OK;
+  if (c->xtab) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree((void*)c->xtab));
+    HIP_TRY(hipHostFree((void*)c->xtab_pinned));
+  }
+  const int64_t cap = std::max<int64_t>(n, 1024);
+  HIP_TRY(hipMalloc((void**)&c->xtab, cap * sizeof(float*)));
+  HIP_TRY(hipHostMalloc((void**)&c->xtab_pinned, cap * sizeof(float*), hipHostMallocDefault));
+  c->xtab_cap = cap;
+  return SMAML_OK;
+}
+
+int upload_xtab(smaml_ctx* c, hipStream_t s, const float* const* ptrs, int64_t n) {
+  TRY(ensure_xtab(c, n));
+  HIP_TRY(hipEventSynchronize(c->xtab_evt));  // previous upload has consumed the staging table
+  std::memcpy((void*)c->xtab_pinned, ptrs, n * sizeof(float*));
+  HIP_TRY(hipMemcpyAsync((void*)c->xtab, c->xtab_pinned, n * sizeof(float*), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(c->xtab_evt, s));
+  return SMAML_OK;
+}
+
+void set_work(smaml_ctx* c, int Z, int B) {
+  c->w.Z = Z;
+  c->w.B = B;
+  c->w.M = B * c->d.N;
+  c->w.lblocks = (c->w.M + 127) / 128;
+}
+
+#define TIMED(c, s, cat, fl, stmt)                              \
+  do {                                                           \
+    if ((c)->tm.on) {                                            \
+      hipEvent_t a_ = (c)->tm.get(), b_ = (c)->tm.get();         \
+      (void)hipEventRecord(a_, s);                               \
+      stmt;                                                      \
+      (void)hipEventRecord(b_, s);                               \
+      (c)->tm.recs.push_back({cat, a_, b_, (double)(fl)});       \
+    } else {                                                     \
+      stmt;                                                      \
+    }                                                            \
+  } while (0)
+
+// GCN x4 (no_grad, F2) + LSTM forward over all layers and time steps.
+int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  const int rps = d.T * d.N;
+  const int zb = w.Z * w.B;
+  const float* src = nullptr;
+  float* bufs[2] = {w.gcnA, w.gcnB};
+  for (int k = 0; k < 4; ++k) {
+    const bool last = k == 3;
+    float* dst = last ? w.F : bufs[k & 1];
+    TIMED(c, s, C_GCN, 2.0 * zb * rps * c->go.cin[k] * d.Hc,
+          launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
+                           c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
+                           rps, d.N));
+    src = dst;
+  }
+  for (int l = 0; l < d.L; ++l)
+    for (int t = 0; t < d.T; ++t)
+      TIMED(c, s, C_FWD, 2.0 * w.Z * w.M * 4 * d.H * (c->po.lay[l].cin + (t > 0 ? d.H : 0)),
+            launch_lstm_fwd_step(s, d, w, l, t, theta, tstride, c->po.lay[l]));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+// Backward from dpred (already written by k_head_loss) into grad [Z][P].
+int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, float* grad) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  const ParamOff& po = c->po;
+  const int64_t TM = (int64_t)d.T * w.M;
+  const int64_t lsz = (int64_t)w.Z * TM * d.H;
+  TIMED(c, s, C_MISC, 0, (void)hipMemsetAsync(w.dH, 0, (size_t)lsz * 4, s));
+  TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
+  const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
+  TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
+        launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, top + (int64_t)(d.T - 1) * w.M * d.H,
+                     TM * d.H, d.H, nullptr, 0, 0, w.M, 0, grad, po.P, po.wo, -1, po.bo, -1));
+  for (int l = d.L - 1; l >= 0; --l) {
+    const LayerOff& lo = po.lay[l];
+    for (int t = d.T - 1; t >= 0; --t)
+      TIMED(c, s, C_BWD, t + 1 < d.T ? 2.0 * w.Z * w.M * 4 * d.H * d.H : 0.0,
+            launch_lstm_bwd_step(s, d, w, l, t, theta, tstride, lo));
+    const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
+    TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H),
+          launch_wgrad(s, d, w, w.dG, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
+                       TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih, lo.bhh));
+    if (l > 0) TIMED(c, s, C_DX, 2.0 * w.Z * TM * 4 * d.H * lo.cin, launch_dx(s, d, w, theta, tstride, lo));
+  }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int require_ready(smaml_ctx* c) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!c->ell_c) return fail(SMAML_ESTATE, "smaml_set_graph not called");
+  if (!c->gcn) return fail(SMAML_ESTATE, "smaml_set_gcn_params not called");
+  return SMAML_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// =====================================================================================
+extern "C" {
+
+const char* smaml_last_error(void) { return g_err.c_str(); }
+
+int32_t smaml_abi_version(void) { return 1; }
+
+int smaml_param_layout(const smaml_dims* dims, int32_t which, int64_t* offsets, int64_t* sizes, int32_t cap,
+                       int32_t* count, int64_t* total) {
+  TRY(check_dims(dims));
+  if (which != 0 && which != 1) return fail(SMAML_EINVAL, "which must be 0 (trainable) or 1 (gcn)");
+  std::vector<Spec> sp;
+  int64_t tot = 0;
+  layout(*dims, which, sp, tot);
+  if (count) *count = (int32_t)sp.size();
+  if (total) *total = tot;
+  for (int i = 0; i < (int)sp.size() && i < cap; ++i) {
+    if (offsets) offsets[i] = sp[i].off;
+    if (sizes) sizes[i] = sp[i].size;
+  }
+  return SMAML_OK;
+}
+
+int smaml_graph_ell(const int64_t* edge_index_host, int64_t num_edges, int32_t num_nodes, int32_t* cols_host,
+                    float* vals_host) {
+  if (!edge_index_host || !cols_host || !vals_host || num_nodes <= 0 || num_edges < 0)
+    return fail(SMAML_EINVAL, "bad arguments to smaml_graph_ell");
+  std::vector<int32_t> cols;
+  std::vector<float> vals;
+  TRY(build_ell(edge_index_host, num_edges, num_nodes, cols, vals));
+  std::memcpy(cols_host, cols.data(), cols.size() * 4);
+  std::memcpy(vals_host, vals.data(), vals.size() * 4);
+  return SMAML_OK;
+}
+
+int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out) {
+  if (!out) return fail(SMAML_EINVAL, "out is NULL");
+  *out = nullptr;
+  TRY(check_dims(dims));
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(SMAML_EINVAL, "device ordinal out of range");
+  smaml_ctx* c = new smaml_ctx();
+  c->dims = *dims;
+  c->device = device;
+  Dims& d = c->d;
+  d.N = dims->num_nodes;
+  d.T = dims->window_size;
+  d.Cin0 = dims->input_channels;
+  d.Hc = dims->hidden_channels;
+  d.H = dims->lstm_hidden_size;
+  d.L = dims->lstm_num_layers;
+  d.Hf = dims->forecast_horizon;
+  d.C = dims->output_channels;
+  d.HfC = d.Hf * d.C;
+  std::vector<Spec> sp;
+  int64_t tot = 0;
+  layout(*dims, 0, sp, tot);
+  for (int l = 0; l < d.L; ++l) {
+    c->po.lay[l].wih = sp[4 * l].off;
+    c->po.lay[l].whh = sp[4 * l + 1].off;
+    c->po.lay[l].bih = sp[4 * l + 2].off;
+    c->po.lay[l].bhh = sp[4 * l + 3].off;
+    c->po.lay[l].cin = l == 0 ? d.Hc : d.H;
+  }
+  c->po.wo = sp[4 * d.L].off;
+  c->po.bo = sp[4 * d.L + 1].off;
+  c->po.P = tot;
+  int64_t nv = 0;
+  for (auto& x : sp) nv += x.size;
+  c->po.n_valid = nv;
+  layout(*dims, 1, sp, tot);
+  for (int k = 0; k < 4; ++k) {
+    c->go.b[k] = sp[2 * k].off;
+    c->go.w[k] = sp[2 * k + 1].off;
+    c->go.cin[k] = k == 0 ? d.Cin0 : d.Hc;
+  }
+  c->go.total = tot;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xtab_evt, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(SMAML_EHIP, std::string("context init: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return SMAML_OK;
+}
+
+int smaml_destroy(smaml_ctx* c) {
+  if (!c) return SMAML_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  if (c->arena) (void)hipFree(c->arena);
+  if (c->ell_c) (void)hipFree(c->ell_c);
+  if (c->ell_v) (void)hipFree(c->ell_v);
+  if (c->xtab) (void)hipFree((void*)c->xtab);
+  if (c->xtab_pinned) (void)hipHostFree((void*)c->xtab_pinned);
+  if (c->scratch_loss) (void)hipFree(c->scratch_loss);
+  if (c->xtab_evt) (void)hipEventDestroy(c->xtab_evt);
+  for (auto& r : c->tm.recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : c->tm.pool) (void)hipEventDestroy(e);
+  delete c;
+  return SMAML_OK;
+}
+
+int smaml_set_graph(smaml_ctx* c, const int64_t* edge_index_host, int64_t num_edges) {
+  if (!c || !edge_index_host) return fail(SMAML_EINVAL, "NULL argument");
+  TRY(ensure_device(c));
+  std::vector<int32_t> cols;
+  std::vector<float> vals;
+  TRY(build_ell(edge_index_host, num_edges, c->d.N, cols, vals));
+  if (!c->ell_c) {
+    HIP_TRY(hipMalloc((void**)&c->ell_c, cols.size() * 4));
+    HIP_TRY(hipMalloc((void**)&c->ell_v, vals.size() * 4));
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(c->ell_c, cols.data(), cols.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->ell_v, vals.data(), vals.size() * 4, hipMemcpyHostToDevice));
+  return SMAML_OK;
+}
+
+int smaml_set_gcn_params(smaml_ctx* c, const float* gcn_flat) {
+  if (!c || !gcn_flat) return fail(SMAML_EINVAL, "NULL argument");
+  if (!aligned16(gcn_flat)) return fail(SMAML_EINVAL, "gcn params must be 16-byte aligned");
+  c->gcn = gcn_flat;
+  return SMAML_OK;
+}
+
+int smaml_reserve(smaml_ctx* c, int32_t tasks, int32_t batch) {
+  if (!c || tasks <= 0 || batch <= 0) return fail(SMAML_EINVAL, "bad reserve arguments");
+  TRY(ensure_device(c));
+  return reserve(c, tasks, batch);
+}
+
+int64_t smaml_workspace_bytes(const smaml_ctx* c) { return c ? c->arena_bytes : 0; }
+
+int smaml_gcn_conv(smaml_ctx* c, void* stream, const float* x, int32_t rows, int32_t cin, const float* weight,
+                   const float* bias, int32_t cout, float* out) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!c->ell_c) return fail(SMAML_ESTATE, "smaml_set_graph not called");
+  if (!x || !weight || !bias || !out || rows <= 0 || cin <= 0 || cout <= 0)
+    return fail(SMAML_EINVAL, "bad gcn_conv arguments");
+  if (cin % 4) return fail(SMAML_EINVAL, "cin must be a multiple of 4");
+  if (!aligned16(x) || !aligned16(weight)) return fail(SMAML_EINVAL, "x / weight must be 16-byte aligned");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  launch_gcn_layer(s, c->d, 0, 1, 1, nullptr, x, out, false, false, weight, bias, cin, cout, c->ell_c, c->ell_v,
+                   rows, std::min(rows, c->d.N));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_forward(smaml_ctx* c, void* stream, const float* theta, const float* const* x_host, int32_t nsamples,
+                  float* pred, float* feats) {
+  TRY(require_ready(c));
+  if (!theta || !x_host || nsamples <= 0 || !pred) return fail(SMAML_EINVAL, "bad forward arguments");
+  for (int i = 0; i < nsamples; ++i)
+    if (!x_host[i] || !aligned16(x_host[i])) return fail(SMAML_EINVAL, "sample x pointers must be 16-B aligned");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  TRY(reserve(c, 1, nsamples));
+  set_work(c, 1, nsamples);
+  TRY(upload_xtab(c, s, x_host, nsamples));
+  TRY(run_forward(c, s, theta, 0, c->xtab));
+  Work w = c->w;
+  w.pred = pred;
+  launch_head_loss(s, c->d, w, theta, 0, c->po, nullptr, 0.f, false);
+  if (feats) {
+    const Dims& d = c->d;
+    const int64_t blk = (int64_t)d.N * d.Hc;
+    for (int si = 0; si < nsamples; ++si) {
+      // F is [T][M][Hc] with M = nsamples*N; feats is [s][T*N][Hc]
+      HIP_TRY(hipMemcpy2DAsync(feats + (int64_t)si * d.T * blk, blk * 4, c->w.F + (int64_t)si * blk,
+                               (int64_t)nsamples * blk * 4, blk * 4, d.T, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_set_tasks(smaml_ctx* c, int32_t ntasks, const float* const* features_host, const int32_t* t_total_host) {
+  if (!c || ntasks <= 0 || !features_host || !t_total_host) return fail(SMAML_EINVAL, "bad set_tasks arguments");
+  c->feats.assign(features_host, features_host + ntasks);
+  c->t_total.assign(t_total_host, t_total_host + ntasks);
+  for (int j = 0; j < ntasks; ++j) {
+    if (!c->feats[j] || !aligned16(c->feats[j])) return fail(SMAML_EINVAL, "feature streams must be 16-B aligned");
+    if (c->t_total[j] < c->d.T + c->d.Hf + 1) return fail(SMAML_EINVAL, "feature stream shorter than one sample");
+  }
+  return SMAML_OK;
+}
+
+int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t order, int32_t steps, int32_t batch,
+                    const int32_t* windows_host, float inner_lr, float max_norm, float query_scale,
+                    float* meta_grad, float* losses, float* norms, float* fast_out) {
+  TRY(require_ready(c));
+  if (c->feats.empty()) return fail(SMAML_ESTATE, "smaml_set_tasks not called");
+  if (!theta || steps < 0 || batch <= 0 || !windows_host) return fail(SMAML_EINVAL, "bad meta_step arguments");
+  if (order < 0 || order > 2) return fail(SMAML_EINVAL, "order must be 0, 1 or 2");
+  if (order == 2) return fail(SMAML_ENOTIMPL, "second-order meta-gradient not built yet");
+  if (order >= 1 && !meta_grad) return fail(SMAML_EINVAL, "meta_grad required for order >= 1");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  const Dims& d = c->d;
+  const int Z = (int)c->feats.size();
+  const int B = batch;
+  TRY(reserve(c, Z, B));
+  set_work(c, Z, B);
+  // sample window table for every step (support steps then the query batch)
+  const int64_t nptr = (int64_t)(steps + 1) * Z * B;
+  std::vector<const float*> ptrs(nptr);
+  const int max_w_off = d.T + d.Hf;  // last stream index read by a sample = w + T + Hf
+  for (int k = 0; k <= steps; ++k)
+    for (int z = 0; z < Z; ++z)
+      for (int b = 0; b < B; ++b) {
+        const int64_t i = ((int64_t)k * Z + z) * B + b;
+        const int wv = windows_host[i];
+        if (wv < 0 || wv + max_w_off >= c->t_total[z])
+          return fail(SMAML_EINVAL, "window start out of range for task " + std::to_string(z));
+        ptrs[i] = c->feats[z] + (int64_t)wv * d.N * d.Cin0;
+      }
+  TRY(upload_xtab(c, s, ptrs.data(), nptr));
+  if (!losses) {
+    const int64_t need = (int64_t)(steps + 1) * Z;
+    if (need > c->scratch_loss_cap) {
+      if (c->scratch_loss) HIP_TRY(hipFree(c->scratch_loss));
+      HIP_TRY(hipMalloc((void**)&c->scratch_loss, need * 4));
+      c->scratch_loss_cap = need;
+    }
+    losses = c->scratch_loss;
+  }
+  const int64_t P = c->po.P;
+  const float inv = 1.f / ((float)d.N * d.HfC * B);
+  launch_broadcast(s, theta, P, Z, c->fast);
+  const double head_fl = 2.0 * Z * c->w.M * d.HfC * d.H;
+  for (int k = 0; k < steps; ++k) {
+    const float* const* xt = c->xtab + (int64_t)k * Z * B;
+    TRY(run_forward(c, s, c->fast, P, xt));
+    TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
+    TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
+    TRY(run_backward(c, s, c->fast, P, c->grad));
+    TIMED(c, s, C_MISC, 0, launch_sqsum(s, c->grad, P, Z, c->w.sqpart));
+    TIMED(c, s, C_MISC, 0,
+          launch_clip_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
+                          norms ? norms + (int64_t)k * Z : nullptr, nullptr));
+  }
+  const float* const* xq = c->xtab + (int64_t)steps * Z * B;
+  TRY(run_forward(c, s, c->fast, P, xq));
+  TIMED(c, s, C_HEAD, head_fl,
+        launch_head_loss(s, d, c->w, c->fast, P, c->po, xq, 2.f * inv * query_scale, true));
+  TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)steps * Z));
+  if (order == 1) {
+    TRY(run_backward(c, s, c->fast, P, c->grad));
+    TIMED(c, s, C_MISC, 0, launch_sum_tasks(s, c->grad, P, Z, meta_grad));
+  }
+  if (fast_out) HIP_TRY(hipMemcpyAsync(fast_out, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_timing(smaml_ctx* c, int32_t enable) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  c->tm.on = enable != 0;
+  return SMAML_OK;
+}
+
+int smaml_timing_collect(smaml_ctx* c, double* ms, double* flops, int64_t* count, int32_t cap) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  TRY(ensure_device(c));
+  HIP_TRY(hipDeviceSynchronize());
+  for (auto& r : c->tm.recs) {
+    float e = 0.f;
+    HIP_TRY(hipEventElapsedTime(&e, r.a, r.b));
+    c->tm.ms[r.cat] += e;
+    c->tm.flops[r.cat] += r.flops;
+    c->tm.count[r.cat] += 1;
+    c->tm.pool.push_back(r.a);
+    c->tm.pool.push_back(r.b);
+  }
+  c->tm.recs.clear();
+  for (int i = 0; i < NCAT && i < cap; ++i) {
+    if (ms) ms[i] = c->tm.ms[i];
+    if (flops) flops[i] = c->tm.flops[i];
+    if (count) count[i] = c->tm.count[i];
+    c->tm.ms[i] = 0;
+    c->tm.flops[i] = 0;
+    c->tm.count[i] = 0;
+  }
+  return SMAML_OK;
+}
+
+int smaml_adamw_step(smaml_ctx* c, void* stream, float* theta, const float* grad, float* m, float* v, int64_t n,
+                     int32_t step, float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                     float* norm_out) {
+  if (!c || !theta || !grad || !m || !v || n <= 0 || step < 1) return fail(SMAML_EINVAL, "bad adamw arguments");
+  TRY(ensure_device(c));
+  TRY(reserve(c, 1, 1));
+  hipStream_t s = (hipStream_t)stream;
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  launch_adamw(s, theta, grad, m, v, n, c->w.sqpart + (int64_t)c->z_cap * SQB, lr, beta1, beta2, eps, weight_decay,
+               (float)(lr / bc1), (float)std::sqrt(bc2), max_norm, norm_out);
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,88 @@
+// Internal (C++) interface between the C-ABI driver (api.cpp) and the HIP kernels
+// (kernels.hip). Not part of the public boundary -- see include/smaml.h for that.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smaml {
+
+constexpr int ELLW = 8;        // ELL width of the normalised t=0 adjacency (max in-degree 6 + self)
+constexpr int MAX_LAYERS = 8;
+
+struct Dims {
+  int N;      // nodes per region (graph size)
+  int T;      // window (time steps)
+  int Cin0;   // input channels (24)
+  int Hc;     // GCN hidden channels (256)
+  int H;      // LSTM hidden (128)
+  int L;      // LSTM layers (4)
+  int Hf;     // forecast horizon (8)
+  int C;      // output channels (12)
+  int HfC;    // head width (96)
+};
+
+struct LayerOff {
+  int64_t wih, whh, bih, bhh;  // offsets into the flat trainable vector
+  int cin;
+};
+
+struct ParamOff {
+  LayerOff lay[MAX_LAYERS];
+  int64_t wo, bo;
+  int64_t P;  // padded flat size (stride between tasks' fast weights)
+  int64_t n_valid;
+};
+
+struct GcnOff {
+  int64_t w[4], b[4];
+  int cin[4];
+  int64_t total;
+};
+
+// Activations of one forward pass for Z tasks x B samples (M = B*N sequences per task).
+struct Work {
+  int Z, B, M;
+  float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
+  float* F;                // [Z][T][M][Hc] LSTM layer-0 input
+  float *Hs, *Cs, *Gs;     // [L][Z][T][M][H] / [L][Z][T][M][H] / [L][Z][T][M][4H]
+  float *dG, *dH, *dc;     // [Z][T][M][4H], [Z][T][M][H], [Z][M][H]
+  float *pred, *dpred;     // [Z][M][HfC]
+  float* wpart;            // split-K partial slabs
+  int64_t wpart_floats;
+  float* lpart;            // loss partials [Z][lblocks]
+  int lblocks;
+  double* sqpart;          // [Z][SQB]
+};
+
+constexpr int SQB = 64;  // blocks per task for squared-norm partials
+
+// ---- launchers (kernels.hip) ----
+void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
+                      const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
+                      const float* b, int cin, int cout, const int* ell_c, const float* ell_v, int rows_per_sample,
+                      int ell_rows);
+void launch_lstm_fwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          int64_t tstride, const LayerOff& lo);
+void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
+                      const ParamOff& po, const float* const* xtab, float dscale, bool want_loss);
+void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
+void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
+                    const ParamOff& po);
+void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          int64_t tstride, const LayerOff& lo);
+void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
+               const LayerOff& lo);
+void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
+                  int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
+                  int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
+                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2);
+void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part);
+void launch_clip_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, const double* part,
+                     float lr, float max_norm, float* norm_out, float* coef_out);
+void launch_sum_tasks(hipStream_t s, const float* g, int64_t P, int Z, float* out);
+void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float* out);
+void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
+                  float lr, float b1, float b2, float eps, float wd, float step_size, float bc2_sqrt,
+                  float max_norm, float* norm_out);
+
+}  // namespace smaml

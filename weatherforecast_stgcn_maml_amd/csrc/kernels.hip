@@ -1,0 +1,688 @@
+// HIP kernels for the STGCN-LSTM MAML hot path on gfx950 (MI355X).
+//
+// Reference semantics (file:line in Yalt8826/WeatherForecast_STGCN_MAML):
+//   k_gcn_layer        GCNConv x4 + ReLU      hybrid_model.py:60-78, model.py:23-26 (PyG 2.x
+//                      gcn_norm; F3: only rows t=0 see neighbours, rows t>=1 are x W^T + b)
+//   k_lstm_fwd_step    nn.LSTM cell, gates [i,f,g,o]   hybrid_model.py:42-49,93-102
+//   k_head_loss        Linear head + view/reshape + MSELoss (F4 row permutation)
+//                      hybrid_model.py:105-115, train_hybrid_maml_v5.py:119,133
+//   k_lstm_bwd_step    BPTT of the cell (loss.backward through LSTM)   train_hybrid_maml_v5.py:134
+//   k_wgrad            dW_ih | dW_hh | db  as a split-K fp32 MFMA GEMM over B*N*T rows
+//   k_clip_sgd         clip_grad_norm_(1.0) + SGD(lr)   train_hybrid_maml_v5.py:135-139
+//   k_adamw            clip + AdamW (outer)             train_hybrid_maml_v5.py:174-179,245-249
+//
+// Every GEMM-shaped contraction runs on v_mfma_f32_32x32x2_f32 (gemm_core.h). All
+// reductions are in a fixed order (no float atomics), so results are bitwise
+// reproducible run to run and across ranks.
+#include "gemm_core.h"
+#include "kernels.h"
+
+namespace smaml {
+
+using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-contiguous)
+using CfgGate = GemmCfg<128, 128, 4, 1, true, true>;  // LSTM forward: wave = 32 rows x 4 gates
+using CfgNN = GemmCfg<128, 128, 4, 1, true, false>;   // C = A . B   (B n-contiguous)
+using CfgTN = GemmCfg<128, 128, 2, 2, false, false>;  // C = A^T . B (split-K weight grads)
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ------------------------------------------------------------------------------------
+// Block-wide deterministic sum (fixed shuffle tree + fixed wave order).
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+  }
+  return s;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+  }
+  return s;
+}
+
+// ====================================================================================
+// GCN layer: out = relu( (A_hat X) W^T + b ), A_hat applied to the first N rows of every
+// sample (t = 0 block) via an ELL gather in the A-operand prologue (aggregate-then-
+// transform), identity elsewhere (F3).
+struct GcnA {
+  const float* const* tab;  // layer 1: per-sample window pointers into the feature stream
+  const float* buf;         // layers 2-4: [g][rows_per_sample][cin]
+  int64_t sstride;
+  const int* ec;
+  const float* ev;
+  int rps, ell_rows, cin, R;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    if (r >= R || k >= cin) return f4zero();
+    const int g = r / rps, q = r - g * rps;
+    const float* base = tab ? tab[g] : buf + (int64_t)g * sstride;
+    if (q < ell_rows) {
+      float4 s = f4zero();
+#pragma unroll
+      for (int e = 0; e < ELLW; ++e) {
+        const float wv = ev[q * ELLW + e];
+        if (wv != 0.f) s = fma4(wv, ld4(base + (int64_t)ec[q * ELLW + e] * cin + k), s);
+      }
+      return s;
+    }
+    return ld4(base + (int64_t)q * cin + k);
+  }
+};
+
+struct RowMajorKC {  // [rows][K] with K contiguous, zero outside [0,rows) x [0,K)
+  const float* p;
+  int rows, K;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    if (r >= rows || k >= K) return f4zero();
+    return ld4(p + (int64_t)r * K + k);
+  }
+};
+
+struct RowMajorMC {  // [K][cols] with cols contiguous (operand row index = col)
+  const float* p;
+  int64_t K;
+  int cols;
+  __device__ __forceinline__ float4 operator()(int64_t k, int c) const {
+    if (k >= K || c >= cols) return f4zero();
+    return ld4(p + k * cols + c);
+  }
+};
+
+__global__ __launch_bounds__(NT) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
+                                                  float* __restrict__ out, int cout, int remap, int relu,
+                                                  int T, int N, int B) {
+  __shared__ float smem[CfgNT::SMEM_FLOATS];
+  const int m0 = blockIdx.x * CfgNT::BM, n0 = blockIdx.y * CfgNT::BN;
+  Acc<CfgNT> acc;
+  acc.zero();
+  gemm_mainloop<CfgNT>(la, lb, m0, n0, 0, la.cin, acc, smem);
+  const int M = B * N;
+#pragma unroll
+  for (int i = 0; i < CfgNT::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < CfgNT::WTN; ++j) {
+      const int c = n0 + acc_col<CfgNT>(j);
+      if (c >= cout) continue;
+      const float bc = bias[c];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<CfgNT>(i, r);
+        if (row >= la.R) continue;
+        float v = acc.v[i][j][r] + bc;
+        if (relu) v = fmaxf(v, 0.f);
+        int64_t orow = row;
+        if (remap) {  // [g][t*N+n] -> [z][t][s*N+n]
+          const int g = row / la.rps, q = row - g * la.rps;
+          const int z = g / B, s = g - z * B;
+          const int t = q / N, n = q - t * N;
+          orow = ((int64_t)z * T + t) * M + (int64_t)s * N + n;
+        }
+        out[orow * cout + c] = v;
+      }
+    }
+}
+
+void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
+                      const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
+                      const float* b, int cin, int cout, const int* ell_c, const float* ell_v,
+                      int rows_per_sample, int ell_rows) {
+  (void)layer;
+  GcnA la;
+  la.tab = xtab;
+  la.buf = src;
+  la.sstride = (int64_t)rows_per_sample * cin;
+  la.ec = ell_c;
+  la.ev = ell_v;
+  la.rps = rows_per_sample;
+  la.ell_rows = ell_rows;
+  la.cin = cin;
+  la.R = Zb * rows_per_sample;
+  RowMajorKC lb{W, cout, cin};
+  dim3 grid((la.R + CfgNT::BM - 1) / CfgNT::BM, (cout + CfgNT::BN - 1) / CfgNT::BN);
+  k_gcn_layer<<<grid, NT, 0, s>>>(la, lb, b, dst, cout, remap_lstm ? 1 : 0, relu ? 1 : 0, d.T, d.N,
+                                  B);
+}
+
+// ====================================================================================
+// LSTM forward step (layer l, time t) for all tasks z (blockIdx.z):
+//   pre[m, g*H+j] = [x_t | h_{t-1}][m] . [W_ih | W_hh][g*H+j] + b_ih + b_hh
+// Column tile = 32 hidden units x 4 gates, so each lane holds i,f,g,o of the same
+// (row, unit) in the same accumulator register and the cell update is in-register.
+struct LstmFwdA {
+  const float* X;   // layer input at time t: [M][cin]
+  const float* Hp;  // h_{t-1}: [M][H] (nullptr at t = 0)
+  int M, cin, H;
+  __device__ __forceinline__ float4 operator()(int m, int k) const {
+    if (m >= M) return f4zero();
+    if (k < cin) return ld4(X + (int64_t)m * cin + k);
+    k -= cin;
+    if (!Hp || k >= H) return f4zero();
+    return ld4(Hp + (int64_t)m * H + k);
+  }
+};
+
+struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + ug*32 + jj
+  const float* Wih;
+  const float* Whh;
+  int cin, H;
+  __device__ __forceinline__ float4 operator()(int n, int k) const {
+    const int ug = n >> 7, rem = n & 127, g = rem >> 5, j = ug * 32 + (rem & 31);
+    if (j >= H) return f4zero();
+    const int row = g * H + j;
+    if (k < cin) return ld4(Wih + (int64_t)row * cin + k);
+    k -= cin;
+    if (k >= H) return f4zero();
+    return ld4(Whh + (int64_t)row * H + k);
+  }
+};
+
+__global__ __launch_bounds__(NT) void k_lstm_fwd_step(const float* __restrict__ X, float* __restrict__ Hs,
+                                                      float* __restrict__ Cs, float* __restrict__ Gs,
+                                                      const float* __restrict__ theta, int64_t tstride,
+                                                      LayerOff lo, int T, int M, int H, int t) {
+  __shared__ float smem[CfgGate::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const float* th = theta + (int64_t)z * tstride;
+  const int cin = lo.cin;
+  LstmFwdA la;
+  la.X = X + ((int64_t)z * T + t) * M * cin;
+  la.Hp = t > 0 ? Hs + ((int64_t)z * T + t - 1) * M * H : nullptr;
+  la.M = M;
+  la.cin = cin;
+  la.H = H;
+  LstmFwdB lb{th + lo.wih, th + lo.whh, cin, H};
+  const int m0 = blockIdx.x * CfgGate::BM, n0 = blockIdx.y * CfgGate::BN;
+  Acc<CfgGate> acc;
+  acc.zero();
+  gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+
+  const int j = blockIdx.y * 32 + (threadIdx.x & 31);
+  if (j >= H) return;
+  const float* bih = th + lo.bih;
+  const float* bhh = th + lo.bhh;
+  float bsum[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bsum[g] = bih[g * H + j] + bhh[g * H + j];
+  const int64_t base_t = ((int64_t)z * T + t) * M;
+  const float* Cp = t > 0 ? Cs + ((int64_t)z * T + t - 1) * M * H : nullptr;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + acc_row<CfgGate>(0, r);
+    if (m >= M) continue;
+    const float pi = acc.v[0][0][r] + bsum[0];
+    const float pf = acc.v[0][1][r] + bsum[1];
+    const float pg = acc.v[0][2][r] + bsum[2];
+    const float po = acc.v[0][3][r] + bsum[3];
+    const float gi = sigmoidf_(pi), gf = sigmoidf_(pf), gg = tanhf(pg), go = sigmoidf_(po);
+    const float cp = Cp ? Cp[(int64_t)m * H + j] : 0.f;
+    const float c = gf * cp + gi * gg;
+    const float h = go * tanhf(c);
+    float* grow = Gs + (base_t + m) * (4 * H);
+    grow[j] = gi;
+    grow[H + j] = gf;
+    grow[2 * H + j] = gg;
+    grow[3 * H + j] = go;
+    Cs[(base_t + m) * H + j] = c;
+    Hs[(base_t + m) * H + j] = h;
+  }
+}
+
+void launch_lstm_fwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          int64_t tstride, const LayerOff& lo) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  const float* X = (l == 0) ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
+  float* Hs = w.Hs + (int64_t)l * lsz;
+  float* Cs = w.Cs + (int64_t)l * lsz;
+  float* Gs = w.Gs + (int64_t)l * lsz * 4;
+  dim3 grid((w.M + CfgGate::BM - 1) / CfgGate::BM, (d.H + 31) / 32, w.Z);
+  k_lstm_fwd_step<<<grid, NT, 0, s>>>(X, Hs, Cs, Gs, theta, tstride, lo, d.T, w.M, d.H, t);
+}
+
+// ====================================================================================
+// Head + loss: pred[m, c'] = h_T[m] . Wo[c'] + bo[c'];  loss = mean (pred - y)^2 with the
+// F4 pairing: pred row (n*Hf + h) of sample s is compared with target row (h'*N + n')
+// of the SAME flat row index r = n*Hf + h  (h' = r / N, n' = r % N).
+__global__ __launch_bounds__(NT) void k_head_loss(const float* __restrict__ hT_base, int64_t hT_zstride,
+                                                  const float* __restrict__ theta, int64_t tstride, int64_t wo,
+                                                  int64_t bo, const float* const* __restrict__ xtab,
+                                                  float* __restrict__ pred, float* __restrict__ dpred,
+                                                  float* __restrict__ lpart, int lblocks, int M, int H,
+                                                  int HfC, int N, int Hf, int C, int T, int cin0, int B,
+                                                  float dscale) {
+  __shared__ float smem[CfgNT::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const float* th = theta + (int64_t)z * tstride;
+  RowMajorKC la{hT_base + (int64_t)z * hT_zstride, M, H};
+  RowMajorKC lb{th + wo, HfC, H};
+  const int m0 = blockIdx.x * CfgNT::BM;
+  Acc<CfgNT> acc;
+  acc.zero();
+  gemm_mainloop<CfgNT>(la, lb, m0, 0, 0, H, acc, smem);
+  float lsum = 0.f;
+#pragma unroll
+  for (int i = 0; i < CfgNT::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < CfgNT::WTN; ++j) {
+      const int cc = acc_col<CfgNT>(j);
+      if (cc >= HfC) continue;
+      const float bc = th[bo + cc];
+      const int h = cc / C, c = cc - h * C;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + acc_row<CfgNT>(i, r);
+        if (m >= M) continue;
+        const float p = acc.v[i][j][r] + bc;
+        const int64_t o = ((int64_t)z * M + m) * HfC + cc;
+        if (pred) pred[o] = p;
+        if (xtab) {
+          const int s = m / N, n = m - s * N;
+          const int rr = n * Hf + h;
+          const int hp = rr / N, np = rr - hp * N;
+          const float* xs = xtab[z * B + s];
+          const float y = xs[((int64_t)(T + 1 + hp) * N + np) * cin0 + c];
+          const float df = p - y;
+          lsum = fmaf(df, df, lsum);
+          if (dpred) dpred[o] = dscale * df;
+        }
+      }
+    }
+  if (lpart) {
+    const float s = block_sum(lsum, smem);
+    if (threadIdx.x == 0) lpart[(int64_t)z * lblocks + blockIdx.x] = s;
+  }
+}
+
+void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
+                      const ParamOff& po, const float* const* xtab, float dscale, bool want_loss) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
+  const float* hT = top + (int64_t)(d.T - 1) * w.M * d.H;  // z stride T*M*H
+  dim3 grid((w.M + CfgNT::BM - 1) / CfgNT::BM, 1, w.Z);
+  k_head_loss<<<grid, NT, 0, s>>>(hT, (int64_t)d.T * w.M * d.H, theta, tstride, po.wo, po.bo,
+                                  want_loss ? xtab : nullptr, w.pred, want_loss ? w.dpred : nullptr,
+                                  want_loss ? w.lpart : nullptr, w.lblocks, w.M, d.H, d.HfC, d.N, d.Hf,
+                                  d.C, d.T, d.Cin0, w.B, dscale);
+}
+
+__global__ void k_loss_final(const float* __restrict__ lpart, int lblocks, float inv_count,
+                             float* __restrict__ out) {
+  __shared__ float red[NT / 64];
+  const int z = blockIdx.x;
+  float v = 0.f;
+  for (int i = threadIdx.x; i < lblocks; i += NT) v += lpart[(int64_t)z * lblocks + i];
+  const float s = block_sum(v, red);
+  if (threadIdx.x == 0) out[z] = s * inv_count;
+}
+
+void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out) {
+  k_loss_final<<<w.Z, NT, 0, s>>>(w.lpart, w.lblocks, inv_count, out);
+}
+
+// ====================================================================================
+// Generic C = A . B (A k-contiguous, B n-contiguous) with plain store; used for
+//   dh_T = dpred . Wo      (head backward into the top layer's dH at t = T-1)
+//   dX_l = dG_l . W_ih_l   (input grads of LSTM layer l > 0 over all T*M rows)
+__global__ __launch_bounds__(NT) void k_gemm_nn(const float* __restrict__ A, int64_t a_zstride, int rows,
+                                                int K, const float* __restrict__ theta, int64_t tstride,
+                                                int64_t woff, int ncols, float* __restrict__ out,
+                                                int64_t o_zstride) {
+  __shared__ float smem[CfgNN::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  RowMajorKC la{A + (int64_t)z * a_zstride, rows, K};
+  RowMajorMC lb{theta + (int64_t)z * tstride + woff, K, ncols};
+  const int m0 = blockIdx.x * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
+  Acc<CfgNN> acc;
+  acc.zero();
+  gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, K, acc, smem);
+  float* o = out + (int64_t)z * o_zstride;
+#pragma unroll
+  for (int j = 0; j < CfgNN::WTN; ++j) {
+    const int c = n0 + acc_col<CfgNN>(j);
+    if (c >= ncols) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + acc_row<CfgNN>(0, r);
+      if (m < rows) o[(int64_t)m * ncols + c] = acc.v[0][j][r];
+    }
+  }
+}
+
+void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
+                    const ParamOff& po) {
+  // dH (top layer) holds zeros for t < T-1 (memset by the driver); write t = T-1.
+  float* out = w.dH + (int64_t)(d.T - 1) * w.M * d.H;
+  dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
+  k_gemm_nn<<<grid, NT, 0, s>>>(w.dpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, tstride, po.wo, d.H,
+                                out, (int64_t)d.T * w.M * d.H);
+}
+
+void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
+               const LayerOff& lo) {
+  const int rows = d.T * w.M;
+  dim3 grid((rows + CfgNN::BM - 1) / CfgNN::BM, (lo.cin + CfgNN::BN - 1) / CfgNN::BN, w.Z);
+  k_gemm_nn<<<grid, NT, 0, s>>>(w.dG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, tstride, lo.wih,
+                                lo.cin, w.dH, (int64_t)rows * lo.cin);
+}
+
+// ====================================================================================
+// LSTM backward step (layer l, time t):
+//   dh = dG_{t+1} . W_hh  (+ dH_above[t])          [fp32 MFMA, K = 4H]
+//   dc = dc_carry + dh * o * (1 - tanh(c_t)^2)
+//   dG_t = [dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tanh(c_t)*o(1-o)]
+//   dc_carry = dc * f
+__global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, const float* __restrict__ dH,
+                                                      float* __restrict__ dc, const float* __restrict__ Gs,
+                                                      const float* __restrict__ Cs,
+                                                      const float* __restrict__ theta, int64_t tstride,
+                                                      LayerOff lo, int T, int M, int H, int t) {
+  __shared__ float smem[CfgNN::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const int G4 = 4 * H;
+  const int m0 = blockIdx.x * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
+  Acc<CfgNN> acc;
+  acc.zero();
+  if (t + 1 < T) {
+    RowMajorKC la{dG + ((int64_t)z * T + t + 1) * M * G4, M, G4};
+    RowMajorMC lb{theta + (int64_t)z * tstride + lo.whh, G4, H};
+    gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, G4, acc, smem);
+  }
+  const int64_t bt = ((int64_t)z * T + t) * M;
+  const float* Cprev = t > 0 ? Cs + ((int64_t)z * T + t - 1) * M * H : nullptr;
+  float* dcz = dc + (int64_t)z * M * H;
+  const bool first = (t == T - 1);
+#pragma unroll
+  for (int jj = 0; jj < CfgNN::WTN; ++jj) {
+    const int j = n0 + acc_col<CfgNN>(jj);
+    if (j >= H) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + acc_row<CfgNN>(0, r);
+      if (m >= M) continue;
+      const int64_t row = bt + m;
+      const float dh = acc.v[0][jj][r] + dH[row * H + j];
+      const float* g = Gs + row * G4;
+      const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
+      const float c = Cs[row * H + j];
+      const float tc = tanhf(c);
+      const float cp = Cprev ? Cprev[(int64_t)m * H + j] : 0.f;
+      const float dcin = first ? 0.f : dcz[(int64_t)m * H + j];
+      const float dct = dcin + dh * go * (1.f - tc * tc);
+      float* dg = dG + row * G4;
+      dg[j] = dct * gg * gi * (1.f - gi);
+      dg[H + j] = dct * cp * gf * (1.f - gf);
+      dg[2 * H + j] = dct * gi * (1.f - gg * gg);
+      dg[3 * H + j] = dh * tc * go * (1.f - go);
+      dcz[(int64_t)m * H + j] = dct * gf;
+    }
+  }
+}
+
+void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          int64_t tstride, const LayerOff& lo) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
+  k_lstm_bwd_step<<<grid, NT, 0, s>>>(w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz,
+                                      theta, tstride, lo, d.T, w.M, d.H, t);
+}
+
+// ====================================================================================
+// Weight gradients, split-K:  part[z][split][i][j] = sum_k A[k][i] * Bcat[k][j]
+//   Bcat[k] = [ B1[k][0..c1) | (k >= Mshift ? B2[k - Mshift][0..c2) : 0) | 1 ]
+// (the trailing column of ones is produced as column sums of A in tile column 0:
+//  the bias gradient). For LSTM layer l: A = dG [T*M][4H], B1 = x_l [T*M][cin],
+//  B2 = h_l (shifted one time block: h_{t-1}); for the head: A = dpred, B1 = h_T.
+struct WgB {
+  const float* B1;
+  const float* B2;
+  int c1, c2;
+  int64_t K, Mshift;
+  __device__ __forceinline__ float4 operator()(int64_t k, int j) const {
+    if (k >= K) return f4zero();
+    if (j < c1) return ld4(B1 + k * c1 + j);
+    j -= c1;
+    if (j >= c2 || k < Mshift) return f4zero();
+    return ld4(B2 + (k - Mshift) * c2 + j);
+  }
+};
+
+struct ColSumHook {
+  float* acc;
+  __device__ __forceinline__ void operator()(const float* as, int) const {
+    if (threadIdx.x < CfgTN::BM) {
+      float s = *acc;
+#pragma unroll 8
+      for (int kk = 0; kk < BK; ++kk) s += as[kk * CfgTN::LDA + threadIdx.x];
+      *acc = s;
+    }
+  }
+};
+
+__global__ __launch_bounds__(NT) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
+                                              WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
+                                              int ntn, float* __restrict__ part, int ldp) {
+  __shared__ float smem[CfgTN::SMEM_FLOATS];
+  const int z = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
+  const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+  RowMajorMC la{A + (int64_t)z * a_zstride, lb.K, Mrows};
+  WgB b = lb;
+  b.B1 += (int64_t)z * b1_zstride;
+  if (b.B2) b.B2 += (int64_t)z * b2_zstride;
+  const int64_t kbeg = (int64_t)split * kchunk;
+  const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
+  const int m0 = tm * CfgTN::BM, n0 = tn * CfgTN::BN;
+  Acc<CfgTN> acc;
+  acc.zero();
+  float bsum = 0.f;
+  // k indices exceed int range only in the loaders (int64 there); the mainloop
+  // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
+  if (tn == 0) {
+    ColSumHook hook{&bsum};
+    gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+  } else {
+    gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
+  }
+  const int ncols = lb.c1 + lb.c2;
+  float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
+#pragma unroll
+  for (int i = 0; i < CfgTN::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < CfgTN::WTN; ++j) {
+      const int c = n0 + acc_col<CfgTN>(j);
+      if (c >= ncols) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<CfgTN>(i, r);
+        if (row < Mrows) P[(int64_t)row * ldp + c] = acc.v[i][j][r];
+      }
+    }
+  if (tn == 0 && threadIdx.x < CfgTN::BM) {
+    const int row = m0 + threadIdx.x;
+    if (row < Mrows) P[(int64_t)row * ldp + ncols] = bsum;
+  }
+}
+
+__global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int Mrows, int ldp, int c1, int c2,
+                               float* __restrict__ grad, int64_t P, int64_t off_w1, int64_t off_w2,
+                               int64_t off_b1, int64_t off_b2) {
+  const int z = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)Mrows * ldp;
+  if (e >= total) return;
+  const float* p = part + (int64_t)z * nsplit * total + e;
+  float v = 0.f;
+  for (int s = 0; s < nsplit; ++s) v += p[(int64_t)s * total];
+  const int i = (int)(e / ldp), j = (int)(e - (int64_t)i * ldp);
+  float* g = grad + (int64_t)z * P;
+  if (j < c1) {
+    g[off_w1 + (int64_t)i * c1 + j] = v;
+  } else if (j < c1 + c2) {
+    g[off_w2 + (int64_t)i * c2 + (j - c1)] = v;
+  } else {
+    g[off_b1 + i] = v;
+    if (off_b2 >= 0) g[off_b2 + i] = v;
+  }
+}
+
+void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
+                  int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
+                  int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
+                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2) {
+  (void)d;
+  const int ncols = c1 + c2;
+  const int ldp = ncols + 1;
+  const int ntm = (Mrows + CfgTN::BM - 1) / CfgTN::BM;
+  const int ntn = (ncols + CfgTN::BN - 1) / CfgTN::BN;
+  const int64_t ktiles = (K + BK - 1) / BK;
+  // aim for ~2048 workgroups, at least 8 K-tiles per split, bounded by the slab buffer
+  int64_t nsplit = 2048 / ((int64_t)ntm * ntn * w.Z);
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > ktiles / 8) nsplit = ktiles / 8 > 0 ? ktiles / 8 : 1;
+  const int64_t per_split = (int64_t)w.Z * Mrows * ldp;
+  if (nsplit * per_split > w.wpart_floats) nsplit = w.wpart_floats / per_split;
+  if (nsplit < 1) nsplit = 1;
+  const int64_t kchunk = ((ktiles + nsplit - 1) / nsplit) * BK;
+  nsplit = (K + kchunk - 1) / kchunk;
+  WgB lb;
+  lb.B1 = B1;
+  lb.B2 = B2;
+  lb.c1 = c1;
+  lb.c2 = c2;
+  lb.K = K;
+  lb.Mshift = Mshift;
+  dim3 grid(ntm * ntn, (unsigned)nsplit, w.Z);
+  k_wgrad<<<grid, NT, 0, s>>>(A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, w.wpart, ldp);
+  const int64_t total = (int64_t)Mrows * ldp;
+  dim3 g2((unsigned)((total + 255) / 256), w.Z);
+  k_wgrad_reduce<<<g2, 256, 0, s>>>(w.wpart, (int)nsplit, Mrows, ldp, c1, c2, grad, P, off_w1, off_w2, off_b1,
+                                    off_b2);
+}
+
+// ====================================================================================
+// clip_grad_norm_ + SGD, per task z. Squared norm accumulated in fp64, fixed order.
+__global__ void k_sqsum(const float* __restrict__ g, int64_t P, double* __restrict__ part) {
+  __shared__ double red[NT / 64];
+  const int z = blockIdx.y;
+  const float* gz = g + (int64_t)z * P;
+  const int64_t per = (P + SQB - 1) / SQB;
+  const int64_t b = (int64_t)blockIdx.x * per, e = b + per < P ? b + per : P;
+  double acc = 0.0;
+  for (int64_t i = b + threadIdx.x; i < e; i += NT) {
+    const double v = gz[i];
+    acc += v * v;
+  }
+  const double s = block_sum_d(acc, red);
+  if (threadIdx.x == 0) part[(int64_t)z * SQB + blockIdx.x] = s;
+}
+
+void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part) {
+  k_sqsum<<<dim3(SQB, Z), NT, 0, s>>>(g, P, part);
+}
+
+__device__ __forceinline__ float clip_coef_from(const double* part, float max_norm, float* total_out) {
+  double t = 0.0;
+  for (int i = 0; i < SQB; ++i) t += part[i];
+  const float total = (float)sqrt(t);
+  if (total_out) *total_out = total;
+  const float coef = max_norm / (total + 1e-6f);
+  return coef < 1.f ? coef : 1.f;
+}
+
+__global__ void k_clip_sgd(float* __restrict__ theta, const float* __restrict__ g, int64_t P,
+                           const double* __restrict__ part, float lr, float max_norm, float* norm_out,
+                           float* coef_out) {
+  const int z = blockIdx.y;
+  float total;
+  const float coef = clip_coef_from(part + (int64_t)z * SQB, max_norm, &total);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (norm_out) norm_out[z] = total;
+    if (coef_out) coef_out[z] = coef;
+  }
+  float* tz = theta + (int64_t)z * P;
+  const float* gz = g + (int64_t)z * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gc = gz[i] * coef;
+    tz[i] = fmaf(-lr, gc, tz[i]);
+  }
+}
+
+void launch_clip_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, const double* part,
+                     float lr, float max_norm, float* norm_out, float* coef_out) {
+  int nb = (int)((P + 4 * NT - 1) / (4 * NT));
+  if (nb > 1024) nb = 1024;
+  k_clip_sgd<<<dim3(nb, Z), NT, 0, s>>>(theta, g, P, part, lr, max_norm, norm_out, coef_out);
+}
+
+__global__ void k_sum_tasks(const float* __restrict__ g, int64_t P, int Z, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < Z; ++z) v += g[(int64_t)z * P + i];
+    out[i] = v;
+  }
+}
+
+void launch_sum_tasks(hipStream_t s, const float* g, int64_t P, int Z, float* out) {
+  int nb = (int)((P + NT - 1) / NT);
+  if (nb > 2048) nb = 2048;
+  k_sum_tasks<<<nb, NT, 0, s>>>(g, P, Z, out);
+}
+
+__global__ void k_broadcast(const float* __restrict__ theta, int64_t P, float* __restrict__ out) {
+  const int z = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    out[(int64_t)z * P + i] = theta[i];
+}
+
+void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float* out) {
+  int nb = (int)((P + NT - 1) / NT);
+  if (nb > 1024) nb = 1024;
+  k_broadcast<<<dim3(nb, Z), NT, 0, s>>>(theta, P, out);
+}
+
+// ====================================================================================
+// Outer step: clip_grad_norm_(max_norm) on the (all-reduced) meta-gradient, then
+// torch.optim.AdamW (decoupled weight decay, lerp first moment).
+__global__ void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, int64_t n, const double* __restrict__ part, float lr, float b1,
+                        float b2, float eps, float wd, float step, float bc2_sqrt, float max_norm,
+                        float* norm_out) {
+  float total;
+  const float coef = clip_coef_from(part, max_norm, &total);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) *norm_out = total;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
+                  float lr, float b1, float b2, float eps, float wd, float step_size, float bc2_sqrt,
+                  float max_norm, float* norm_out) {
+  k_sqsum<<<dim3(SQB, 1), NT, 0, s>>>(g, n, part);
+  int nb = (int)((n + NT - 1) / NT);
+  if (nb > 2048) nb = 2048;
+  k_adamw<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr, b1, b2, eps, wd, step_size, bc2_sqrt, max_norm, norm_out);
+}
+
+}  // namespace smaml

@@ -1,0 +1,152 @@
+"""Drop-in for the reference ``hybrid_model.py`` (``HybridSTGCN_LSTM``).
+
+Constructor signature, attributes (``base_stgcn``, ``lstm``, ``output_layer``,
+``dropout``, ``forecast_horizon``, ``out_channels``, ``lstm_hidden_size``), methods
+(``extract_base_features``, ``forward``, ``get_trainable_parameters``,
+``freeze_base_model``, ``unfreeze_base_model``) and state_dict keys follow
+``hybrid_model.py:6-134``. ``forward`` runs the whole STGCN-LSTM forward in libsmaml.so:
+GCN x4 (fp32 MFMA, F3 semantics), the 4-layer LSTM batched over nodes (the reference's
+per-node loop, F6, is one batched recurrence here), head. No CPU fallback.
+
+Training does not go through torch autograd: use ``weatherforecast_stgcn_maml_amd.maml``
+(meta-steps run entirely inside the library).
+"""
+from __future__ import annotations
+
+import math
+import warnings
+
+import torch
+import torch.nn as nn
+
+from . import _capi, params
+from .config import ModelDims
+from .model import _context, _set_graph
+
+
+class LSTMParams(nn.Module):
+    """Parameter container with ``nn.LSTM``'s names, shapes and init
+    (``weight_ih_l{k}`` [4H, in], ``weight_hh_l{k}`` [4H, H], ``bias_ih_l{k}``,
+    ``bias_hh_l{k}``; U(+-1/sqrt(H))). The recurrence itself runs in the HIP library."""
+
+    def __init__(self, input_size, hidden_size, num_layers=1, batch_first=True, dropout=0.0,
+                 bidirectional=False):
+        super().__init__()
+        if bidirectional:
+            raise ValueError("bidirectional LSTM is not part of the reference path")
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.num_layers = num_layers
+        self.batch_first = batch_first
+        self.dropout = dropout
+        self.bidirectional = False
+        G = 4 * hidden_size
+        for l in range(num_layers):
+            cin = input_size if l == 0 else hidden_size
+            self.register_parameter(f"weight_ih_l{l}", nn.Parameter(torch.empty(G, cin)))
+            self.register_parameter(f"weight_hh_l{l}", nn.Parameter(torch.empty(G, hidden_size)))
+            self.register_parameter(f"bias_ih_l{l}", nn.Parameter(torch.empty(G)))
+            self.register_parameter(f"bias_hh_l{l}", nn.Parameter(torch.empty(G)))
+        a = 1.0 / math.sqrt(hidden_size)
+        for p in self.parameters():
+            nn.init.uniform_(p, -a, a)
+
+    def flatten_parameters(self):
+        """No-op (called at train_hybrid_maml_v5.py:212, adapt_hybrid_v5.py:125)."""
+
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("LSTMParams holds weights; HybridSTGCN_LSTM.forward runs the recurrence")
+
+
+class HybridSTGCN_LSTM(nn.Module):
+    def __init__(self, base_stgcn, lstm_hidden_size=64, lstm_num_layers=2, lstm_dropout=0.2,
+                 out_channels=12, forecast_horizon=8, freeze_base=True):
+        super().__init__()
+        self.forecast_horizon = forecast_horizon
+        self.out_channels = out_channels
+        self.lstm_hidden_size = lstm_hidden_size
+        self.base_stgcn = base_stgcn
+        if freeze_base:
+            for p in self.base_stgcn.parameters():
+                p.requires_grad = False
+        base_hidden_channels = self.base_stgcn.conv1.out_channels
+        self.lstm = LSTMParams(input_size=base_hidden_channels, hidden_size=lstm_hidden_size,
+                               num_layers=lstm_num_layers, batch_first=True,
+                               dropout=lstm_dropout if lstm_num_layers > 1 else 0.0)
+        self.output_layer = nn.Linear(lstm_hidden_size, out_channels * forecast_horizon)
+        self.dropout = nn.Dropout(lstm_dropout)
+
+    # ------------------------------------------------------------------ helpers
+    def dims(self, num_nodes: int) -> ModelDims:
+        b = self.base_stgcn
+        return ModelDims(num_nodes=num_nodes, window_size=b.window_size,
+                         input_channels=b.conv1.in_channels, hidden_channels=b.conv1.out_channels,
+                         lstm_hidden_size=self.lstm_hidden_size,
+                         lstm_num_layers=self.lstm.num_layers,
+                         forecast_horizon=self.forecast_horizon, output_channels=self.out_channels)
+
+    def named_trainable(self):
+        sd = {}
+        for n, p in self.lstm.named_parameters():
+            sd["lstm." + n] = p.detach()
+        sd["output_layer.weight"] = self.output_layer.weight.detach()
+        sd["output_layer.bias"] = self.output_layer.bias.detach()
+        return sd
+
+    def named_gcn(self):
+        b = self.base_stgcn
+        out = {}
+        for k in range(1, 5):
+            conv = getattr(b, f"conv{k}")
+            out[f"base_stgcn.conv{k}.bias"] = conv.bias.detach()
+            out[f"base_stgcn.conv{k}.lin.weight"] = conv.lin.weight.detach()
+        return out
+
+    def _prepare(self, x, edge_index):
+        if x.device.type != "cuda":
+            raise _capi.SmamlError(-1, "HybridSTGCN_LSTM.forward runs on a HIP device only")
+        if self.training and (self.dropout.p > 0 or self.base_stgcn.dropout_rate > 0):
+            warnings.warn("the HIP path applies no dropout; build the model with dropout 0 "
+                          "for train-mode parity (SURVEY F7)", stacklevel=3)
+        T = self.base_stgcn.window_size
+        if x.shape[0] % T:
+            raise ValueError(f"x has {x.shape[0]} rows, not a multiple of window_size={T}")
+        dims = self.dims(x.shape[0] // T)
+        ctx = _context(dims, x.device)
+        _set_graph(ctx, edge_index)
+        gflat = params.pack(self.named_gcn(), dims, which=1, device=x.device)
+        ctx.set_gcn_params(gflat)
+        theta = params.pack(self.named_trainable(), dims, which=0, device=x.device)
+        return ctx, dims, theta
+
+    # ------------------------------------------------------------------ module API
+    def extract_base_features(self, x, edge_index):
+        """hybrid_model.py:60-78 -> [T*N, hidden_channels]."""
+        ctx, dims, theta = self._prepare(x, edge_index)
+        x = x.contiguous().float()
+        pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
+        feats = torch.empty(x.shape[0], dims.hidden_channels, device=x.device)
+        ctx.forward(_capi.stream_ptr(torch), theta, [x], pred, feats)
+        return feats
+
+    def forward(self, x, edge_index):
+        """hybrid_model.py:80-117 -> [N*forecast_horizon, out_channels] (rows n*Hf + h)."""
+        ctx, dims, theta = self._prepare(x, edge_index)
+        x = x.contiguous().float()
+        pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
+        ctx.forward(_capi.stream_ptr(torch), theta, [x], pred)
+        return pred
+
+    def get_trainable_parameters(self):
+        trainable = []
+        trainable.extend(self.lstm.parameters())
+        trainable.extend(self.output_layer.parameters())
+        return trainable
+
+    def freeze_base_model(self):
+        for p in self.base_stgcn.parameters():
+            p.requires_grad = False
+
+    def unfreeze_base_model(self):
+        for p in self.base_stgcn.parameters():
+            p.requires_grad = True

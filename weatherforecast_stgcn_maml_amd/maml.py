@@ -1,0 +1,127 @@
+"""MAML driver over libsmaml.so (replaces train_hybrid_maml_v5.py:110-184's hot loop).
+
+One ``MetaLearner.meta_step()`` = for every task: K inner SGD steps of B samples
+(``inner_loop_v4``, train_hybrid_maml_v5.py:110-141: MSE, backward, clip_grad_norm_(1.0),
+SGD lr 0.01), then one B-sample query batch; the meta-gradient (order 1 = first-order,
+order 0 = reference semantics where the outer update is a no-op) is summed
+over tasks, all-reduced across ranks (RCCL via torch.distributed, one flat buffer),
+clipped and applied with AdamW (train_hybrid_maml_v5.py:174-179,245-249) identically
+on every rank. The inner loop never returns to Python.
+
+Semantic note (F10): the reference steps its (no-op) outer optimiser every
+GRAD_ACCUMULATION_STEPS=2 tasks; here there is one outer step per meta-batch.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _capi, params, synth
+from .config import MamlConfig, ModelDims
+
+
+def shard_tasks(n_tasks: int, rank: int, world: int) -> List[int]:
+    """Round-robin task -> rank assignment (15 tasks on 8 ranks: {2,2,2,2,2,2,2,1})."""
+    return [j for j in range(n_tasks) if j % world == rank]
+
+
+def window_table(cfg: MamlConfig, n_tasks: int, support: Optional[int] = None,
+                 query_start: Optional[int] = None) -> np.ndarray:
+    """int32 [(K+1)][tasks][B]: support step k uses samples (k*B + b) mod S (with B=1,
+    S=15 this is the reference's 6 epochs x first 15 support samples, :124-127); the
+    query batch uses samples S .. S+B-1 (query_ds[0] when B=1, :162-164)."""
+    K, B = cfg.inner_steps, cfg.batch
+    S = support or cfg.support_samples or K * B
+    q0 = S if query_start is None else query_start
+    w = np.empty((K + 1, n_tasks, B), np.int32)
+    for k in range(K):
+        w[k] = ((k * B + np.arange(B)) % S)[None, :]
+    w[K] = (q0 + np.arange(B))[None, :]
+    return w
+
+
+def stream_len_for(cfg: MamlConfig, dims: ModelDims, support: Optional[int] = None) -> int:
+    S = support or cfg.support_samples or cfg.inner_steps * cfg.batch
+    return synth.t_total_for(S + cfg.batch, dims.window_size, dims.forecast_horizon)
+
+
+@dataclass
+class StepResult:
+    losses: torch.Tensor        # [(K+1), tasks] (device); last row = query MSE
+    norms: torch.Tensor         # [K, tasks] pre-clip inner grad norms
+    meta_loss: float            # sum_tasks query_mse * query_loss_scale (all ranks)
+    meta_grad_norm: Optional[float]
+
+
+class MetaLearner:
+    """Holds theta (flat trainable vector), AdamW state and the tasks of this rank."""
+
+    def __init__(self, dims: ModelDims, cfg: MamlConfig, gcn_params: dict, theta: dict,
+                 edge_index: np.ndarray, device=None, process_group=None):
+        self.dims = dims
+        self.cfg = cfg
+        self.device = torch.device(device or "cuda")
+        self.ctx = _capi.Context(dims, self.device.index or 0)
+        self.ctx.set_graph(edge_index)
+        self.gcn = params.pack(gcn_params, dims, which=1, device=self.device)
+        self.ctx.set_gcn_params(self.gcn)
+        self.theta = params.pack(theta, dims, which=0, device=self.device)
+        P = self.theta.numel()
+        self.meta_grad = torch.zeros(P, device=self.device)
+        self.m = torch.zeros(P, device=self.device)
+        self.v = torch.zeros(P, device=self.device)
+        self.step = 0
+        self.pg = process_group
+        self.tasks: List[torch.Tensor] = []
+
+    # tasks are [t_total, N, 24] float32 feature streams resident in HBM
+    def set_tasks(self, features: Sequence):
+        feats = []
+        for f in features:
+            t = f if torch.is_tensor(f) else torch.from_numpy(np.ascontiguousarray(f))
+            feats.append(t.to(self.device, torch.float32).contiguous())
+        self.tasks = feats
+        self.ctx.set_tasks(feats)
+        self.ctx.reserve(len(feats), self.cfg.batch)
+
+    def _dist(self):
+        import torch.distributed as dist
+        return dist if dist.is_available() and dist.is_initialized() else None
+
+    def meta_step(self, windows: Optional[np.ndarray] = None, fast_out=None, sync=True) -> StepResult:
+        cfg = self.cfg
+        Z = len(self.tasks)
+        if windows is None:
+            windows = window_table(cfg, Z)
+        K = cfg.inner_steps
+        losses = torch.empty(K + 1, Z, device=self.device)
+        norms = torch.empty(max(K, 1), Z, device=self.device)
+        stream = _capi.stream_ptr(torch)
+        self.ctx.meta_step(stream, self.theta, cfg.order, K, cfg.batch, windows, cfg.inner_lr,
+                           cfg.max_norm, cfg.query_loss_scale,
+                           meta_grad=self.meta_grad if cfg.order >= 1 else None,
+                           losses=losses, norms=norms, fast_out=fast_out)
+        dist = self._dist()
+        qsum = (losses[K].sum() * cfg.query_loss_scale).reshape(1)
+        if cfg.order >= 1:
+            if dist is not None:
+                dist.all_reduce(self.meta_grad, group=self.pg)
+            self.step += 1
+            norm_out = torch.empty(1, device=self.device)
+            self.ctx.adamw_step(stream, self.theta, self.meta_grad, self.m, self.v, self.step,
+                                cfg.outer_lr, cfg.outer_betas, cfg.outer_eps, cfg.outer_weight_decay,
+                                cfg.outer_max_norm, norm_out)
+        else:
+            norm_out = None
+        if dist is not None:
+            dist.all_reduce(qsum, group=self.pg)
+        if not sync:
+            return StepResult(losses, norms, float("nan"), None)
+        return StepResult(losses, norms, float(qsum.item()),
+                          float(norm_out.item()) if norm_out is not None else None)
+
+    def theta_named(self):
+        return {k: v.detach().clone() for k, v in params.unpack(self.theta, self.dims, 0).items()}

@@ -1,0 +1,114 @@
+"""Drop-in for the reference ``model.py`` (``STGCN`` + the PyG ``GCNConv`` it uses).
+
+Same constructor signatures, attribute names and state_dict keys
+(``conv{k}.bias``, ``conv{k}.lin.weight``, ``output_layer.{weight,bias}``) as
+``model.py:7-52`` with PyG 2.x ``GCNConv``. Compute runs in libsmaml.so (HIP, gfx950);
+there is no CPU path.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _capi
+from .config import ModelDims
+
+_CTX_CACHE = {}
+
+
+def _context(dims: ModelDims, device: torch.device):
+    if device.type != "cuda":
+        raise _capi.SmamlError(-1, "the STGCN-LSTM HIP path needs tensors on a HIP device (cuda)")
+    key = (dims, device.index or 0)
+    ctx = _CTX_CACHE.get(key)
+    if ctx is None:
+        ctx = _capi.Context(dims, device.index or 0)
+        _CTX_CACHE[key] = ctx
+    return ctx
+
+
+def _set_graph(ctx, edge_index: torch.Tensor):
+    ei = edge_index.detach().to("cpu", torch.int64).contiguous().numpy()
+    key = ei.tobytes()
+    if ctx.graph_key != key:
+        ctx.set_graph(ei)
+
+
+class _Linear(nn.Module):
+    """PyG ``Linear(in, out, bias=False, weight_initializer='glorot')``."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.weight = nn.Parameter(torch.empty(out_channels, in_channels))
+        a = math.sqrt(6.0 / (in_channels + out_channels))
+        nn.init.uniform_(self.weight, -a, a)
+
+    def forward(self, x):  # pragma: no cover - GCNConv drives the fused kernel
+        raise NotImplementedError("GCNConv.lin is applied inside the HIP GCN kernel")
+
+
+class GCNConv(nn.Module):
+    """PyG 2.x ``GCNConv(in, out)`` (normalize=True, add self loops, bias). forward
+    runs ``smaml_gcn_conv``: rows < num_nodes of the graph aggregate over in-edges
+    (symmetric normalisation), all other rows see only their self loop (F3)."""
+
+    def __init__(self, in_channels, out_channels, **kwargs):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.lin = _Linear(in_channels, out_channels)
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+
+    def forward(self, x, edge_index):
+        ei = edge_index.detach().to("cpu", torch.int64)
+        n_graph = int(ei.max().item()) + 1 if ei.numel() else 1
+        dims = ModelDims(num_nodes=n_graph, window_size=1, input_channels=max(4, self.in_channels),
+                         hidden_channels=max(4, self.out_channels), lstm_hidden_size=32,
+                         lstm_num_layers=1, forecast_horizon=1, output_channels=1)
+        ctx = _context(dims, x.device)
+        _set_graph(ctx, ei)
+        x = x.contiguous().float()
+        out = torch.empty(x.shape[0], self.out_channels, device=x.device, dtype=torch.float32)
+        ctx.gcn_conv(_capi.stream_ptr(torch), x, self.lin.weight.detach().contiguous(),
+                     self.bias.detach().contiguous(), out)
+        return out
+
+    def __repr__(self):
+        return f"GCNConv({self.in_channels}, {self.out_channels})"
+
+
+class STGCN(nn.Module):
+    """model.py:7-52. ``forward`` (not on the hybrid path) returns the last time block's
+    node features through ``output_layer`` as the reference does (model.py:44-52)."""
+
+    def __init__(self, in_channels, hidden_channels, out_channels=12, window_size=6,
+                 forecast_horizon=1, dropout_rate=0.3):
+        super().__init__()
+        self.window_size = window_size
+        self.out_channels = out_channels
+        self.forecast_horizon = forecast_horizon
+        self.dropout_rate = dropout_rate
+        self.conv1 = GCNConv(in_channels, hidden_channels)
+        self.conv2 = GCNConv(hidden_channels, hidden_channels)
+        self.conv3 = GCNConv(hidden_channels, hidden_channels)
+        self.conv4 = GCNConv(hidden_channels, hidden_channels)
+        self.dropout = nn.Dropout(p=dropout_rate)
+        self.output_layer = nn.Linear(hidden_channels, out_channels * forecast_horizon)
+
+    def forward(self, x, edge_index):
+        if self.training and self.dropout_rate > 0:
+            warnings.warn("HIP STGCN path applies no dropout (SURVEY F7)", stacklevel=2)
+        with torch.no_grad():
+            h = x
+            for conv in (self.conv1, self.conv2, self.conv3, self.conv4):
+                h = torch.relu_(conv(h, edge_index))
+            num_nodes = h.shape[0] // self.window_size
+            h = h[-num_nodes:]
+            out = torch.nn.functional.linear(h, self.output_layer.weight, self.output_layer.bias)
+        return out.view(num_nodes, self.forecast_horizon, self.out_channels).reshape(-1, self.out_channels)
