@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--inner-steps", type=int, default=5)
     p.add_argument("--nodes", type=int, default=441)
-    p.add_argument("--order", type=int, default=1)
+    p.add_argument("--order", type=int, default=2, help="2 = second-order MAML (BASELINE config 2)")
     p.add_argument("--cpu-sample-steps", type=int, default=6,
                    help="reference-port CPU sample-steps to time (0 = skip)")
     p.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
@@ -142,7 +142,7 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed
-    flops_meta = algorithmic_flops(d, args.tasks, cfg.inner_steps, cfg.batch, 1)
+    flops_meta = algorithmic_flops(d, args.tasks, cfg.inner_steps, cfg.batch, cfg.order)
     out = {
         "metric": "MAML meta-steps/sec (15-task batch, N=441, T=24)",
         "value": value,
@@ -168,8 +168,6 @@ def main():
         "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,
         "query_mse": qmse,
     }
-    if world == 1 and cfg.order == 2:
-        out["meta_step_tflop_so"] = algorithmic_flops(d, args.tasks, cfg.inner_steps, cfg.batch, 2) / 1e12
     if kern is not None:
         dom = max((k for k in kern if k != "misc"), key=lambda k: kern[k]["ms"])
         kd = kern[dom]

@@ -277,3 +277,59 @@ def test_full_size_meta_step_properties():
     assert 0.5 < L[-1].mean() < 2.0
     assert not torch.equal(theta0, ml.theta)
     assert np.isfinite(res.meta_loss)
+
+
+# ----------------------------------------------------------------------------- second order
+@pytest.mark.parametrize("clip", [0, 1])
+def test_second_order_meta_grad_cfg1(golden_dir, clip):
+    """Second-order meta-gradient (through both inner SGD steps, the Hessian of each support
+    loss and the clip_grad_norm_ coefficient) vs torch.func through the reference module."""
+    d = CONFIG1
+    z = load(golden_dir, "cfg1_maml.npz")
+    steps, batch, support, qb = (int(z[k]) for k in ("steps", "batch", "support", "qbatch"))
+    P = synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    cfg = MamlConfig(inner_steps=steps, batch=batch, order=2, support_samples=support,
+                     max_norm=float(z["max_norms"][clip]))
+    ml = MetaLearner(d, cfg, gcn, theta, z["edge_index"], device=DEV)
+    feats = [synth.make_features(int(s), d.num_nodes, synth.t_total_for(support + qb)) for s in z["feat_seeds"]]
+    ml.set_tasks(feats)
+    res = ml.meta_step()
+    losses = res.losses.cpu().numpy()
+    total = {k: 0.0 for k in names}
+    for j in range(len(feats)):
+        tag = f"t{j}_c{clip}_o2"
+        assert rel(losses[:steps, j], z[tag + "_losses"]) < 1e-5
+        assert abs(losses[steps, j] - float(z[tag + "_query"])) < 1e-5 * float(z[tag + "_query"])
+        for k in names:
+            total[k] = total[k] + z[f"{tag}_metagrad/{k}"]
+    mg = params.unpack(ml.meta_grad, d, 0)
+    for k in names:
+        assert rel(mg[k].cpu().numpy(), total[k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 0.02])
+def test_second_order_matches_oracle_cfg2(max_norm):
+    """Config-2 shapes (N=441, Hc=256, LSTM 4x128), K=2 inner steps, B=1, 2 tasks."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=1, order=2, max_norm=max_norm)
+    P = synth.init_params(8, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    T = stream_len_for(cfg, d)
+    feats = [synth.make_features(1200 + j, d.num_nodes, T) for j in range(2)]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml.set_tasks(feats)
+    res = ml.meta_step()
+    PT = refcpu.to_torch(P)
+    Pg = {k: v for k, v in PT.items() if k not in names}
+    S = cfg.inner_steps * cfg.batch
+    tasks = [refcpu.TaskData(f, ei, d) for f in feats]
+    ref = refcpu.meta_step({k: PT[k] for k in names}, Pg, tasks, list(range(S, S + cfg.batch)),
+                           cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, 2)
+    losses = res.losses.cpu().numpy()
+    for j in range(2):
+        assert abs(losses[-1, j] - ref["query_losses"][j]) < 1e-4 * ref["query_losses"][j]
+    mg = params.unpack(ml.meta_grad, d, 0)
+    for k in names:
+        assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k

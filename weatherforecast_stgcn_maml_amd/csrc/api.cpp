@@ -175,6 +175,11 @@ struct smaml_ctx {
   std::vector<const float*> feats;
   std::vector<int> t_total;
   Timer tm;
+  // second-order state
+  bool so_cap = false;
+  float *so_u = nullptr, *so_hu = nullptr;
+  float *so_theta = nullptr, *so_grad = nullptr, *so_norm = nullptr, *so_coef = nullptr;
+  int64_t so_store_cap = 0, so_nc_cap = 0;
 };
 
 namespace {
@@ -184,9 +189,10 @@ int ensure_device(smaml_ctx* c) {
   return SMAML_OK;
 }
 
-int reserve(smaml_ctx* c, int Z, int B) {
+int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   const int zb = Z * B;
-  if (zb <= c->zb_cap && Z <= c->z_cap) return SMAML_OK;
+  so = so || c->so_cap;
+  if (zb <= c->zb_cap && Z <= c->z_cap && so == c->so_cap) return SMAML_OK;
   const int zbc = std::max(zb, c->zb_cap), zc = std::max(Z, c->z_cap);
   const Dims& d = c->d;
   const int64_t rows = (int64_t)zbc * d.T * d.N;
@@ -217,6 +223,18 @@ int reserve(smaml_ctx* c, int Z, int B) {
   if (!alias_gcn) {
     parts.push_back({(void**)&w.gcnA, rows * d.Hc * 4});
     parts.push_back({(void**)&w.gcnB, rows * d.Hc * 4});
+  }
+  float *so_u = nullptr, *so_hu = nullptr;
+  if (so) {
+    parts.push_back({(void**)&w.RHs, rows * d.L * d.H * 4});
+    parts.push_back({(void**)&w.RCs, rows * d.L * d.H * 4});
+    parts.push_back({(void**)&w.RGs, rows * d.L * G * 4});
+    parts.push_back({(void**)&w.RdG, rows * G * 4});
+    parts.push_back({(void**)&w.RdH, rows * d.H * 4});
+    parts.push_back({(void**)&w.Rdc, seq * d.H * 4});
+    parts.push_back({(void**)&w.Rdpred, seq * d.HfC * 4});
+    parts.push_back({(void**)&so_u, (int64_t)zc * c->po.P * 4});
+    parts.push_back({(void**)&so_hu, (int64_t)zc * c->po.P * 4});
   }
   (void)dummy;
   int64_t total = 0;
@@ -251,6 +269,31 @@ int reserve(smaml_ctx* c, int Z, int B) {
   c->grad = grad;
   c->zb_cap = zbc;
   c->z_cap = zc;
+  c->so_cap = so;
+  c->so_u = so_u;
+  c->so_hu = so_hu;
+  if (so_hu) HIP_TRY(hipMemset(so_hu, 0, (size_t)zc * c->po.P * 4));
+  return SMAML_OK;
+}
+
+// Per-step stores of the second-order sweep: theta_k and g_k [K][Z][P], |g_k| and the
+// clip coefficient [K][Z].
+int ensure_so_store(smaml_ctx* c, int K, int Z) {
+  const int64_t need = (int64_t)K * Z * c->po.P;
+  if (need <= c->so_store_cap && (int64_t)K * Z <= c->so_nc_cap) return SMAML_OK;
+  if (c->so_theta) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree(c->so_theta));
+    HIP_TRY(hipFree(c->so_grad));
+    HIP_TRY(hipFree(c->so_norm));
+    HIP_TRY(hipFree(c->so_coef));
+  }
+  HIP_TRY(hipMalloc((void**)&c->so_theta, need * 4));
+  HIP_TRY(hipMalloc((void**)&c->so_grad, need * 4));
+  HIP_TRY(hipMalloc((void**)&c->so_norm, (int64_t)K * Z * 4));
+  HIP_TRY(hipMalloc((void**)&c->so_coef, (int64_t)K * Z * 4));
+  c->so_store_cap = need;
+  c->so_nc_cap = (int64_t)K * Z;
   return SMAML_OK;
 }
 
@@ -345,6 +388,75 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
           launch_wgrad(s, d, w, w.dG, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
                        TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih, lo.bhh));
     if (l > 0) TIMED(c, s, C_DX, 2.0 * w.Z * TM * 4 * d.H * lo.cin, launch_dx(s, d, w, theta, tstride, lo));
+  }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+// Primal recompute + tangent along U (second-order sweep), GCN features recomputed.
+int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride,
+                     const float* const* xtab_dev) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  const int rps = d.T * d.N;
+  const int zb = w.Z * w.B;
+  const float* src = nullptr;
+  float* bufs[2] = {w.gcnA, w.gcnB};
+  for (int k = 0; k < 4; ++k) {
+    const bool last = k == 3;
+    float* dst = last ? w.F : bufs[k & 1];
+    TIMED(c, s, C_GCN, 2.0 * zb * rps * c->go.cin[k] * d.Hc,
+          launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
+                           c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
+                           rps, d.N));
+    src = dst;
+  }
+  for (int l = 0; l < d.L; ++l) {
+    const LayerOff& lo = c->po.lay[l];
+    for (int t = 0; t < d.T; ++t) {
+      const double k1 = lo.cin + (t > 0 ? d.H : 0);
+      const double k2 = (l > 0 ? 2.0 : 1.0) * lo.cin + (t > 0 ? 2.0 * d.H : 0.0);
+      TIMED(c, s, C_FWD, 2.0 * w.Z * w.M * 4 * d.H * (k1 + k2),
+            launch_lstm_fwd_dual(s, d, w, l, t, theta, U, tstride, lo));
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+// Tangent of the backward pass: HU[z] = H_z U[z] (primal weight grads are not formed).
+int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride, float* HU) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  const ParamOff& po = c->po;
+  const int64_t TM = (int64_t)d.T * w.M;
+  const int64_t lsz = (int64_t)w.Z * TM * d.H;
+  TIMED(c, s, C_MISC, 0, (void)hipMemsetAsync(w.dH, 0, (size_t)lsz * 4, s));
+  TIMED(c, s, C_MISC, 0, (void)hipMemsetAsync(w.RdH, 0, (size_t)lsz * 4, s));
+  TIMED(c, s, C_HEAD_DH, 3.0 * 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh_dual(s, d, w, theta, U, tstride, po));
+  const int64_t toff = (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
+  TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
+        launch_wgrad(s, d, w, w.Rdpred, (int64_t)w.M * d.HfC, d.HfC, w.Hs + toff, TM * d.H, d.H, nullptr, 0, 0,
+                     w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false));
+  TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
+        launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, w.RHs + toff, TM * d.H, d.H, nullptr, 0, 0,
+                     w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true));
+  for (int l = d.L - 1; l >= 0; --l) {
+    const LayerOff& lo = po.lay[l];
+    for (int t = d.T - 1; t >= 0; --t)
+      TIMED(c, s, C_BWD, t + 1 < d.T ? 3.0 * 2.0 * w.Z * w.M * 4 * d.H * d.H : 0.0,
+            launch_lstm_bwd_dual(s, d, w, l, t, theta, U, tstride, lo));
+    const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
+    const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
+    TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H),
+          launch_wgrad(s, d, w, w.RdG, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
+                       TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false));
+    TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H),
+          launch_wgrad(s, d, w, w.dG, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
+                       w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh,
+                       false, true));
+    if (l > 0)
+      TIMED(c, s, C_DX, 3.0 * 2.0 * w.Z * TM * 4 * d.H * lo.cin, launch_dx_dual(s, d, w, theta, U, tstride, lo));
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -460,6 +572,10 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->xtab_pinned) (void)hipHostFree((void*)c->xtab_pinned);
   if (c->scratch_loss) (void)hipFree(c->scratch_loss);
   if (c->xtab_evt) (void)hipEventDestroy(c->xtab_evt);
+  if (c->so_theta) (void)hipFree(c->so_theta);
+  if (c->so_grad) (void)hipFree(c->so_grad);
+  if (c->so_norm) (void)hipFree(c->so_norm);
+  if (c->so_coef) (void)hipFree(c->so_coef);
   for (auto& r : c->tm.recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -562,14 +678,14 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   if (c->feats.empty()) return fail(SMAML_ESTATE, "smaml_set_tasks not called");
   if (!theta || steps < 0 || batch <= 0 || !windows_host) return fail(SMAML_EINVAL, "bad meta_step arguments");
   if (order < 0 || order > 2) return fail(SMAML_EINVAL, "order must be 0, 1 or 2");
-  if (order == 2) return fail(SMAML_ENOTIMPL, "second-order meta-gradient not built yet");
   if (order >= 1 && !meta_grad) return fail(SMAML_EINVAL, "meta_grad required for order >= 1");
   TRY(ensure_device(c));
   hipStream_t s = (hipStream_t)stream;
   const Dims& d = c->d;
   const int Z = (int)c->feats.size();
   const int B = batch;
-  TRY(reserve(c, Z, B));
+  TRY(reserve(c, Z, B, order == 2));
+  if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z));
   set_work(c, Z, B);
   // sample window table for every step (support steps then the query batch)
   const int64_t nptr = (int64_t)(steps + 1) * Z * B;
@@ -598,16 +714,28 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const float inv = 1.f / ((float)d.N * d.HfC * B);
   launch_broadcast(s, theta, P, Z, c->fast);
   const double head_fl = 2.0 * Z * c->w.M * d.HfC * d.H;
+  const bool so = order == 2;
   for (int k = 0; k < steps; ++k) {
     const float* const* xt = c->xtab + (int64_t)k * Z * B;
+    if (so)
+      HIP_TRY(hipMemcpyAsync(c->so_theta + (int64_t)k * Z * P, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
     TRY(run_forward(c, s, c->fast, P, xt));
     TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
     TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
     TRY(run_backward(c, s, c->fast, P, c->grad));
     TIMED(c, s, C_MISC, 0, launch_sqsum(s, c->grad, P, Z, c->w.sqpart));
-    TIMED(c, s, C_MISC, 0,
-          launch_clip_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
-                          norms ? norms + (int64_t)k * Z : nullptr, nullptr));
+    if (so) {
+      HIP_TRY(hipMemcpyAsync(c->so_grad + (int64_t)k * Z * P, c->grad, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
+      TIMED(c, s, C_MISC, 0,
+            launch_clip_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm, c->so_norm + (int64_t)k * Z,
+                            c->so_coef + (int64_t)k * Z));
+      if (norms)
+        HIP_TRY(hipMemcpyAsync(norms + (int64_t)k * Z, c->so_norm + (int64_t)k * Z, Z * 4, hipMemcpyDeviceToDevice, s));
+    } else {
+      TIMED(c, s, C_MISC, 0,
+            launch_clip_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
+                            norms ? norms + (int64_t)k * Z : nullptr, nullptr));
+    }
   }
   const float* const* xq = c->xtab + (int64_t)steps * Z * B;
   TRY(run_forward(c, s, c->fast, P, xq));
@@ -617,6 +745,26 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   if (order == 1) {
     TRY(run_backward(c, s, c->fast, P, c->grad));
     TIMED(c, s, C_MISC, 0, launch_sum_tasks(s, c->grad, P, Z, meta_grad));
+  } else if (so) {
+    // v_K = d(query_scale * L_q)/d theta_K, then back through every inner step:
+    //   v_k = v_{k+1} - lr * H_k w_k,  w_k = clip-adjusted v_{k+1}
+    if (fast_out) HIP_TRY(hipMemcpyAsync(fast_out, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
+    fast_out = nullptr;
+    TRY(run_backward(c, s, c->fast, P, c->grad));
+    float* V = c->grad;
+    for (int k = steps - 1; k >= 0; --k) {
+      const float* th = c->so_theta + (int64_t)k * Z * P;
+      const float* gk = c->so_grad + (int64_t)k * Z * P;
+      const float* const* xt = c->xtab + (int64_t)k * Z * B;
+      TIMED(c, s, C_MISC, 0,
+            launch_so_dir(s, V, gk, P, Z, c->w.sqpart, c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z,
+                          max_norm, c->so_u));
+      TRY(run_forward_dual(c, s, th, c->so_u, P, xt));
+      TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
+      TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
+      TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
+    }
+    TIMED(c, s, C_MISC, 0, launch_sum_tasks(s, V, P, Z, meta_grad));
   }
   if (fast_out) HIP_TRY(hipMemcpyAsync(fast_out, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipGetLastError());

@@ -52,6 +52,10 @@ struct Work {
   float* lpart;            // loss partials [Z][lblocks]
   int lblocks;
   double* sqpart;          // [Z][SQB]
+  // second-order (tangent) buffers; null unless reserved with so = true
+  float *RHs, *RCs, *RGs;  // like Hs, Cs, Gs
+  float *RdG, *RdH, *Rdc;  // like dG, dH, dc
+  float* Rdpred;           // like dpred
 };
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
@@ -75,7 +79,8 @@ void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, 
 void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
                   int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
                   int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
-                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2);
+                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias = true,
+                  bool accumulate = false);
 void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part);
 void launch_clip_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, const double* part,
                      float lr, float max_norm, float* norm_out, float* coef_out);
@@ -84,5 +89,20 @@ void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float
 void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
                   float lr, float b1, float b2, float eps, float wd, float step_size, float bc2_sqrt,
                   float max_norm, float* norm_out);
+
+// ---- second-order launchers (kernels_dual.hip) ----
+void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          const float* U, int64_t tstride, const LayerOff& lo);
+void launch_head_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
+                      int64_t tstride, const ParamOff& po, const float* const* xtab, float dscale);
+void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
+                         int64_t tstride, const ParamOff& po);
+void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U, int64_t tstride,
+                    const LayerOff& lo);
+void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          const float* U, int64_t tstride, const LayerOff& lo);
+void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,
+                   const float* coefs, float max_norm, float* U);
+void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha);
 
 }  // namespace smaml

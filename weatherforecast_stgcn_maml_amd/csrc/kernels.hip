@@ -14,8 +14,8 @@
 // Every GEMM-shaped contraction runs on v_mfma_f32_32x32x2_f32 (gemm_core.h). All
 // reductions are in a fixed order (no float atomics), so results are bitwise
 // reproducible run to run and across ranks.
-#include "gemm_core.h"
 #include "kernels.h"
+#include "loaders.h"
 
 namespace smaml {
 
@@ -23,8 +23,6 @@ using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-con
 using CfgGate = GemmCfg<128, 128, 4, 1, true, true>;  // LSTM forward: wave = 32 rows x 4 gates
 using CfgNN = GemmCfg<128, 128, 4, 1, true, false>;   // C = A . B   (B n-contiguous)
 using CfgTN = GemmCfg<128, 128, 2, 2, false, false>;  // C = A^T . B (split-K weight grads)
-
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------------------------
 // Block-wide deterministic sum (fixed shuffle tree + fixed wave order).
@@ -81,25 +79,6 @@ struct GcnA {
       return s;
     }
     return ld4(base + (int64_t)q * cin + k);
-  }
-};
-
-struct RowMajorKC {  // [rows][K] with K contiguous, zero outside [0,rows) x [0,K)
-  const float* p;
-  int rows, K;
-  __device__ __forceinline__ float4 operator()(int r, int k) const {
-    if (r >= rows || k >= K) return f4zero();
-    return ld4(p + (int64_t)r * K + k);
-  }
-};
-
-struct RowMajorMC {  // [K][cols] with cols contiguous (operand row index = col)
-  const float* p;
-  int64_t K;
-  int cols;
-  __device__ __forceinline__ float4 operator()(int64_t k, int c) const {
-    if (k >= K || c >= cols) return f4zero();
-    return ld4(p + k * cols + c);
   }
 };
 
@@ -446,20 +425,6 @@ void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, in
 // (the trailing column of ones is produced as column sums of A in tile column 0:
 //  the bias gradient). For LSTM layer l: A = dG [T*M][4H], B1 = x_l [T*M][cin],
 //  B2 = h_l (shifted one time block: h_{t-1}); for the head: A = dpred, B1 = h_T.
-struct WgB {
-  const float* B1;
-  const float* B2;
-  int c1, c2;
-  int64_t K, Mshift;
-  __device__ __forceinline__ float4 operator()(int64_t k, int j) const {
-    if (k >= K) return f4zero();
-    if (j < c1) return ld4(B1 + k * c1 + j);
-    j -= c1;
-    if (j >= c2 || k < Mshift) return f4zero();
-    return ld4(B2 + (k - Mshift) * c2 + j);
-  }
-};
-
 struct ColSumHook {
   float* acc;
   __device__ __forceinline__ void operator()(const float* as, int) const {
@@ -474,13 +439,13 @@ struct ColSumHook {
 
 __global__ __launch_bounds__(NT) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
-                                              int ntn, float* __restrict__ part, int ldp) {
+                                              int ntn, float* __restrict__ part, int ldp, int with_bias) {
   __shared__ float smem[CfgTN::SMEM_FLOATS];
   const int z = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
   const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
   RowMajorMC la{A + (int64_t)z * a_zstride, lb.K, Mrows};
   WgB b = lb;
-  b.B1 += (int64_t)z * b1_zstride;
+  if (b.B1) b.B1 += (int64_t)z * b1_zstride;
   if (b.B2) b.B2 += (int64_t)z * b2_zstride;
   const int64_t kbeg = (int64_t)split * kchunk;
   const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
@@ -490,7 +455,7 @@ __global__ __launch_bounds__(NT) void k_wgrad(const float* __restrict__ A, int64
   float bsum = 0.f;
   // k indices exceed int range only in the loaders (int64 there); the mainloop
   // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
-  if (tn == 0) {
+  if (tn == 0 && with_bias) {
     ColSumHook hook{&bsum};
     gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
@@ -512,13 +477,13 @@ __global__ __launch_bounds__(NT) void k_wgrad(const float* __restrict__ A, int64
     }
   if (tn == 0 && threadIdx.x < CfgTN::BM) {
     const int row = m0 + threadIdx.x;
-    if (row < Mrows) P[(int64_t)row * ldp + ncols] = bsum;
+    if (row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? bsum : 0.f;
   }
 }
 
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int Mrows, int ldp, int c1, int c2,
                                float* __restrict__ grad, int64_t P, int64_t off_w1, int64_t off_w2,
-                               int64_t off_b1, int64_t off_b2) {
+                               int64_t off_b1, int64_t off_b2, int accumulate) {
   const int z = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)Mrows * ldp;
@@ -528,20 +493,25 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int M
   for (int s = 0; s < nsplit; ++s) v += p[(int64_t)s * total];
   const int i = (int)(e / ldp), j = (int)(e - (int64_t)i * ldp);
   float* g = grad + (int64_t)z * P;
+  float* dst;
   if (j < c1) {
-    g[off_w1 + (int64_t)i * c1 + j] = v;
+    dst = g + off_w1 + (int64_t)i * c1 + j;
   } else if (j < c1 + c2) {
-    g[off_w2 + (int64_t)i * c2 + (j - c1)] = v;
+    dst = g + off_w2 + (int64_t)i * c2 + (j - c1);
   } else {
+    if (accumulate) return;  // bias written by the first (bias-carrying) pass
     g[off_b1 + i] = v;
     if (off_b2 >= 0) g[off_b2 + i] = v;
+    return;
   }
+  *dst = accumulate ? *dst + v : v;
 }
 
 void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
                   int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
                   int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
-                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2) {
+                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias,
+                  bool accumulate) {
   (void)d;
   const int ncols = c1 + c2;
   const int ldp = ncols + 1;
@@ -565,11 +535,12 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
   lb.K = K;
   lb.Mshift = Mshift;
   dim3 grid(ntm * ntn, (unsigned)nsplit, w.Z);
-  k_wgrad<<<grid, NT, 0, s>>>(A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, w.wpart, ldp);
+  k_wgrad<<<grid, NT, 0, s>>>(A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, w.wpart, ldp,
+                              with_bias ? 1 : 0);
   const int64_t total = (int64_t)Mrows * ldp;
   dim3 g2((unsigned)((total + 255) / 256), w.Z);
   k_wgrad_reduce<<<g2, 256, 0, s>>>(w.wpart, (int)nsplit, Mrows, ldp, c1, c2, grad, P, off_w1, off_w2, off_b1,
-                                    off_b2);
+                                    off_b2, accumulate ? 1 : 0);
 }
 
 // ====================================================================================

@@ -1,0 +1,396 @@
+// Second-order MAML: forward-over-reverse Hessian-vector products through the LSTM + head.
+//
+// For inner step k the meta-backward needs  H_k w  (H_k = Hessian of the step-k support
+// loss at theta_k, w = the clip-adjusted meta-gradient direction). Every kernel here
+// recomputes the primal quantity of its reference counterpart (kernels.hip) and, in the
+// same launch, its directional derivative R{.} along w (Pearlmutter's R-operator):
+//   k_lstm_fwd_dual    pre, R(pre) = [x|h|Rx|Rh].[U_ih|U_hh|W_ih|W_hh]^T + U_b  ->  gates, c, h and tangents
+//   k_head_dual        pred, R(pred) -> dpred, R(dpred)
+//   k_gemm_nn_dual     dh_T / dX and their tangents ([R(A) | A] . [W ; U])
+//   k_lstm_bwd_dual    BPTT cell step and its tangent (product rule through every gate)
+// The tangent weight gradient R(dW) = R(dG)^T [x|h] + dG^T [Rx|Rh] reuses k_wgrad (two
+// accumulating passes). All contractions are fp32 MFMA (gemm_core.h).
+#include "kernels.h"
+#include "loaders.h"
+
+namespace smaml {
+
+using CfgGateD = GemmCfg<128, 128, 4, 1, true, true>;
+using CfgNTD = GemmCfg<128, 128, 2, 2, true, true>;
+using CfgNND = GemmCfg<128, 128, 4, 1, true, false>;
+
+__device__ __forceinline__ float block_sum_f(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+
+// ====================================================================================
+__global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ X, const float* __restrict__ RX,
+                                                      float* __restrict__ Hs, float* __restrict__ Cs,
+                                                      float* __restrict__ Gs, float* __restrict__ RHs,
+                                                      float* __restrict__ RCs, float* __restrict__ RGs,
+                                                      const float* __restrict__ theta, const float* __restrict__ U,
+                                                      int64_t tstride, LayerOff lo, int T, int M, int H, int t) {
+  __shared__ float smem[CfgGateD::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const float* th = theta + (int64_t)z * tstride;
+  const float* u = U + (int64_t)z * tstride;
+  const int cin = lo.cin;
+  const int64_t bt = ((int64_t)z * T + t) * M;
+  const float* xt = X + bt * cin;
+  const float* rxt = RX ? RX + bt * cin : nullptr;
+  const float* hp = t > 0 ? Hs + (bt - M) * H : nullptr;
+  const float* rhp = t > 0 ? RHs + (bt - M) * H : nullptr;
+  const int wh = hp ? H : 0;
+  const int m0 = blockIdx.x * CfgGateD::BM, n0 = blockIdx.y * CfgGateD::BN;
+
+  Acc<CfgGateD> ap, at;
+  ap.zero();
+  at.zero();
+  {
+    SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
+    SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
+    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh, ap, smem);
+  }
+  {
+    const int wrx = rxt ? cin : 0;
+    SegKC la{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M};
+    SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
+    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+  }
+  const int j = blockIdx.y * 32 + (threadIdx.x & 31);
+  if (j >= H) return;
+  float bp[4], bu[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bp[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
+    bu[g] = u[lo.bih + g * H + j] + u[lo.bhh + g * H + j];
+  }
+  const float* Cp = t > 0 ? Cs + (bt - M) * H : nullptr;
+  const float* RCp = t > 0 ? RCs + (bt - M) * H : nullptr;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + acc_row<CfgGateD>(0, r);
+    if (m >= M) continue;
+    const float gi = sigmoidf_(ap.v[0][0][r] + bp[0]);
+    const float gf = sigmoidf_(ap.v[0][1][r] + bp[1]);
+    const float gg = tanhf(ap.v[0][2][r] + bp[2]);
+    const float go = sigmoidf_(ap.v[0][3][r] + bp[3]);
+    const float ri = gi * (1.f - gi) * (at.v[0][0][r] + bu[0]);
+    const float rf = gf * (1.f - gf) * (at.v[0][1][r] + bu[1]);
+    const float rg = (1.f - gg * gg) * (at.v[0][2][r] + bu[2]);
+    const float ro = go * (1.f - go) * (at.v[0][3][r] + bu[3]);
+    const float cp = Cp ? Cp[(int64_t)m * H + j] : 0.f;
+    const float rcp = RCp ? RCp[(int64_t)m * H + j] : 0.f;
+    const float c = gf * cp + gi * gg;
+    const float rc = rf * cp + gf * rcp + ri * gg + gi * rg;
+    const float tc = tanhf(c);
+    const float h = go * tc;
+    const float rh = ro * tc + go * (1.f - tc * tc) * rc;
+    const int64_t row = bt + m;
+    float* grow = Gs + row * (4 * H);
+    float* rgrow = RGs + row * (4 * H);
+    grow[j] = gi;
+    grow[H + j] = gf;
+    grow[2 * H + j] = gg;
+    grow[3 * H + j] = go;
+    rgrow[j] = ri;
+    rgrow[H + j] = rf;
+    rgrow[2 * H + j] = rg;
+    rgrow[3 * H + j] = ro;
+    Cs[row * H + j] = c;
+    Hs[row * H + j] = h;
+    RCs[row * H + j] = rc;
+    RHs[row * H + j] = rh;
+  }
+}
+
+void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          const float* U, int64_t tstride, const LayerOff& lo) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  const float* X = (l == 0) ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
+  const float* RX = (l == 0) ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
+  dim3 grid((w.M + CfgGateD::BM - 1) / CfgGateD::BM, (d.H + 31) / 32, w.Z);
+  k_lstm_fwd_dual<<<grid, NT, 0, s>>>(X, RX, w.Hs + l * lsz, w.Cs + l * lsz, w.Gs + l * lsz * 4, w.RHs + l * lsz,
+                                      w.RCs + l * lsz, w.RGs + l * lsz * 4, theta, U, tstride, lo, d.T, w.M, d.H, t);
+}
+
+// ====================================================================================
+__global__ __launch_bounds__(NT) void k_head_dual(const float* __restrict__ hT, const float* __restrict__ RhT,
+                                                  int64_t zstride, const float* __restrict__ theta,
+                                                  const float* __restrict__ U, int64_t tstride, int64_t wo,
+                                                  int64_t bo, const float* const* __restrict__ xtab,
+                                                  float* __restrict__ dpred, float* __restrict__ Rdpred, int M,
+                                                  int H, int HfC, int N, int Hf, int C, int T, int cin0, int B,
+                                                  float dscale) {
+  __shared__ float smem[CfgNTD::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const float* th = theta + (int64_t)z * tstride;
+  const float* u = U + (int64_t)z * tstride;
+  const float* h = hT + (int64_t)z * zstride;
+  const float* rh = RhT + (int64_t)z * zstride;
+  const int m0 = blockIdx.x * CfgNTD::BM;
+  Acc<CfgNTD> ap, at;
+  ap.zero();
+  at.zero();
+  {
+    RowMajorKC la{h, M, H};
+    RowMajorKC lb{th + wo, HfC, H};
+    gemm_mainloop<CfgNTD>(la, lb, m0, 0, 0, H, ap, smem);
+  }
+  {
+    SegKC la{{h, rh, nullptr, nullptr}, {H, H, 0, 0}, M};
+    SegKC lb{{u + wo, th + wo, nullptr, nullptr}, {H, H, 0, 0}, HfC};
+    gemm_mainloop<CfgNTD>(la, lb, m0, 0, 0, 2 * H, at, smem);
+  }
+#pragma unroll
+  for (int i = 0; i < CfgNTD::WTM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < CfgNTD::WTN; ++jj) {
+      const int cc = acc_col<CfgNTD>(jj);
+      if (cc >= HfC) continue;
+      const float bc = th[bo + cc], ubc = u[bo + cc];
+      const int hh = cc / C, c = cc - hh * C;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + acc_row<CfgNTD>(i, r);
+        if (m >= M) continue;
+        const float p = ap.v[i][jj][r] + bc;
+        const float rp = at.v[i][jj][r] + ubc;
+        const int s = m / N, n = m - s * N;
+        const int rr = n * Hf + hh;
+        const int hp = rr / N, np = rr - hp * N;
+        const float y = xtab[z * B + s][((int64_t)(T + 1 + hp) * N + np) * cin0 + c];
+        const int64_t o = ((int64_t)z * M + m) * HfC + cc;
+        dpred[o] = dscale * (p - y);
+        Rdpred[o] = dscale * rp;
+      }
+    }
+}
+
+void launch_head_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
+                      int64_t tstride, const ParamOff& po, const float* const* xtab, float dscale) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  const int64_t off = (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
+  dim3 grid((w.M + CfgNTD::BM - 1) / CfgNTD::BM, 1, w.Z);
+  k_head_dual<<<grid, NT, 0, s>>>(w.Hs + off, w.RHs + off, (int64_t)d.T * w.M * d.H, theta, U, tstride, po.wo,
+                                  po.bo, xtab, w.dpred, w.Rdpred, w.M, d.H, d.HfC, d.N, d.Hf, d.C, d.T, d.Cin0, w.B,
+                                  dscale);
+}
+
+// ====================================================================================
+// out = A . W ;  Rout = [RA | A] . [W ; U_W]     (W, U_W: [K][ncols] at woff in theta / U)
+__global__ __launch_bounds__(NT) void k_gemm_nn_dual(const float* __restrict__ A, const float* __restrict__ RA,
+                                                     int64_t a_zstride, int rows, int K,
+                                                     const float* __restrict__ theta, const float* __restrict__ U,
+                                                     int64_t tstride, int64_t woff, int ncols, float* __restrict__ out,
+                                                     float* __restrict__ Rout, int64_t o_zstride) {
+  __shared__ float smem[CfgNND::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const float* a = A + (int64_t)z * a_zstride;
+  const float* ra = RA + (int64_t)z * a_zstride;
+  const float* W = theta + (int64_t)z * tstride + woff;
+  const float* UW = U + (int64_t)z * tstride + woff;
+  const int m0 = blockIdx.x * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
+  Acc<CfgNND> ap, at;
+  ap.zero();
+  at.zero();
+  {
+    RowMajorKC la{a, rows, K};
+    RowMajorMC lb{W, K, ncols};
+    gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, K, ap, smem);
+  }
+  {
+    SegKC la{{ra, a, nullptr, nullptr}, {K, K, 0, 0}, rows};
+    SegMC lb{{W, UW}, {K, K}, ncols};
+    gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, 2 * K, at, smem);
+  }
+  float* o = out + (int64_t)z * o_zstride;
+  float* ro = Rout + (int64_t)z * o_zstride;
+#pragma unroll
+  for (int jj = 0; jj < CfgNND::WTN; ++jj) {
+    const int c = n0 + acc_col<CfgNND>(jj);
+    if (c >= ncols) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + acc_row<CfgNND>(0, r);
+      if (m >= rows) continue;
+      o[(int64_t)m * ncols + c] = ap.v[0][jj][r];
+      ro[(int64_t)m * ncols + c] = at.v[0][jj][r];
+    }
+  }
+}
+
+void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
+                         int64_t tstride, const ParamOff& po) {
+  const int64_t off = (int64_t)(d.T - 1) * w.M * d.H;
+  dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
+  k_gemm_nn_dual<<<grid, NT, 0, s>>>(w.dpred, w.Rdpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, U, tstride, po.wo,
+                                     d.H, w.dH + off, w.RdH + off, (int64_t)d.T * w.M * d.H);
+}
+
+void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U, int64_t tstride,
+                    const LayerOff& lo) {
+  const int rows = d.T * w.M;
+  dim3 grid((rows + CfgNND::BM - 1) / CfgNND::BM, (lo.cin + CfgNND::BN - 1) / CfgNND::BN, w.Z);
+  k_gemm_nn_dual<<<grid, NT, 0, s>>>(w.dG, w.RdG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, U, tstride,
+                                     lo.wih, lo.cin, w.dH, w.RdH, (int64_t)rows * lo.cin);
+}
+
+// ====================================================================================
+__global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, float* __restrict__ RdG,
+                                                      const float* __restrict__ dH, const float* __restrict__ RdH,
+                                                      float* __restrict__ dc, float* __restrict__ Rdc,
+                                                      const float* __restrict__ Gs, const float* __restrict__ Cs,
+                                                      const float* __restrict__ RGs, const float* __restrict__ RCs,
+                                                      const float* __restrict__ theta, const float* __restrict__ U,
+                                                      int64_t tstride, LayerOff lo, int T, int M, int H, int t) {
+  __shared__ float smem[CfgNND::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const int G4 = 4 * H;
+  const int m0 = blockIdx.x * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
+  Acc<CfgNND> ap, at;
+  ap.zero();
+  at.zero();
+  if (t + 1 < T) {
+    const int64_t nx = ((int64_t)z * T + t + 1) * M * G4;
+    const float* W = theta + (int64_t)z * tstride + lo.whh;
+    const float* UW = U + (int64_t)z * tstride + lo.whh;
+    {
+      RowMajorKC la{dG + nx, M, G4};
+      RowMajorMC lb{W, G4, H};
+      gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, G4, ap, smem);
+    }
+    {
+      SegKC la{{RdG + nx, dG + nx, nullptr, nullptr}, {G4, G4, 0, 0}, M};
+      SegMC lb{{W, UW}, {G4, G4}, H};
+      gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, 2 * G4, at, smem);
+    }
+  }
+  const int64_t bt = ((int64_t)z * T + t) * M;
+  const bool first = (t == T - 1);
+  float* dcz = dc + (int64_t)z * M * H;
+  float* rdcz = Rdc + (int64_t)z * M * H;
+#pragma unroll
+  for (int jj = 0; jj < CfgNND::WTN; ++jj) {
+    const int j = n0 + acc_col<CfgNND>(jj);
+    if (j >= H) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + acc_row<CfgNND>(0, r);
+      if (m >= M) continue;
+      const int64_t row = bt + m;
+      const float dh = ap.v[0][jj][r] + dH[row * H + j];
+      const float rdh = at.v[0][jj][r] + RdH[row * H + j];
+      const float* g = Gs + row * G4;
+      const float* rg = RGs + row * G4;
+      const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
+      const float ri = rg[j], rf = rg[H + j], rgg = rg[2 * H + j], ro = rg[3 * H + j];
+      const float c = Cs[row * H + j], rc = RCs[row * H + j];
+      const float cp = t > 0 ? Cs[(row - M) * H + j] : 0.f;
+      const float rcp = t > 0 ? RCs[(row - M) * H + j] : 0.f;
+      const float dcin = first ? 0.f : dcz[(int64_t)m * H + j];
+      const float rdcin = first ? 0.f : rdcz[(int64_t)m * H + j];
+      const float tc = tanhf(c);
+      const float s2 = 1.f - tc * tc;
+      const float rtc = s2 * rc;
+      const float dct = dcin + dh * go * s2;
+      const float rdct = rdcin + rdh * go * s2 + dh * ro * s2 - 2.f * dh * go * tc * rtc;
+      const float si = gi * (1.f - gi), sf = gf * (1.f - gf), so = go * (1.f - go), sg = 1.f - gg * gg;
+      float* d = dG + row * G4;
+      float* rd = RdG + row * G4;
+      d[j] = dct * gg * si;
+      d[H + j] = dct * cp * sf;
+      d[2 * H + j] = dct * gi * sg;
+      d[3 * H + j] = dh * tc * so;
+      rd[j] = rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri;
+      rd[H + j] = rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf;
+      rd[2 * H + j] = rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg;
+      rd[3 * H + j] = rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro;
+      dcz[(int64_t)m * H + j] = dct * gf;
+      rdcz[(int64_t)m * H + j] = rdct * gf + dct * rf;
+    }
+  }
+}
+
+void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
+                          const float* U, int64_t tstride, const LayerOff& lo) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
+  k_lstm_bwd_dual<<<grid, NT, 0, s>>>(w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
+                                      w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, d.H, t);
+}
+
+// ====================================================================================
+// Meta-backward bookkeeping (per task z):
+//   dot[z] = g_k . v                                     (fp64 partials, fixed order)
+//   w = c_k v - [c_k < 1] * max_norm * dot / (n (n + 1e-6)^2) * g_k
+//     = (d(c_k g_k)/d theta_k)^T v expressed as H_k w  (clip_grad_norm_ derivative)
+//   v -= lr * H_k w
+__global__ void k_dot(const float* __restrict__ a, const float* __restrict__ b, int64_t P, double* __restrict__ part) {
+  __shared__ double red[NT / 64];
+  const int z = blockIdx.y;
+  const float* az = a + (int64_t)z * P;
+  const float* bz = b + (int64_t)z * P;
+  const int64_t per = (P + SQB - 1) / SQB;
+  const int64_t beg = (int64_t)blockIdx.x * per, end = beg + per < P ? beg + per : P;
+  double acc = 0.0;
+  for (int64_t i = beg + threadIdx.x; i < end; i += NT) acc += (double)az[i] * (double)bz[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
+    part[(int64_t)z * SQB + blockIdx.x] = s;
+  }
+}
+
+__global__ void k_so_dir(const float* __restrict__ V, const float* __restrict__ G, int64_t P,
+                         const double* __restrict__ part, const float* __restrict__ norms,
+                         const float* __restrict__ coefs, float max_norm, float* __restrict__ Uo) {
+  const int z = blockIdx.y;
+  double dot = 0.0;
+  for (int i = 0; i < SQB; ++i) dot += part[(int64_t)z * SQB + i];
+  const float n = norms[z], c = coefs[z];
+  float beta = 0.f;
+  if (c < 1.f && n > 0.f) {
+    const double ne = (double)n + 1e-6;
+    beta = (float)((double)max_norm * dot / ((double)n * ne * ne));
+  }
+  const float* vz = V + (int64_t)z * P;
+  const float* gz = G + (int64_t)z * P;
+  float* uz = Uo + (int64_t)z * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
+    uz[i] = c * vz[i] - beta * gz[i];
+}
+
+__global__ void k_axpy(float* __restrict__ V, const float* __restrict__ X, int64_t n, float alpha) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    V[i] = fmaf(alpha, X[i], V[i]);
+}
+
+void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,
+                   const float* coefs, float max_norm, float* U) {
+  k_dot<<<dim3(SQB, Z), NT, 0, s>>>(G, V, P, part);
+  int nb = (int)((P + NT - 1) / NT);
+  if (nb > 1024) nb = 1024;
+  k_so_dir<<<dim3(nb, Z), NT, 0, s>>>(V, G, P, part, norms, coefs, max_norm, U);
+}
+
+void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha) {
+  int nb = (int)((n + NT - 1) / NT);
+  if (nb > 4096) nb = 4096;
+  k_axpy<<<nb, NT, 0, s>>>(V, X, n, alpha);
+}
+
+}  // namespace smaml

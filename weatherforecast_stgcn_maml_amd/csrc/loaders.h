@@ -1,0 +1,98 @@
+// Operand loaders for gemm_mainloop (gemm_core.h). A loader returns the float4 at a
+// logical (row, k) [KC: 4 consecutive k] or (k, col) [MC: 4 consecutive cols] position
+// of its operand, zero outside. "Seg" loaders concatenate several matrices along K,
+// which is how the fused concatenated-K GEMMs ([x_t | h_{t-1}] . [W_ih | W_hh]^T and the
+// tangent GEMMs of the second-order path) are expressed.
+#pragma once
+#include "gemm_core.h"
+
+namespace smaml {
+
+struct RowMajorKC {  // [rows][K] with K contiguous
+  const float* p;
+  int rows, K;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    if (r >= rows || k >= K) return f4zero();
+    return ld4(p + (int64_t)r * K + k);
+  }
+};
+
+struct RowMajorMC {  // [K][cols] with cols contiguous
+  const float* p;
+  int64_t K;
+  int cols;
+  __device__ __forceinline__ float4 operator()(int64_t k, int c) const {
+    if (k >= K || c >= cols) return f4zero();
+    return ld4(p + k * cols + c);
+  }
+};
+
+// A operand [rows][w0 | w1 | w2 | w3]: segment s is a row-major [rows][w_s] matrix
+// (nullptr = zeros). Widths must be multiples of 4.
+struct SegKC {
+  const float* p[4];
+  int w[4];
+  int rows;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    if (r >= rows) return f4zero();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (k < w[s]) return p[s] ? ld4(p[s] + (int64_t)r * w[s] + k) : f4zero();
+      k -= w[s];
+    }
+    return f4zero();
+  }
+};
+
+// B operand for the LSTM gate GEMMs: logical row n = ug*128 + g*32 + jj maps to weight
+// row g*H + ug*32 + jj of each segment matrix [4H][w_s] (k-concatenated).
+struct SegGateB {
+  const float* p[4];
+  int w[4];
+  int H;
+  __device__ __forceinline__ float4 operator()(int n, int k) const {
+    const int ug = n >> 7, rem = n & 127, g = rem >> 5, j = ug * 32 + (rem & 31);
+    if (j >= H) return f4zero();
+    const int64_t row = (int64_t)g * H + j;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (k < w[s]) return p[s] ? ld4(p[s] + row * w[s] + k) : f4zero();
+      k -= w[s];
+    }
+    return f4zero();
+  }
+};
+
+// B operand [K0 + K1][cols]: two row-major matrices stacked along K (cols contiguous).
+struct SegMC {
+  const float* p[2];
+  int64_t K[2];
+  int cols;
+  __device__ __forceinline__ float4 operator()(int64_t k, int c) const {
+    if (c >= cols) return f4zero();
+    if (k < K[0]) return ld4(p[0] + k * cols + c);
+    k -= K[0];
+    if (k < K[1]) return ld4(p[1] + k * cols + c);
+    return f4zero();
+  }
+};
+
+// Weight-gradient B operand: Bcat[k] = [B1[k][0..c1) | (k >= Mshift ? B2[k-Mshift][0..c2) : 0)]
+// (B1 == nullptr -> zeros: the layer-0 input has no tangent).
+struct WgB {
+  const float* B1;
+  const float* B2;
+  int c1, c2;
+  int64_t K, Mshift;
+  __device__ __forceinline__ float4 operator()(int64_t k, int j) const {
+    if (k >= K) return f4zero();
+    if (j < c1) return B1 ? ld4(B1 + k * c1 + j) : f4zero();
+    j -= c1;
+    if (j >= c2 || k < Mshift) return f4zero();
+    return ld4(B2 + (k - Mshift) * c2 + j);
+  }
+};
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace smaml
