@@ -89,12 +89,11 @@ def main():
     from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, shard_tasks, stream_len_for
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from weatherforecast_stgcn_maml_amd.distributed import env_rank, init_from_env, max_over_ranks
+
+    rank, world, local = env_rank()
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    init_from_env("nccl", torch.device("cuda", local))
 
     d = ModelDims(num_nodes=args.nodes)
     cfg = MamlConfig(inner_steps=args.inner_steps, batch=args.batch, order=args.order)
@@ -133,9 +132,7 @@ def main():
         kern = ml.ctx.timing_collect()
     qmse = float(res.losses[-1].mean().item())
     if world > 1:
-        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, f"cuda:{local}")
         q = torch.tensor([qmse * len(mine)], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(q)
         qmse = float(q.item()) / args.tasks

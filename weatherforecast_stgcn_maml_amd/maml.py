@@ -21,11 +21,7 @@ import torch
 
 from . import _capi, params, synth
 from .config import MamlConfig, ModelDims
-
-
-def shard_tasks(n_tasks: int, rank: int, world: int) -> List[int]:
-    """Round-robin task -> rank assignment (15 tasks on 8 ranks: {2,2,2,2,2,2,2,1})."""
-    return [j for j in range(n_tasks) if j % world == rank]
+from .distributed import reduce_meta, shard_tasks  # noqa: F401  (shard_tasks re-exported)
 
 
 def window_table(cfg: MamlConfig, n_tasks: int, support: Optional[int] = None,
@@ -87,11 +83,8 @@ class MetaLearner:
         self.ctx.set_tasks(feats)
         self.ctx.reserve(len(feats), self.cfg.batch)
 
-    def _dist(self):
-        import torch.distributed as dist
-        return dist if dist.is_available() and dist.is_initialized() else None
-
-    def meta_step(self, windows: Optional[np.ndarray] = None, fast_out=None, sync=True) -> StepResult:
+    def meta_step(self, windows: Optional[np.ndarray] = None, fast_out=None, sync=True,
+                  lr: Optional[float] = None) -> StepResult:
         cfg = self.cfg
         Z = len(self.tasks)
         if windows is None:
@@ -104,20 +97,16 @@ class MetaLearner:
                            cfg.max_norm, cfg.query_loss_scale,
                            meta_grad=self.meta_grad if cfg.order >= 1 else None,
                            losses=losses, norms=norms, fast_out=fast_out)
-        dist = self._dist()
         qsum = (losses[K].sum() * cfg.query_loss_scale).reshape(1)
+        reduce_meta(self.meta_grad if cfg.order >= 1 else None, qsum, self.pg)
         if cfg.order >= 1:
-            if dist is not None:
-                dist.all_reduce(self.meta_grad, group=self.pg)
             self.step += 1
             norm_out = torch.empty(1, device=self.device)
             self.ctx.adamw_step(stream, self.theta, self.meta_grad, self.m, self.v, self.step,
-                                cfg.outer_lr, cfg.outer_betas, cfg.outer_eps, cfg.outer_weight_decay,
+                                cfg.outer_lr if lr is None else lr, cfg.outer_betas, cfg.outer_eps, cfg.outer_weight_decay,
                                 cfg.outer_max_norm, norm_out)
         else:
             norm_out = None
-        if dist is not None:
-            dist.all_reduce(qsum, group=self.pg)
         if not sync:
             return StepResult(losses, norms, float("nan"), None)
         return StepResult(losses, norms, float(qsum.item()),
