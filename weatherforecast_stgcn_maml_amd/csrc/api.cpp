@@ -372,7 +372,6 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   const ParamOff& po = c->po;
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
-  TIMED(c, s, C_MISC, 0, (void)hipMemsetAsync(w.dH, 0, (size_t)lsz * 4, s));
   TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
   const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
@@ -431,8 +430,6 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   const ParamOff& po = c->po;
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
-  TIMED(c, s, C_MISC, 0, (void)hipMemsetAsync(w.dH, 0, (size_t)lsz * 4, s));
-  TIMED(c, s, C_MISC, 0, (void)hipMemsetAsync(w.RdH, 0, (size_t)lsz * 4, s));
   TIMED(c, s, C_HEAD_DH, 3.0 * 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh_dual(s, d, w, theta, U, tstride, po));
   const int64_t toff = (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,

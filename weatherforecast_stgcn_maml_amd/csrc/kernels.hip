@@ -21,7 +21,7 @@ namespace smaml {
 
 using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-contiguous)
 using CfgGate = GemmCfg<128, 128, 4, 1, true, true>;  // LSTM forward: wave = 32 rows x 4 gates
-using CfgNN = GemmCfg<128, 128, 4, 1, true, false>;   // C = A . B   (B n-contiguous)
+using CfgNN = GemmCfg<64, 128, 2, 2, true, false>;    // C = A . B   (B n-contiguous)
 using CfgTN = GemmCfg<128, 128, 2, 2, false, false>;  // C = A^T . B (split-K weight grads)
 
 // ------------------------------------------------------------------------------------
@@ -64,10 +64,11 @@ struct GcnA {
   int64_t sstride;
   const int* ec;
   const float* ev;
+  FastDiv rps_div;
   int rps, ell_rows, cin, R;
   __device__ __forceinline__ float4 operator()(int r, int k) const {
     if (r >= R || k >= cin) return f4zero();
-    const int g = r / rps, q = r - g * rps;
+    const int g = (int)rps_div.div((uint32_t)r), q = r - g * rps;
     const float* base = tab ? tab[g] : buf + (int64_t)g * sstride;
     if (q < ell_rows) {
       float4 s = f4zero();
@@ -82,36 +83,46 @@ struct GcnA {
   }
 };
 
-__global__ __launch_bounds__(NT) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
-                                                  float* __restrict__ out, int cout, int remap, int relu,
-                                                  int T, int N, int B) {
-  __shared__ float smem[CfgNT::SMEM_FLOATS];
-  const int m0 = blockIdx.x * CfgNT::BM, n0 = blockIdx.y * CfgNT::BN;
-  Acc<CfgNT> acc;
+// 8 waves, 128 rows x 256 cols: one workgroup covers a row block's whole Hc=256 output,
+// so each input row is read once.
+using CfgGcn = GemmCfg<128, 256, 2, 4, true, true>;
+
+__global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
+                                                           float* __restrict__ out, int cout, int remap, int relu,
+                                                           int T, int N, int B, FastDiv ndiv, FastDiv bdiv) {
+  __shared__ float smem[CfgGcn::SMEM_FLOATS];
+  const int m0 = blockIdx.x * CfgGcn::BM, n0 = blockIdx.y * CfgGcn::BN;
+  Acc<CfgGcn> acc;
   acc.zero();
-  gemm_mainloop<CfgNT>(la, lb, m0, n0, 0, la.cin, acc, smem);
-  const int M = B * N;
+  gemm_mainloop<CfgGcn>(la, lb, m0, n0, 0, la.cin, acc, smem);
+  const int64_t M = (int64_t)B * N;
+  float bc[CfgGcn::WTN];
 #pragma unroll
-  for (int i = 0; i < CfgNT::WTM; ++i)
+  for (int j = 0; j < CfgGcn::WTN; ++j) {
+    const int c = n0 + acc_col<CfgGcn>(j);
+    bc[j] = c < cout ? bias[c] : 0.f;
+  }
 #pragma unroll
-    for (int j = 0; j < CfgNT::WTN; ++j) {
-      const int c = n0 + acc_col<CfgNT>(j);
-      if (c >= cout) continue;
-      const float bc = bias[c];
+  for (int i = 0; i < CfgGcn::WTM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + acc_row<CfgNT>(i, r);
-        if (row >= la.R) continue;
-        float v = acc.v[i][j][r] + bc;
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + acc_row<CfgGcn>(i, r);
+      if (row >= la.R) continue;
+      int64_t orow = row;
+      if (remap) {  // [g][t*N+n] -> [z][t][s*N+n]
+        const int g = (int)la.rps_div.div((uint32_t)row), q = row - g * la.rps;
+        const int z = (int)bdiv.div((uint32_t)g), s = g - z * B;
+        const int t = (int)ndiv.div((uint32_t)q), n = q - t * N;
+        orow = ((int64_t)z * T + t) * M + (int64_t)s * N + n;
+      }
+      float* o = out + orow * cout;
+#pragma unroll
+      for (int j = 0; j < CfgGcn::WTN; ++j) {
+        const int c = n0 + acc_col<CfgGcn>(j);
+        if (c >= cout) continue;
+        float v = acc.v[i][j][r] + bc[j];
         if (relu) v = fmaxf(v, 0.f);
-        int64_t orow = row;
-        if (remap) {  // [g][t*N+n] -> [z][t][s*N+n]
-          const int g = row / la.rps, q = row - g * la.rps;
-          const int z = g / B, s = g - z * B;
-          const int t = q / N, n = q - t * N;
-          orow = ((int64_t)z * T + t) * M + (int64_t)s * N + n;
-        }
-        out[orow * cout + c] = v;
+        o[c] = v;
       }
     }
 }
@@ -127,14 +138,15 @@ void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, co
   la.sstride = (int64_t)rows_per_sample * cin;
   la.ec = ell_c;
   la.ev = ell_v;
+  la.rps_div = FastDiv((uint32_t)rows_per_sample);
   la.rps = rows_per_sample;
   la.ell_rows = ell_rows;
   la.cin = cin;
   la.R = Zb * rows_per_sample;
   RowMajorKC lb{W, cout, cin};
-  dim3 grid((la.R + CfgNT::BM - 1) / CfgNT::BM, (cout + CfgNT::BN - 1) / CfgNT::BN);
-  k_gcn_layer<<<grid, NT, 0, s>>>(la, lb, b, dst, cout, remap_lstm ? 1 : 0, relu ? 1 : 0, d.T, d.N,
-                                  B);
+  dim3 grid((la.R + CfgGcn::BM - 1) / CfgGcn::BM, (cout + CfgGcn::BN - 1) / CfgGcn::BN);
+  k_gcn_layer<<<grid, CfgGcn::NTH, 0, s>>>(la, lb, b, dst, cout, remap_lstm ? 1 : 0, relu ? 1 : 0, d.T, d.N, B,
+                                           FastDiv((uint32_t)d.N), FastDiv((uint32_t)B));
 }
 
 // ====================================================================================
@@ -346,7 +358,7 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
   // dH (top layer) holds zeros for t < T-1 (memset by the driver); write t = T-1.
   float* out = w.dH + (int64_t)(d.T - 1) * w.M * d.H;
   dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
-  k_gemm_nn<<<grid, NT, 0, s>>>(w.dpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, tstride, po.wo, d.H,
+  k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(w.dpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, tstride, po.wo, d.H,
                                 out, (int64_t)d.T * w.M * d.H);
 }
 
@@ -354,7 +366,7 @@ void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, 
                const LayerOff& lo) {
   const int rows = d.T * w.M;
   dim3 grid((rows + CfgNN::BM - 1) / CfgNN::BM, (lo.cin + CfgNN::BN - 1) / CfgNN::BN, w.Z);
-  k_gemm_nn<<<grid, NT, 0, s>>>(w.dG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, tstride, lo.wih,
+  k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(w.dG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, tstride, lo.wih,
                                 lo.cin, w.dH, (int64_t)rows * lo.cin);
 }
 
@@ -368,7 +380,7 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, co
                                                       float* __restrict__ dc, const float* __restrict__ Gs,
                                                       const float* __restrict__ Cs,
                                                       const float* __restrict__ theta, int64_t tstride,
-                                                      LayerOff lo, int T, int M, int H, int t) {
+                                                      LayerOff lo, int T, int M, int H, int t, int dh_zero) {
   __shared__ float smem[CfgNN::SMEM_FLOATS];
   const int z = blockIdx.z;
   const int G4 = 4 * H;
@@ -393,7 +405,7 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, co
       const int m = m0 + acc_row<CfgNN>(0, r);
       if (m >= M) continue;
       const int64_t row = bt + m;
-      const float dh = acc.v[0][jj][r] + dH[row * H + j];
+      const float dh = acc.v[0][jj][r] + (dh_zero ? 0.f : dH[row * H + j]);
       const float* g = Gs + row * G4;
       const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
       const float c = Cs[row * H + j];
@@ -415,8 +427,10 @@ void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, in
                           int64_t tstride, const LayerOff& lo) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
-  k_lstm_bwd_step<<<grid, NT, 0, s>>>(w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz,
-                                      theta, tstride, lo, d.T, w.M, d.H, t);
+  // the top layer's dH is zero except at t = T-1 (written by the head backward)
+  const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
+  k_lstm_bwd_step<<<grid, CfgNN::NTH, 0, s>>>(w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz,
+                                              theta, tstride, lo, d.T, w.M, d.H, t, dh_zero);
 }
 
 // ====================================================================================

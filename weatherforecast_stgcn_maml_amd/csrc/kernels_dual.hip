@@ -17,7 +17,7 @@ namespace smaml {
 
 using CfgGateD = GemmCfg<128, 128, 4, 1, true, true>;
 using CfgNTD = GemmCfg<128, 128, 2, 2, true, true>;
-using CfgNND = GemmCfg<128, 128, 4, 1, true, false>;
+using CfgNND = GemmCfg<64, 128, 2, 2, true, false>;
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
 #pragma unroll
@@ -233,7 +233,7 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
                          int64_t tstride, const ParamOff& po) {
   const int64_t off = (int64_t)(d.T - 1) * w.M * d.H;
   dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
-  k_gemm_nn_dual<<<grid, NT, 0, s>>>(w.dpred, w.Rdpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, U, tstride, po.wo,
+  k_gemm_nn_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dpred, w.Rdpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, U, tstride, po.wo,
                                      d.H, w.dH + off, w.RdH + off, (int64_t)d.T * w.M * d.H);
 }
 
@@ -241,7 +241,7 @@ void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* th
                     const LayerOff& lo) {
   const int rows = d.T * w.M;
   dim3 grid((rows + CfgNND::BM - 1) / CfgNND::BM, (lo.cin + CfgNND::BN - 1) / CfgNND::BN, w.Z);
-  k_gemm_nn_dual<<<grid, NT, 0, s>>>(w.dG, w.RdG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, U, tstride,
+  k_gemm_nn_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dG, w.RdG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, U, tstride,
                                      lo.wih, lo.cin, w.dH, w.RdH, (int64_t)rows * lo.cin);
 }
 
@@ -252,7 +252,8 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, fl
                                                       const float* __restrict__ Gs, const float* __restrict__ Cs,
                                                       const float* __restrict__ RGs, const float* __restrict__ RCs,
                                                       const float* __restrict__ theta, const float* __restrict__ U,
-                                                      int64_t tstride, LayerOff lo, int T, int M, int H, int t) {
+                                                      int64_t tstride, LayerOff lo, int T, int M, int H, int t,
+                                                      int dh_zero) {
   __shared__ float smem[CfgNND::SMEM_FLOATS];
   const int z = blockIdx.z;
   const int G4 = 4 * H;
@@ -288,8 +289,8 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, fl
       const int m = m0 + acc_row<CfgNND>(0, r);
       if (m >= M) continue;
       const int64_t row = bt + m;
-      const float dh = ap.v[0][jj][r] + dH[row * H + j];
-      const float rdh = at.v[0][jj][r] + RdH[row * H + j];
+      const float dh = ap.v[0][jj][r] + (dh_zero ? 0.f : dH[row * H + j]);
+      const float rdh = at.v[0][jj][r] + (dh_zero ? 0.f : RdH[row * H + j]);
       const float* g = Gs + row * G4;
       const float* rg = RGs + row * G4;
       const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
@@ -325,8 +326,10 @@ void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, in
                           const float* U, int64_t tstride, const LayerOff& lo) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
-  k_lstm_bwd_dual<<<grid, NT, 0, s>>>(w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
-                                      w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, d.H, t);
+  const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
+  k_lstm_bwd_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4,
+                                               w.Cs + l * lsz, w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride,
+                                               lo, d.T, w.M, d.H, t, dh_zero);
 }
 
 // ====================================================================================
