@@ -53,7 +53,9 @@ int check_dims(const smaml_dims* d) {
     return fail(SMAML_EINVAL, "non-positive dimension");
   if (d->input_channels % 4 || d->hidden_channels % 4)
     return fail(SMAML_EINVAL, "input/hidden channels must be multiples of 4");
-  if (d->lstm_hidden_size % 32) return fail(SMAML_EINVAL, "lstm_hidden_size must be a multiple of 32");
+  if (d->lstm_hidden_size != 32 && d->lstm_hidden_size != 64 && d->lstm_hidden_size != 128 &&
+      d->lstm_hidden_size != 256)
+    return fail(SMAML_EINVAL, "lstm_hidden_size must be 32, 64, 128 or 256");
   if (d->forecast_horizon * d->output_channels > 128)
     return fail(SMAML_EINVAL, "forecast_horizon*output_channels must be <= 128");
   if (d->output_channels > d->input_channels)
@@ -180,6 +182,9 @@ struct smaml_ctx {
   float *so_u = nullptr, *so_hu = nullptr;
   float *so_theta = nullptr, *so_grad = nullptr, *so_norm = nullptr, *so_coef = nullptr;
   int64_t so_store_cap = 0, so_nc_cap = 0;
+  float* so_F = nullptr;  // [K][Z][T][M][Hc] GCN features of every inner step (null: recompute)
+  int64_t so_F_cap = 0;
+  float* F_main = nullptr;  // the workspace's own F buffer
 };
 
 namespace {
@@ -191,6 +196,9 @@ int ensure_device(smaml_ctx* c) {
 
 int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   const int zb = Z * B;
+  // per-task activation slabs are addressed with 32-bit offsets inside the kernels
+  if ((int64_t)c->d.T * B * c->d.N * 4 * c->d.H >= (1ll << 31))
+    return fail(SMAML_EINVAL, "batch too large: T*B*N*4H must stay below 2^31 per task");
   so = so || c->so_cap;
   if (zb <= c->zb_cap && Z <= c->z_cap && so == c->so_cap) return SMAML_OK;
   const int zbc = std::max(zb, c->zb_cap), zc = std::max(Z, c->z_cap);
@@ -270,6 +278,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   c->zb_cap = zbc;
   c->z_cap = zc;
   c->so_cap = so;
+  c->F_main = w.F;
   c->so_u = so_u;
   c->so_hu = so_hu;
   if (so_hu) HIP_TRY(hipMemset(so_hu, 0, (size_t)zc * c->po.P * 4));
@@ -278,7 +287,26 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
 
 // Per-step stores of the second-order sweep: theta_k and g_k [K][Z][P], |g_k| and the
 // clip coefficient [K][Z].
-int ensure_so_store(smaml_ctx* c, int K, int Z) {
+int ensure_so_store(smaml_ctx* c, int K, int Z, int B) {
+  // GCN features of each inner step, kept for the second-order sweep (weight-independent, F2).
+  // Best effort: without room the sweep recomputes them.
+  const int64_t fneed = (int64_t)K * Z * B * c->d.T * c->d.N * c->d.Hc;
+  if (fneed > c->so_F_cap) {
+    if (c->so_F) {
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipFree(c->so_F));
+      c->so_F = nullptr;
+      c->so_F_cap = 0;
+    }
+    size_t freeb = 0, totb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totb));
+    if ((int64_t)freeb > fneed * 4 + (4ll << 30) && hipMalloc((void**)&c->so_F, fneed * 4) == hipSuccess) {
+      c->so_F_cap = fneed;
+    } else {
+      (void)hipGetLastError();
+      c->so_F = nullptr;
+    }
+  }
   const int64_t need = (int64_t)K * Z * c->po.P;
   if (need <= c->so_store_cap && (int64_t)K * Z <= c->so_nc_cap) return SMAML_OK;
   if (c->so_theta) {
@@ -325,6 +353,7 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.B = B;
   c->w.M = B * c->d.N;
   c->w.lblocks = (c->w.M + 127) / 128;
+  c->w.F = c->F_main;
 }
 
 #define TIMED(c, s, cat, fl, stmt)                              \
@@ -394,14 +423,14 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
 
 // Primal recompute + tangent along U (second-order sweep), GCN features recomputed.
 int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride,
-                     const float* const* xtab_dev) {
+                     const float* const* xtab_dev, bool gcn_cached) {
   const Dims& d = c->d;
   Work& w = c->w;
   const int rps = d.T * d.N;
   const int zb = w.Z * w.B;
   const float* src = nullptr;
   float* bufs[2] = {w.gcnA, w.gcnB};
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 4 && !gcn_cached; ++k) {
     const bool last = k == 3;
     float* dst = last ? w.F : bufs[k & 1];
     TIMED(c, s, C_GCN, 2.0 * zb * rps * c->go.cin[k] * d.Hc,
@@ -573,6 +602,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->so_grad) (void)hipFree(c->so_grad);
   if (c->so_norm) (void)hipFree(c->so_norm);
   if (c->so_coef) (void)hipFree(c->so_coef);
+  if (c->so_F) (void)hipFree(c->so_F);
   for (auto& r : c->tm.recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -682,7 +712,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const int Z = (int)c->feats.size();
   const int B = batch;
   TRY(reserve(c, Z, B, order == 2));
-  if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z));
+  if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z, B));
   set_work(c, Z, B);
   // sample window table for every step (support steps then the query batch)
   const int64_t nptr = (int64_t)(steps + 1) * Z * B;
@@ -714,8 +744,10 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const bool so = order == 2;
   for (int k = 0; k < steps; ++k) {
     const float* const* xt = c->xtab + (int64_t)k * Z * B;
-    if (so)
+    if (so) {
       HIP_TRY(hipMemcpyAsync(c->so_theta + (int64_t)k * Z * P, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
+      c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
+    }
     TRY(run_forward(c, s, c->fast, P, xt));
     TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
     TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
@@ -735,6 +767,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     }
   }
   const float* const* xq = c->xtab + (int64_t)steps * Z * B;
+  c->w.F = c->F_main;
   TRY(run_forward(c, s, c->fast, P, xq));
   TIMED(c, s, C_HEAD, head_fl,
         launch_head_loss(s, d, c->w, c->fast, P, c->po, xq, 2.f * inv * query_scale, true));
@@ -756,12 +789,14 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       TIMED(c, s, C_MISC, 0,
             launch_so_dir(s, V, gk, P, Z, c->w.sqpart, c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z,
                           max_norm, c->so_u));
-      TRY(run_forward_dual(c, s, th, c->so_u, P, xt));
+      c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
+      TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
       TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
     }
     TIMED(c, s, C_MISC, 0, launch_sum_tasks(s, V, P, Z, meta_grad));
+    c->w.F = c->F_main;
   }
   if (fast_out) HIP_TRY(hipMemcpyAsync(fast_out, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipGetLastError());

@@ -154,10 +154,11 @@ void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, co
 //   pre[m, g*H+j] = [x_t | h_{t-1}][m] . [W_ih | W_hh][g*H+j] + b_ih + b_hh
 // Column tile = 32 hidden units x 4 gates, so each lane holds i,f,g,o of the same
 // (row, unit) in the same accumulator register and the cell update is in-register.
+template <int H>
 struct LstmFwdA {
   const float* X;   // layer input at time t: [M][cin]
   const float* Hp;  // h_{t-1}: [M][H] (nullptr at t = 0)
-  int M, cin, H;
+  int M, cin;
   __device__ __forceinline__ float4 operator()(int m, int k) const {
     if (m >= M) return f4zero();
     if (k < cin) return ld4(X + (int64_t)m * cin + k);
@@ -167,10 +168,11 @@ struct LstmFwdA {
   }
 };
 
+template <int H>
 struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + ug*32 + jj
   const float* Wih;
   const float* Whh;
-  int cin, H;
+  int cin;
   __device__ __forceinline__ float4 operator()(int n, int k) const {
     const int ug = n >> 7, rem = n & 127, g = rem >> 5, j = ug * 32 + (rem & 31);
     if (j >= H) return f4zero();
@@ -182,54 +184,61 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
   }
 };
 
+// Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
+template <int H>
 __global__ __launch_bounds__(NT) void k_lstm_fwd_step(const float* __restrict__ X, float* __restrict__ Hs,
                                                       float* __restrict__ Cs, float* __restrict__ Gs,
                                                       const float* __restrict__ theta, int64_t tstride,
-                                                      LayerOff lo, int T, int M, int H, int t) {
+                                                      LayerOff lo, int T, int M, int t) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
   const int z = blockIdx.z;
   const float* th = theta + (int64_t)z * tstride;
   const int cin = lo.cin;
-  LstmFwdA la;
-  la.X = X + ((int64_t)z * T + t) * M * cin;
-  la.Hp = t > 0 ? Hs + ((int64_t)z * T + t - 1) * M * H : nullptr;
+  const int64_t slab = (int64_t)z * T * M;
+  float* Gz = Gs + slab * (4 * H);
+  float* Cz = Cs + slab * H;
+  float* Hz = Hs + slab * H;
+  LstmFwdA<H> la;
+  la.X = X + (slab + (int64_t)t * M) * cin;
+  la.Hp = t > 0 ? Hz + (int64_t)(t - 1) * M * H : nullptr;
   la.M = M;
   la.cin = cin;
-  la.H = H;
-  LstmFwdB lb{th + lo.wih, th + lo.whh, cin, H};
-  const int m0 = blockIdx.x * CfgGate::BM, n0 = blockIdx.y * CfgGate::BN;
+  LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
+  int tm, ug;
+  if (!gate_tile((M + CfgGate::BM - 1) / CfgGate::BM, (H + 31) / 32, tm, ug)) return;
+  const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
   acc.zero();
   gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
 
-  const int j = blockIdx.y * 32 + (threadIdx.x & 31);
+  const int j = ug * 32 + (threadIdx.x & 31);
   if (j >= H) return;
-  const float* bih = th + lo.bih;
-  const float* bhh = th + lo.bhh;
   float bsum[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) bsum[g] = bih[g * H + j] + bhh[g * H + j];
-  const int64_t base_t = ((int64_t)z * T + t) * M;
-  const float* Cp = t > 0 ? Cs + ((int64_t)z * T + t - 1) * M * H : nullptr;
+  for (int g = 0; g < 4; ++g) bsum[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
+  const int rb = m0 + acc_row<CfgGate>(0, 0);
+  const bool full = m0 + CfgGate::BM <= M;
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int m = m0 + acc_row<CfgGate>(0, r);
-    if (m >= M) continue;
-    const float pi = acc.v[0][0][r] + bsum[0];
-    const float pf = acc.v[0][1][r] + bsum[1];
-    const float pg = acc.v[0][2][r] + bsum[2];
-    const float po = acc.v[0][3][r] + bsum[3];
-    const float gi = sigmoidf_(pi), gf = sigmoidf_(pf), gg = tanhf(pg), go = sigmoidf_(po);
-    const float cp = Cp ? Cp[(int64_t)m * H + j] : 0.f;
+    const int m = rb + racc(r);
+    if (!full && m >= M) continue;
+    const uint32_t row = tM + (uint32_t)m;
+    const uint32_t oh = row * H + j;
+    const uint32_t og = row * (4 * H) + j;
+    const float gi = sigmoidf_(acc.v[0][0][r] + bsum[0]);
+    const float gf = sigmoidf_(acc.v[0][1][r] + bsum[1]);
+    const float gg = tanhf_(acc.v[0][2][r] + bsum[2]);
+    const float go = sigmoidf_(acc.v[0][3][r] + bsum[3]);
+    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
     const float c = gf * cp + gi * gg;
-    const float h = go * tanhf(c);
-    float* grow = Gs + (base_t + m) * (4 * H);
-    grow[j] = gi;
-    grow[H + j] = gf;
-    grow[2 * H + j] = gg;
-    grow[3 * H + j] = go;
-    Cs[(base_t + m) * H + j] = c;
-    Hs[(base_t + m) * H + j] = h;
+    const float h = go * tanhf_(c);
+    stb(Gz, 4u * (og), gi);
+    stb(Gz, 4u * (og + H), gf);
+    stb(Gz, 4u * (og + 2 * H), gg);
+    stb(Gz, 4u * (og + 3 * H), go);
+    stb(Cz, 4u * (oh), c);
+    stb(Hz, 4u * (oh), h);
   }
 }
 
@@ -240,8 +249,9 @@ void launch_lstm_fwd_step(hipStream_t s, const Dims& d, const Work& w, int l, in
   float* Hs = w.Hs + (int64_t)l * lsz;
   float* Cs = w.Cs + (int64_t)l * lsz;
   float* Gs = w.Gs + (int64_t)l * lsz * 4;
-  dim3 grid((w.M + CfgGate::BM - 1) / CfgGate::BM, (d.H + 31) / 32, w.Z);
-  k_lstm_fwd_step<<<grid, NT, 0, s>>>(X, Hs, Cs, Gs, theta, tstride, lo, d.T, w.M, d.H, t);
+  const int ntm = (w.M + CfgGate::BM - 1) / CfgGate::BM;
+  dim3 grid((ntm + 7) / 8 * 8 * ((d.H + 31) / 32), 1, w.Z);
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, NT, 0, s>>>(X, Hs, Cs, Gs, theta, tstride, lo, d.T, w.M, t));
 }
 
 // ====================================================================================
@@ -376,49 +386,57 @@ void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, 
 //   dc = dc_carry + dh * o * (1 - tanh(c_t)^2)
 //   dG_t = [dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tanh(c_t)*o(1-o)]
 //   dc_carry = dc * f
+template <int H>
 __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, const float* __restrict__ dH,
                                                       float* __restrict__ dc, const float* __restrict__ Gs,
                                                       const float* __restrict__ Cs,
                                                       const float* __restrict__ theta, int64_t tstride,
-                                                      LayerOff lo, int T, int M, int H, int t, int dh_zero) {
+                                                      LayerOff lo, int T, int M, int t, int dh_zero) {
   __shared__ float smem[CfgNN::SMEM_FLOATS];
+  constexpr int G4 = 4 * H;
   const int z = blockIdx.z;
-  const int G4 = 4 * H;
   const int m0 = blockIdx.x * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
+  const int64_t slab = (int64_t)z * T * M;
+  float* dGz = dG + slab * G4;
+  const float* dHz = dH + slab * H;
+  const float* Gz = Gs + slab * G4;
+  const float* Cz = Cs + slab * H;
+  float* dcz = dc + (int64_t)z * M * H;
   Acc<CfgNN> acc;
   acc.zero();
   if (t + 1 < T) {
-    RowMajorKC la{dG + ((int64_t)z * T + t + 1) * M * G4, M, G4};
+    RowMajorKC la{dGz + (int64_t)(t + 1) * M * G4, M, G4};
     RowMajorMC lb{theta + (int64_t)z * tstride + lo.whh, G4, H};
     gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, G4, acc, smem);
   }
-  const int64_t bt = ((int64_t)z * T + t) * M;
-  const float* Cprev = t > 0 ? Cs + ((int64_t)z * T + t - 1) * M * H : nullptr;
-  float* dcz = dc + (int64_t)z * M * H;
   const bool first = (t == T - 1);
+  const bool full = m0 + CfgNN::BM <= M;
+  const int rb = m0 + acc_row<CfgNN>(0, 0);
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
   for (int jj = 0; jj < CfgNN::WTN; ++jj) {
     const int j = n0 + acc_col<CfgNN>(jj);
     if (j >= H) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + acc_row<CfgNN>(0, r);
-      if (m >= M) continue;
-      const int64_t row = bt + m;
-      const float dh = acc.v[0][jj][r] + (dh_zero ? 0.f : dH[row * H + j]);
-      const float* g = Gs + row * G4;
-      const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
-      const float c = Cs[row * H + j];
-      const float tc = tanhf(c);
-      const float cp = Cprev ? Cprev[(int64_t)m * H + j] : 0.f;
-      const float dcin = first ? 0.f : dcz[(int64_t)m * H + j];
+      const int m = rb + racc(r);
+      if (!full && m >= M) continue;
+      const uint32_t row = tM + (uint32_t)m;
+      const uint32_t oh = row * H + j;
+      const uint32_t og = row * G4 + j;
+      const uint32_t oc = (uint32_t)m * H + j;
+      const float dh = acc.v[0][jj][r] + (dh_zero ? 0.f : ldb(dHz, 4u * (oh)));
+      const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
+      const float c = ldb(Cz, 4u * (oh));
+      const float tc = tanhf_(c);
+      const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+      const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
       const float dct = dcin + dh * go * (1.f - tc * tc);
-      float* dg = dG + row * G4;
-      dg[j] = dct * gg * gi * (1.f - gi);
-      dg[H + j] = dct * cp * gf * (1.f - gf);
-      dg[2 * H + j] = dct * gi * (1.f - gg * gg);
-      dg[3 * H + j] = dh * tc * go * (1.f - go);
-      dcz[(int64_t)m * H + j] = dct * gf;
+      stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
+      stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
+      stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
+      stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
+      stb(dcz, 4u * (oc), dct * gf);
     }
   }
 }
@@ -429,8 +447,9 @@ void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, in
   dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
   // the top layer's dH is zero except at t = T-1 (written by the head backward)
   const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
-  k_lstm_bwd_step<<<grid, CfgNN::NTH, 0, s>>>(w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz,
-                                              theta, tstride, lo, d.T, w.M, d.H, t, dh_zero);
+  SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT><<<grid, CfgNN::NTH, 0, s>>>(
+                            w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz, theta, tstride,
+                            lo, d.T, w.M, t, dh_zero));
 }
 
 // ====================================================================================

@@ -33,24 +33,34 @@ __device__ __forceinline__ float block_sum_f(float v, float* red) {
 }
 
 // ====================================================================================
+template <int H>
 __global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ X, const float* __restrict__ RX,
                                                       float* __restrict__ Hs, float* __restrict__ Cs,
                                                       float* __restrict__ Gs, float* __restrict__ RHs,
                                                       float* __restrict__ RCs, float* __restrict__ RGs,
                                                       const float* __restrict__ theta, const float* __restrict__ U,
-                                                      int64_t tstride, LayerOff lo, int T, int M, int H, int t) {
+                                                      int64_t tstride, LayerOff lo, int T, int M, int t) {
   __shared__ float smem[CfgGateD::SMEM_FLOATS];
+  constexpr int G4 = 4 * H;
   const int z = blockIdx.z;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
   const int cin = lo.cin;
-  const int64_t bt = ((int64_t)z * T + t) * M;
-  const float* xt = X + bt * cin;
-  const float* rxt = RX ? RX + bt * cin : nullptr;
-  const float* hp = t > 0 ? Hs + (bt - M) * H : nullptr;
-  const float* rhp = t > 0 ? RHs + (bt - M) * H : nullptr;
+  const int64_t slab = (int64_t)z * T * M;
+  float* Gz = Gs + slab * G4;
+  float* RGz = RGs + slab * G4;
+  float* Cz = Cs + slab * H;
+  float* RCz = RCs + slab * H;
+  float* Hz = Hs + slab * H;
+  float* RHz = RHs + slab * H;
+  const float* xt = X + (slab + (int64_t)t * M) * cin;
+  const float* rxt = RX ? RX + (slab + (int64_t)t * M) * cin : nullptr;
+  const float* hp = t > 0 ? Hz + (int64_t)(t - 1) * M * H : nullptr;
+  const float* rhp = t > 0 ? RHz + (int64_t)(t - 1) * M * H : nullptr;
   const int wh = hp ? H : 0;
-  const int m0 = blockIdx.x * CfgGateD::BM, n0 = blockIdx.y * CfgGateD::BN;
+  int tm, ug;
+  if (!gate_tile((M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 31) / 32, tm, ug)) return;
+  const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
 
   Acc<CfgGateD> ap, at;
   ap.zero();
@@ -66,7 +76,7 @@ __global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ 
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
   }
-  const int j = blockIdx.y * 32 + (threadIdx.x & 31);
+  const int j = ug * 32 + (threadIdx.x & 31);
   if (j >= H) return;
   float bp[4], bu[4];
 #pragma unroll
@@ -74,42 +84,41 @@ __global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ 
     bp[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
     bu[g] = u[lo.bih + g * H + j] + u[lo.bhh + g * H + j];
   }
-  const float* Cp = t > 0 ? Cs + (bt - M) * H : nullptr;
-  const float* RCp = t > 0 ? RCs + (bt - M) * H : nullptr;
+  const int rb = m0 + acc_row<CfgGateD>(0, 0);
+  const bool full = m0 + CfgGateD::BM <= M;
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int m = m0 + acc_row<CfgGateD>(0, r);
-    if (m >= M) continue;
+    const int m = rb + racc(r);
+    if (!full && m >= M) continue;
+    const uint32_t row = tM + (uint32_t)m;
+    const uint32_t oh = row * H + j;
+    const uint32_t og = row * G4 + j;
     const float gi = sigmoidf_(ap.v[0][0][r] + bp[0]);
     const float gf = sigmoidf_(ap.v[0][1][r] + bp[1]);
-    const float gg = tanhf(ap.v[0][2][r] + bp[2]);
+    const float gg = tanhf_(ap.v[0][2][r] + bp[2]);
     const float go = sigmoidf_(ap.v[0][3][r] + bp[3]);
     const float ri = gi * (1.f - gi) * (at.v[0][0][r] + bu[0]);
     const float rf = gf * (1.f - gf) * (at.v[0][1][r] + bu[1]);
     const float rg = (1.f - gg * gg) * (at.v[0][2][r] + bu[2]);
     const float ro = go * (1.f - go) * (at.v[0][3][r] + bu[3]);
-    const float cp = Cp ? Cp[(int64_t)m * H + j] : 0.f;
-    const float rcp = RCp ? RCp[(int64_t)m * H + j] : 0.f;
+    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+    const float rcp = t > 0 ? ldb(RCz, 4u * (oh - (uint32_t)M * H)) : 0.f;
     const float c = gf * cp + gi * gg;
     const float rc = rf * cp + gf * rcp + ri * gg + gi * rg;
-    const float tc = tanhf(c);
-    const float h = go * tc;
-    const float rh = ro * tc + go * (1.f - tc * tc) * rc;
-    const int64_t row = bt + m;
-    float* grow = Gs + row * (4 * H);
-    float* rgrow = RGs + row * (4 * H);
-    grow[j] = gi;
-    grow[H + j] = gf;
-    grow[2 * H + j] = gg;
-    grow[3 * H + j] = go;
-    rgrow[j] = ri;
-    rgrow[H + j] = rf;
-    rgrow[2 * H + j] = rg;
-    rgrow[3 * H + j] = ro;
-    Cs[row * H + j] = c;
-    Hs[row * H + j] = h;
-    RCs[row * H + j] = rc;
-    RHs[row * H + j] = rh;
+    const float tc = tanhf_(c);
+    stb(Gz, 4u * (og), gi);
+    stb(Gz, 4u * (og + H), gf);
+    stb(Gz, 4u * (og + 2 * H), gg);
+    stb(Gz, 4u * (og + 3 * H), go);
+    stb(RGz, 4u * (og), ri);
+    stb(RGz, 4u * (og + H), rf);
+    stb(RGz, 4u * (og + 2 * H), rg);
+    stb(RGz, 4u * (og + 3 * H), ro);
+    stb(Cz, 4u * (oh), c);
+    stb(Hz, 4u * (oh), go * tc);
+    stb(RCz, 4u * (oh), rc);
+    stb(RHz, 4u * (oh), ro * tc + go * (1.f - tc * tc) * rc);
   }
 }
 
@@ -118,9 +127,12 @@ void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, in
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   const float* X = (l == 0) ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
   const float* RX = (l == 0) ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
-  dim3 grid((w.M + CfgGateD::BM - 1) / CfgGateD::BM, (d.H + 31) / 32, w.Z);
-  k_lstm_fwd_dual<<<grid, NT, 0, s>>>(X, RX, w.Hs + l * lsz, w.Cs + l * lsz, w.Gs + l * lsz * 4, w.RHs + l * lsz,
-                                      w.RCs + l * lsz, w.RGs + l * lsz * 4, theta, U, tstride, lo, d.T, w.M, d.H, t);
+  const int ntm = (w.M + CfgGateD::BM - 1) / CfgGateD::BM;
+  dim3 grid((ntm + 7) / 8 * 8 * ((d.H + 31) / 32), 1, w.Z);
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT><<<grid, NT, 0, s>>>(X, RX, w.Hs + l * lsz, w.Cs + l * lsz,
+                                                                w.Gs + l * lsz * 4, w.RHs + l * lsz, w.RCs + l * lsz,
+                                                                w.RGs + l * lsz * 4, theta, U, tstride, lo, d.T,
+                                                                w.M, t));
 }
 
 // ====================================================================================
@@ -246,78 +258,89 @@ void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* th
 }
 
 // ====================================================================================
+template <int H>
 __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, float* __restrict__ RdG,
                                                       const float* __restrict__ dH, const float* __restrict__ RdH,
                                                       float* __restrict__ dc, float* __restrict__ Rdc,
                                                       const float* __restrict__ Gs, const float* __restrict__ Cs,
                                                       const float* __restrict__ RGs, const float* __restrict__ RCs,
                                                       const float* __restrict__ theta, const float* __restrict__ U,
-                                                      int64_t tstride, LayerOff lo, int T, int M, int H, int t,
+                                                      int64_t tstride, LayerOff lo, int T, int M, int t,
                                                       int dh_zero) {
   __shared__ float smem[CfgNND::SMEM_FLOATS];
+  constexpr int G4 = 4 * H;
   const int z = blockIdx.z;
-  const int G4 = 4 * H;
   const int m0 = blockIdx.x * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
+  const int64_t slab = (int64_t)z * T * M;
+  float* dGz = dG + slab * G4;
+  float* RdGz = RdG + slab * G4;
+  const float* dHz = dH + slab * H;
+  const float* RdHz = RdH + slab * H;
+  const float* Gz = Gs + slab * G4;
+  const float* RGz = RGs + slab * G4;
+  const float* Cz = Cs + slab * H;
+  const float* RCz = RCs + slab * H;
+  float* dcz = dc + (int64_t)z * M * H;
+  float* rdcz = Rdc + (int64_t)z * M * H;
   Acc<CfgNND> ap, at;
   ap.zero();
   at.zero();
   if (t + 1 < T) {
-    const int64_t nx = ((int64_t)z * T + t + 1) * M * G4;
+    const int64_t nx = (int64_t)(t + 1) * M * G4;
     const float* W = theta + (int64_t)z * tstride + lo.whh;
     const float* UW = U + (int64_t)z * tstride + lo.whh;
     {
-      RowMajorKC la{dG + nx, M, G4};
+      RowMajorKC la{dGz + nx, M, G4};
       RowMajorMC lb{W, G4, H};
       gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, G4, ap, smem);
     }
     {
-      SegKC la{{RdG + nx, dG + nx, nullptr, nullptr}, {G4, G4, 0, 0}, M};
+      SegKC la{{RdGz + nx, dGz + nx, nullptr, nullptr}, {G4, G4, 0, 0}, M};
       SegMC lb{{W, UW}, {G4, G4}, H};
       gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, 2 * G4, at, smem);
     }
   }
-  const int64_t bt = ((int64_t)z * T + t) * M;
   const bool first = (t == T - 1);
-  float* dcz = dc + (int64_t)z * M * H;
-  float* rdcz = Rdc + (int64_t)z * M * H;
+  const bool full = m0 + CfgNND::BM <= M;
+  const int rb = m0 + acc_row<CfgNND>(0, 0);
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
   for (int jj = 0; jj < CfgNND::WTN; ++jj) {
     const int j = n0 + acc_col<CfgNND>(jj);
     if (j >= H) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + acc_row<CfgNND>(0, r);
-      if (m >= M) continue;
-      const int64_t row = bt + m;
-      const float dh = ap.v[0][jj][r] + (dh_zero ? 0.f : dH[row * H + j]);
-      const float rdh = at.v[0][jj][r] + (dh_zero ? 0.f : RdH[row * H + j]);
-      const float* g = Gs + row * G4;
-      const float* rg = RGs + row * G4;
-      const float gi = g[j], gf = g[H + j], gg = g[2 * H + j], go = g[3 * H + j];
-      const float ri = rg[j], rf = rg[H + j], rgg = rg[2 * H + j], ro = rg[3 * H + j];
-      const float c = Cs[row * H + j], rc = RCs[row * H + j];
-      const float cp = t > 0 ? Cs[(row - M) * H + j] : 0.f;
-      const float rcp = t > 0 ? RCs[(row - M) * H + j] : 0.f;
-      const float dcin = first ? 0.f : dcz[(int64_t)m * H + j];
-      const float rdcin = first ? 0.f : rdcz[(int64_t)m * H + j];
-      const float tc = tanhf(c);
+      const int m = rb + racc(r);
+      if (!full && m >= M) continue;
+      const uint32_t row = tM + (uint32_t)m;
+      const uint32_t oh = row * H + j;
+      const uint32_t og = row * G4 + j;
+      const uint32_t oc = (uint32_t)m * H + j;
+      const float dh = ap.v[0][jj][r] + (dh_zero ? 0.f : ldb(dHz, 4u * (oh)));
+      const float rdh = at.v[0][jj][r] + (dh_zero ? 0.f : ldb(RdHz, 4u * (oh)));
+      const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
+      const float ri = ldb(RGz, 4u * (og)), rf = ldb(RGz, 4u * (og + H)), rgg = ldb(RGz, 4u * (og + 2 * H)), ro = ldb(RGz, 4u * (og + 3 * H));
+      const float c = ldb(Cz, 4u * (oh)), rc = ldb(RCz, 4u * (oh));
+      const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+      const float rcp = t > 0 ? ldb(RCz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+      const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
+      const float rdcin = first ? 0.f : ldb(rdcz, 4u * (oc));
+      const float tc = tanhf_(c);
       const float s2 = 1.f - tc * tc;
       const float rtc = s2 * rc;
       const float dct = dcin + dh * go * s2;
       const float rdct = rdcin + rdh * go * s2 + dh * ro * s2 - 2.f * dh * go * tc * rtc;
       const float si = gi * (1.f - gi), sf = gf * (1.f - gf), so = go * (1.f - go), sg = 1.f - gg * gg;
-      float* d = dG + row * G4;
-      float* rd = RdG + row * G4;
-      d[j] = dct * gg * si;
-      d[H + j] = dct * cp * sf;
-      d[2 * H + j] = dct * gi * sg;
-      d[3 * H + j] = dh * tc * so;
-      rd[j] = rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri;
-      rd[H + j] = rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf;
-      rd[2 * H + j] = rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg;
-      rd[3 * H + j] = rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro;
-      dcz[(int64_t)m * H + j] = dct * gf;
-      rdcz[(int64_t)m * H + j] = rdct * gf + dct * rf;
+      stb(dGz, 4u * (og), dct * gg * si);
+      stb(dGz, 4u * (og + H), dct * cp * sf);
+      stb(dGz, 4u * (og + 2 * H), dct * gi * sg);
+      stb(dGz, 4u * (og + 3 * H), dh * tc * so);
+      stb(RdGz, 4u * (og), rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri);
+      stb(RdGz, 4u * (og + H), rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf);
+      stb(RdGz, 4u * (og + 2 * H), rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg);
+      stb(RdGz, 4u * (og + 3 * H), rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro);
+      stb(dcz, 4u * (oc), dct * gf);
+      stb(rdcz, 4u * (oc), rdct * gf + dct * rf);
     }
   }
 }
@@ -327,9 +350,9 @@ void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, in
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
   const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
-  k_lstm_bwd_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4,
-                                               w.Cs + l * lsz, w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride,
-                                               lo, d.T, w.M, d.H, t, dh_zero);
+  SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT><<<grid, CfgNND::NTH, 0, s>>>(
+                            w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
+                            w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, t, dh_zero));
 }
 
 // ====================================================================================

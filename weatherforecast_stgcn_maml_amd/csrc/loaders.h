@@ -93,7 +93,33 @@ struct WgB {
   }
 };
 
+// Gate nonlinearities. SMAML_FAST_GATES (default) uses the hardware transcendentals:
+// v_exp_f32 on x*log2(e) and v_rcp_f32 (1 ulp), and for tanh 1 - 2/(1+e^{2|x|}) with an odd
+// Taylor polynomial below |x| < 0.125 (no cancellation near 0). Relative error <~1e-6 per
+// evaluation (|x| < ~16), absolute error <~2e-7; the parity tests bound the end-to-end effect.
+#ifndef SMAML_FAST_GATES
+#define SMAML_FAST_GATES 1
+#endif
+#if SMAML_FAST_GATES
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float tanhf_(float x) {
+  const float a = fabsf(x);
+  float r;
+  if (a < 0.125f) {
+    const float x2 = x * x;
+    r = x * fmaf(x2, fmaf(x2, fmaf(x2, -0.053968254f, 0.13333334f), -0.33333334f), 1.0f);
+  } else {
+    const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * a);
+    r = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e), x);
+  }
+  return r;
+}
+#else
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
+#endif
 
 // Exact unsigned division by a run-time invariant d for n < 2^31 (one 64-bit multiply):
 // m = ceil(2^(32+s) / d), s = ceil(log2 d)  =>  n / d == (n * m) >> (32 + s).
@@ -111,5 +137,40 @@ struct FastDiv {
     return (uint32_t)(((unsigned __int128)n * m) >> (32 + s));
   }
 };
+
+// Uniform (SGPR) base + 32-bit byte offset: lets the compiler use global_* saddr addressing
+// with the constant part of the offset folded into the instruction's immediate.
+__device__ __forceinline__ float ldb(const float* base, uint32_t byteoff) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + byteoff);
+}
+__device__ __forceinline__ void stb(float* base, uint32_t byteoff, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + byteoff) = v;
+}
+
+// XCD-aware tile mapping for the gate GEMMs: the 4 unit-group workgroups of one row tile
+// are dispatched 8 apart (same XCD under round-robin placement: L2 sharing of the A rows)
+// and within 32 consecutive blocks. Grid: gridDim.x = ceil(ntm/8)*8 * ngrp (ngrp = 4H/128).
+// Speed-only: a different placement changes nothing but speed. Returns false for padding.
+__device__ __forceinline__ bool gate_tile(int ntm, int ngrp, int& tm, int& ug) {
+  const int L = blockIdx.x;
+  const int per = 8 * ngrp;
+  const int q = L / per, rem = L - q * per;
+  ug = rem >> 3;
+  tm = q * 8 + (rem & 7);
+  return tm < ntm;
+}
+
+// Row offset (within the 32-row tile) of accumulator register r: (r&3) + 8*(r>>2).
+__device__ __forceinline__ constexpr int racc(int r) { return (r & 3) + 8 * (r >> 2); }
+
+// LSTM kernels are instantiated per hidden size (compile-time strides).
+#define SMAML_DISPATCH_H(HV, ...)                              \
+  switch (HV) {                                                \
+    case 32: { constexpr int HT = 32; __VA_ARGS__; } break;    \
+    case 64: { constexpr int HT = 64; __VA_ARGS__; } break;    \
+    case 128: { constexpr int HT = 128; __VA_ARGS__; } break;  \
+    case 256: { constexpr int HT = 256; __VA_ARGS__; } break;  \
+    default: break;                                            \
+  }
 
 }  // namespace smaml
