@@ -12,7 +12,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsmaml.so")
+LIB_PATH = os.environ.get("SMAML_LIB") or os.path.join(HERE, "libsmaml.so")
 
 # every function include/smaml.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = (

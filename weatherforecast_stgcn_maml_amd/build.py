@@ -30,16 +30,18 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in SOURCES + HEADERS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Compile libsmaml.so; ``defines`` (e.g. ["SMAML_GATE_BK=16"]) build A/B variants."""
+    if not force and not defines and out == OUT and up_to_date():
+        return out
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(REPO, "include"), "-I", CSRC, *SOURCES, "-o", OUT + ".tmp"]
+           "-I", os.path.join(REPO, "include"), "-I", CSRC, *[f"-D{d}" for d in defines], *SOURCES,
+           "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -23,7 +23,7 @@ namespace smaml {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32;
+constexpr int BK = 32;  // default K-tile (GemmCfg's BK_ parameter)
 constexpr int NT = 256;  // threads per workgroup of the 4-wave configurations
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
@@ -44,8 +44,10 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
   return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
 }
 
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32>
 struct GemmCfg {
+  static constexpr int BK = BK_;
+  static_assert(BK % 16 == 0, "BK multiple of 16");
   static constexpr int BM = BM_;
   static constexpr int BN = BN_;
   static constexpr int WAVES_M = WAVES_M_;
@@ -57,7 +59,7 @@ struct GemmCfg {
   static constexpr int WTN = BN / (WAVES_N * 32);
   static_assert(WTM >= 1 && WTN >= 1, "wave tile");
   // KC: row-major [rows][BK+4]; MC: k-major [BK][rows+4]
-  static constexpr int LDA = A_KC ? BK + 4 : BM + 4;
+  static constexpr int LDA = A_KC ? BK + 4 : BM + 4;  // (BK+4) row stride: conflict-free ds_read_b128
   static constexpr int LDB = B_KC ? BK + 4 : BN + 4;
   static constexpr int A_STAGE = A_KC ? BM * LDA : BK * LDA;
   static constexpr int B_STAGE = B_KC ? BN * LDB : BK * LDB;
@@ -69,7 +71,7 @@ struct GemmCfg {
 
 // Fetch this thread's share of one operand tile into registers.
 // KC: element (row r, k) ; MC: element (k, row r).  `row0`, `k0` absolute.
-template <int ROWS, int F4, int NTH, bool KC, class L>
+template <int ROWS, int F4, int NTH, bool KC, int BK, class L>
 __device__ __forceinline__ void fetch_tile(const L& ld, int row0, int k0, float4 (&r)[F4]) {
   const int tid = threadIdx.x;
 #pragma unroll
@@ -85,7 +87,7 @@ __device__ __forceinline__ void fetch_tile(const L& ld, int row0, int k0, float4
   }
 }
 
-template <int ROWS, int LD, int F4, int NTH, bool KC>
+template <int ROWS, int LD, int F4, int NTH, bool KC, int BK>
 __device__ __forceinline__ void store_tile(float* s, const float4 (&r)[F4]) {
   const int tid = threadIdx.x;
 #pragma unroll
@@ -102,10 +104,10 @@ __device__ __forceinline__ void store_tile(float* s, const float4 (&r)[F4]) {
 }
 
 // 4 consecutive k-steps (4q .. 4q+3 of lane half h) of a 32-row fragment at tile row `row`.
-template <bool KC, int LD>
+template <bool KC, int LD, int BK>
 __device__ __forceinline__ float4 frag4(const float* s, int row, int h, int q) {
-  if (KC) return *reinterpret_cast<const float4*>(s + row * LD + 16 * h + 4 * q);
-  const float* p = s + (16 * h + 4 * q) * LD + row;
+  if (KC) return *reinterpret_cast<const float4*>(s + row * LD + (BK / 2) * h + 4 * q);
+  const float* p = s + ((BK / 2) * h + 4 * q) * LD + row;
   return make_float4(p[0], p[LD], p[2 * LD], p[3 * LD]);
 }
 
@@ -149,12 +151,12 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
   const int brow = wn * (C::WTN * 32) + (lane & 31);
   const int h = lane >> 5;
 #pragma unroll
-  for (int q = 0; q < BK / 8; ++q) {
+  for (int q = 0; q < C::BK / 8; ++q) {
     float4 a[C::WTM], b[C::WTN];
 #pragma unroll
-    for (int i = 0; i < C::WTM; ++i) a[i] = frag4<C::A_KC, C::LDA>(as, arow + 32 * i, h, q);
+    for (int i = 0; i < C::WTM; ++i) a[i] = frag4<C::A_KC, C::LDA, C::BK>(as, arow + 32 * i, h, q);
 #pragma unroll
-    for (int j = 0; j < C::WTN; ++j) b[j] = frag4<C::B_KC, C::LDB>(bs, brow + 32 * j, h, q);
+    for (int j = 0; j < C::WTN; ++j) b[j] = frag4<C::B_KC, C::LDB, C::BK>(bs, brow + 32 * j, h, q);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -172,31 +174,123 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
                                               const Hook& hook = Hook()) {
   float* As = smem;
   float* Bs = smem + 2 * C::A_STAGE;
-  const int nkt = (kend - kbeg + BK - 1) / BK;
+  constexpr int BKc = C::BK;
+  const int nkt = (kend - kbeg + BKc - 1) / BKc;
   if (nkt <= 0) return;
 
   float4 ra[C::A_F4], rb[C::B_F4];
-  fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC>(la, m0, kbeg, ra);
-  fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC>(lb, n0, kbeg, rb);
-  store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC>(As, ra);
-  store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC>(Bs, rb);
+  fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg, ra);
+  fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg, rb);
+  store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(As, ra);
+  store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(Bs, rb);
   __syncthreads();
 
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
     if (more) {
-      fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC>(la, m0, kbeg + (kt + 1) * BK, ra);
-      fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC>(lb, n0, kbeg + (kt + 1) * BK, rb);
+      fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (kt + 1) * BKc, ra);
+      fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg + (kt + 1) * BKc, rb);
     }
     const float* as = As + cur * C::A_STAGE;
     const float* bs = Bs + cur * C::B_STAGE;
     hook(as, kt);
     mma_tile<C>(as, bs, acc);
     if (more) {
-      store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC>(As + (cur ^ 1) * C::A_STAGE, ra);
-      store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC>(Bs + (cur ^ 1) * C::B_STAGE, rb);
+      store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(As + (cur ^ 1) * C::A_STAGE, ra);
+      store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(Bs + (cur ^ 1) * C::B_STAGE, rb);
     }
+    __syncthreads();
+  }
+}
+
+}  // namespace smaml
+
+namespace smaml {
+
+// Fused primal + tangent mainloop (second-order path):
+//   acc_p += A . B            acc_t += A2 . B + A . B2
+// over k in [0, K): A, A2 share the A layout/rows, B, B2 the B layout/rows. Per K-tile the
+// four operand tiles are staged once (LDS: [A | A2 | B | B2] x 2 stages) and 3 MFMAs issue per
+// fragment pair. A2 is known to be zero for k < a2_kbeg (the layer-0 input has no tangent):
+// those K-tiles neither load A2 nor issue its MFMAs (a2_kbeg must be a multiple of BK).
+template <class C>
+struct DualStage {
+  static constexpr int FLOATS = 2 * (2 * C::A_STAGE + 2 * C::B_STAGE);
+};
+
+template <class C, bool A2>
+__device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, int h, Acc<C>& accp, Acc<C>& acct) {
+  constexpr int BKc = C::BK;
+  constexpr int SA = C::A_STAGE, SB = C::B_STAGE;
+#pragma unroll
+  for (int q = 0; q < BKc / 8; ++q) {
+    float4 a[C::WTM], a2[C::WTM], b[C::WTN], b2[C::WTN];
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) {
+      a[i] = frag4<C::A_KC, C::LDA, BKc>(st, arow + 32 * i, h, q);
+      if (A2) a2[i] = frag4<C::A_KC, C::LDA, BKc>(st + SA, arow + 32 * i, h, q);
+    }
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) {
+      b[j] = frag4<C::B_KC, C::LDB, BKc>(st + 2 * SA, brow + 32 * j, h, q);
+      b2[j] = frag4<C::B_KC, C::LDB, BKc>(st + 2 * SA + SB, brow + 32 * j, h, q);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::WTN; ++j) {
+          accp.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b[j], e), accp.v[i][j], 0, 0, 0);
+          acct.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b2[j], e), acct.v[i][j], 0, 0, 0);
+          if (A2)
+            acct.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a2[i], e), f4get(b[j], e), acct.v[i][j], 0, 0, 0);
+        }
+  }
+}
+
+template <class C, class LA, class LA2, class LB, class LB2>
+__device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2, const LB& lb, const LB2& lb2,
+                                                   int m0, int n0, int K, int a2_kbeg, Acc<C>& accp, Acc<C>& acct,
+                                                   float* smem) {
+  constexpr int BKc = C::BK;
+  constexpr int SA = C::A_STAGE, SB = C::B_STAGE;
+  constexpr int STAGE = 2 * SA + 2 * SB;
+  const int nkt = (K + BKc - 1) / BKc;
+  if (nkt <= 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+  const int arow = wm * (C::WTM * 32) + (lane & 31);
+  const int brow = wn * (C::WTN * 32) + (lane & 31);
+  const int h = lane >> 5;
+  float4 ra[C::A_F4], ra2[C::A_F4], rb[C::B_F4], rb2[C::B_F4];
+  auto fetch = [&](int k0) {
+    fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, k0, ra);
+    if (k0 >= a2_kbeg) fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la2, m0, k0, ra2);
+    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, k0, rb);
+    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb2, n0, k0, rb2);
+  };
+  auto store = [&](float* st, int k0) {
+    store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
+    if (k0 >= a2_kbeg) store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(st + SA, ra2);
+    store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(st + 2 * SA, rb);
+    store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(st + 2 * SA + SB, rb2);
+  };
+  fetch(0);
+  store(smem, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const int k0 = kt * BKc;
+    const bool more = kt + 1 < nkt;
+    if (more) fetch(k0 + BKc);
+    const float* st = smem + cur * STAGE;
+    if (k0 >= a2_kbeg)
+      dual_mma<C, true>(st, arow, brow, h, accp, acct);
+    else
+      dual_mma<C, false>(st, arow, brow, h, accp, acct);
+    if (more) store(smem + (cur ^ 1) * STAGE, k0 + BKc);
     __syncthreads();
   }
 }

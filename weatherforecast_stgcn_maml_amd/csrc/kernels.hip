@@ -20,9 +20,9 @@
 namespace smaml {
 
 using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-contiguous)
-using CfgGate = GemmCfg<128, 128, 4, 1, true, true>;  // LSTM forward: wave = 32 rows x 4 gates
-using CfgNN = GemmCfg<64, 128, 2, 2, true, false>;    // C = A . B   (B n-contiguous)
-using CfgTN = GemmCfg<128, 128, 2, 2, false, false>;  // C = A^T . B (split-K weight grads)
+using CfgGate = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;  // LSTM forward: wave = 32 rows x 4 gates
+using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK>;  // C = A . B   (B n-contiguous)
+using CfgTN = GemmCfg<128, 128, 2, 2, false, false, SMAML_TN_BK>;  // C = A^T . B (split-K weight grads)
 
 // ------------------------------------------------------------------------------------
 // Block-wide deterministic sum (fixed shuffle tree + fixed wave order).
@@ -85,7 +85,7 @@ struct GcnA {
 
 // 8 waves, 128 rows x 256 cols: one workgroup covers a row block's whole Hc=256 output,
 // so each input row is read once.
-using CfgGcn = GemmCfg<128, 256, 2, 4, true, true>;
+using CfgGcn = GemmCfg<128, 256, 2, 4, true, true, SMAML_GCN_BK>;
 
 __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
                                                            float* __restrict__ out, int cout, int remap, int relu,
@@ -186,7 +186,7 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
 template <int H>
-__global__ __launch_bounds__(NT) void k_lstm_fwd_step(const float* __restrict__ X, float* __restrict__ Hs,
+__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ X, float* __restrict__ Hs,
                                                       float* __restrict__ Cs, float* __restrict__ Gs,
                                                       const float* __restrict__ theta, int64_t tstride,
                                                       LayerOff lo, int T, int M, int t) {
@@ -205,13 +205,14 @@ __global__ __launch_bounds__(NT) void k_lstm_fwd_step(const float* __restrict__ 
   la.cin = cin;
   LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
   int tm, ug;
-  if (!gate_tile((M + CfgGate::BM - 1) / CfgGate::BM, (H + 31) / 32, tm, ug)) return;
+  constexpr int UPB = CfgGate::WAVES_N;  // 32-unit groups per workgroup
+  if (!gate_tile((M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug)) return;
   const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
   acc.zero();
   gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
 
-  const int j = ug * 32 + (threadIdx.x & 31);
+  const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
   if (j >= H) return;
   float bsum[4];
 #pragma unroll
@@ -250,8 +251,9 @@ void launch_lstm_fwd_step(hipStream_t s, const Dims& d, const Work& w, int l, in
   float* Cs = w.Cs + (int64_t)l * lsz;
   float* Gs = w.Gs + (int64_t)l * lsz * 4;
   const int ntm = (w.M + CfgGate::BM - 1) / CfgGate::BM;
-  dim3 grid((ntm + 7) / 8 * 8 * ((d.H + 31) / 32), 1, w.Z);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, NT, 0, s>>>(X, Hs, Cs, Gs, theta, tstride, lo, d.T, w.M, t));
+  const int ngrp = (d.H + 32 * CfgGate::WAVES_N - 1) / (32 * CfgGate::WAVES_N);
+  dim3 grid((ntm + 7) / 8 * 8 * ngrp, 1, w.Z);
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(X, Hs, Cs, Gs, theta, tstride, lo, d.T, w.M, t));
 }
 
 // ====================================================================================
@@ -464,7 +466,7 @@ struct ColSumHook {
     if (threadIdx.x < CfgTN::BM) {
       float s = *acc;
 #pragma unroll 8
-      for (int kk = 0; kk < BK; ++kk) s += as[kk * CfgTN::LDA + threadIdx.x];
+      for (int kk = 0; kk < CfgTN::BK; ++kk) s += as[kk * CfgTN::LDA + threadIdx.x];
       *acc = s;
     }
   }
@@ -550,7 +552,7 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
   const int ldp = ncols + 1;
   const int ntm = (Mrows + CfgTN::BM - 1) / CfgTN::BM;
   const int ntn = (ncols + CfgTN::BN - 1) / CfgTN::BN;
-  const int64_t ktiles = (K + BK - 1) / BK;
+  const int64_t ktiles = (K + CfgTN::BK - 1) / CfgTN::BK;
   // aim for ~2048 workgroups, at least 8 K-tiles per split, bounded by the slab buffer
   int64_t nsplit = 2048 / ((int64_t)ntm * ntn * w.Z);
   if (nsplit < 1) nsplit = 1;
@@ -558,7 +560,7 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
   const int64_t per_split = (int64_t)w.Z * Mrows * ldp;
   if (nsplit * per_split > w.wpart_floats) nsplit = w.wpart_floats / per_split;
   if (nsplit < 1) nsplit = 1;
-  const int64_t kchunk = ((ktiles + nsplit - 1) / nsplit) * BK;
+  const int64_t kchunk = ((ktiles + nsplit - 1) / nsplit) * CfgTN::BK;
   nsplit = (K + kchunk - 1) / kchunk;
   WgB lb;
   lb.B1 = B1;

@@ -15,9 +15,14 @@
 
 namespace smaml {
 
-using CfgGateD = GemmCfg<128, 128, 4, 1, true, true>;
-using CfgNTD = GemmCfg<128, 128, 2, 2, true, true>;
-using CfgNND = GemmCfg<64, 128, 2, 2, true, false>;
+#ifndef SMAML_DUAL_BK
+#define SMAML_DUAL_BK 16
+#endif
+// The BPTT / dX / head duals stage four operand tiles per K-tile (gemm_dual_mainloop);
+// BK=16 keeps them at 54-80 KiB of LDS (two or more workgroups per CU).
+using CfgGateD = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;
+using CfgNTD = GemmCfg<128, 128, 2, 2, true, true, SMAML_DUAL_BK>;
+using CfgNND = GemmCfg<64, 128, 2, 2, true, false, SMAML_DUAL_BK>;
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
 #pragma unroll
@@ -34,7 +39,7 @@ __device__ __forceinline__ float block_sum_f(float v, float* red) {
 
 // ====================================================================================
 template <int H>
-__global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ X, const float* __restrict__ RX,
+__global__ __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ X, const float* __restrict__ RX,
                                                       float* __restrict__ Hs, float* __restrict__ Cs,
                                                       float* __restrict__ Gs, float* __restrict__ RHs,
                                                       float* __restrict__ RCs, float* __restrict__ RGs,
@@ -59,12 +64,15 @@ __global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ 
   const float* rhp = t > 0 ? RHz + (int64_t)(t - 1) * M * H : nullptr;
   const int wh = hp ? H : 0;
   int tm, ug;
-  if (!gate_tile((M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 31) / 32, tm, ug)) return;
+  constexpr int UPB = CfgGateD::WAVES_N;  // 32-unit groups per workgroup
+  if (!gate_tile((M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug)) return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
 
   Acc<CfgGateD> ap, at;
   ap.zero();
   at.zero();
+  // two passes (the fused 4-operand loop does not fit the 4-gate tile's registers):
+  //   ap = [x|h].[W_ih|W_hh]^T ;  at = [x|h|Rx|Rh].[U_ih|U_hh|W_ih|W_hh]^T
   {
     SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
@@ -76,7 +84,7 @@ __global__ __launch_bounds__(NT) void k_lstm_fwd_dual(const float* __restrict__ 
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
   }
-  const int j = ug * 32 + (threadIdx.x & 31);
+  const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
   if (j >= H) return;
   float bp[4], bu[4];
 #pragma unroll
@@ -128,8 +136,9 @@ void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, in
   const float* X = (l == 0) ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
   const float* RX = (l == 0) ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
   const int ntm = (w.M + CfgGateD::BM - 1) / CfgGateD::BM;
-  dim3 grid((ntm + 7) / 8 * 8 * ((d.H + 31) / 32), 1, w.Z);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT><<<grid, NT, 0, s>>>(X, RX, w.Hs + l * lsz, w.Cs + l * lsz,
+  const int ngrp = (d.H + 32 * CfgGateD::WAVES_N - 1) / (32 * CfgGateD::WAVES_N);
+  dim3 grid((ntm + 7) / 8 * 8 * ngrp, 1, w.Z);
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT><<<grid, CfgGateD::NTH, 0, s>>>(X, RX, w.Hs + l * lsz, w.Cs + l * lsz,
                                                                 w.Gs + l * lsz * 4, w.RHs + l * lsz, w.RCs + l * lsz,
                                                                 w.RGs + l * lsz * 4, theta, U, tstride, lo, d.T,
                                                                 w.M, t));
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(NT) void k_head_dual(const float* __restrict__ hT, 
                                                   float* __restrict__ dpred, float* __restrict__ Rdpred, int M,
                                                   int H, int HfC, int N, int Hf, int C, int T, int cin0, int B,
                                                   float dscale) {
-  __shared__ float smem[CfgNTD::SMEM_FLOATS];
+  __shared__ float smem[DualStage<CfgNTD>::FLOATS];
   const int z = blockIdx.z;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
@@ -155,13 +164,10 @@ __global__ __launch_bounds__(NT) void k_head_dual(const float* __restrict__ hT, 
   at.zero();
   {
     RowMajorKC la{h, M, H};
+    RowMajorKC la2{rh, M, H};
     RowMajorKC lb{th + wo, HfC, H};
-    gemm_mainloop<CfgNTD>(la, lb, m0, 0, 0, H, ap, smem);
-  }
-  {
-    SegKC la{{h, rh, nullptr, nullptr}, {H, H, 0, 0}, M};
-    SegKC lb{{u + wo, th + wo, nullptr, nullptr}, {H, H, 0, 0}, HfC};
-    gemm_mainloop<CfgNTD>(la, lb, m0, 0, 0, 2 * H, at, smem);
+    RowMajorKC lb2{u + wo, HfC, H};
+    gemm_dual_mainloop<CfgNTD>(la, la2, lb, lb2, m0, 0, H, 0, ap, at, smem);
   }
 #pragma unroll
   for (int i = 0; i < CfgNTD::WTM; ++i)
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(NT) void k_gemm_nn_dual(const float* __restrict__ A
                                                      const float* __restrict__ theta, const float* __restrict__ U,
                                                      int64_t tstride, int64_t woff, int ncols, float* __restrict__ out,
                                                      float* __restrict__ Rout, int64_t o_zstride) {
-  __shared__ float smem[CfgNND::SMEM_FLOATS];
+  __shared__ float smem[DualStage<CfgNND>::FLOATS];
   const int z = blockIdx.z;
   const float* a = A + (int64_t)z * a_zstride;
   const float* ra = RA + (int64_t)z * a_zstride;
@@ -217,13 +223,10 @@ __global__ __launch_bounds__(NT) void k_gemm_nn_dual(const float* __restrict__ A
   at.zero();
   {
     RowMajorKC la{a, rows, K};
+    RowMajorKC la2{ra, rows, K};
     RowMajorMC lb{W, K, ncols};
-    gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, K, ap, smem);
-  }
-  {
-    SegKC la{{ra, a, nullptr, nullptr}, {K, K, 0, 0}, rows};
-    SegMC lb{{W, UW}, {K, K}, ncols};
-    gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, 2 * K, at, smem);
+    RowMajorMC lb2{UW, K, ncols};
+    gemm_dual_mainloop<CfgNND>(la, la2, lb, lb2, m0, n0, K, 0, ap, at, smem);
   }
   float* o = out + (int64_t)z * o_zstride;
   float* ro = Rout + (int64_t)z * o_zstride;
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, fl
                                                       const float* __restrict__ theta, const float* __restrict__ U,
                                                       int64_t tstride, LayerOff lo, int T, int M, int t,
                                                       int dh_zero) {
-  __shared__ float smem[CfgNND::SMEM_FLOATS];
+  __shared__ float smem[DualStage<CfgNND>::FLOATS];
   constexpr int G4 = 4 * H;
   const int z = blockIdx.z;
   const int m0 = blockIdx.x * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
@@ -289,16 +292,11 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, fl
     const int64_t nx = (int64_t)(t + 1) * M * G4;
     const float* W = theta + (int64_t)z * tstride + lo.whh;
     const float* UW = U + (int64_t)z * tstride + lo.whh;
-    {
-      RowMajorKC la{dGz + nx, M, G4};
-      RowMajorMC lb{W, G4, H};
-      gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, G4, ap, smem);
-    }
-    {
-      SegKC la{{RdGz + nx, dGz + nx, nullptr, nullptr}, {G4, G4, 0, 0}, M};
-      SegMC lb{{W, UW}, {G4, G4}, H};
-      gemm_mainloop<CfgNND>(la, lb, m0, n0, 0, 2 * G4, at, smem);
-    }
+    RowMajorKC la{dGz + nx, M, G4};
+    RowMajorKC la2{RdGz + nx, M, G4};
+    RowMajorMC lb{W, G4, H};
+    RowMajorMC lb2{UW, G4, H};
+    gemm_dual_mainloop<CfgNND>(la, la2, lb, lb2, m0, n0, G4, 0, ap, at, smem);
   }
   const bool first = (t == T - 1);
   const bool full = m0 + CfgNND::BM <= M;

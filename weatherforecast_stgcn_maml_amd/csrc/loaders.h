@@ -6,6 +6,23 @@
 #pragma once
 #include "gemm_core.h"
 
+// K-tile depth per GEMM family (A/B-able at build time: -DSMAML_GATE_BK=16 ...).
+#ifndef SMAML_GATE_BK
+#define SMAML_GATE_BK 16
+#endif
+#ifndef SMAML_GATE_WN
+#define SMAML_GATE_WN 1  // gate GEMM column waves: 1 -> 128x128 (4 waves), 2 -> 128x256 (8 waves)
+#endif
+#ifndef SMAML_NN_BK
+#define SMAML_NN_BK 16
+#endif
+#ifndef SMAML_GCN_BK
+#define SMAML_GCN_BK 16
+#endif
+#ifndef SMAML_TN_BK
+#define SMAML_TN_BK 32
+#endif
+
 namespace smaml {
 
 struct RowMajorKC {  // [rows][K] with K contiguous
