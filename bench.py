@@ -92,8 +92,12 @@ def main():
     from weatherforecast_stgcn_maml_amd.distributed import env_rank, init_from_env, max_over_ranks
 
     rank, world, local = env_rank()
-    torch.cuda.set_device(local)
-    init_from_env("nccl", torch.device("cuda", local))
+    # one process per GPU; SMAML_DIST_BACKEND=gloo + LOCAL_RANK mod device count lets a
+    # single-GPU box rehearse the N>1 path (the driver's 8-GPU runs use RCCL, one GPU each)
+    dev_idx = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_idx)
+    init_from_env(os.environ.get("SMAML_DIST_BACKEND", "nccl"), torch.device("cuda", dev_idx))
+    local = dev_idx
 
     d = ModelDims(num_nodes=args.nodes)
     cfg = MamlConfig(inner_steps=args.inner_steps, batch=args.batch, order=args.order)

@@ -129,6 +129,18 @@ int smaml_adamw_step(smaml_ctx* ctx, void* stream, float* theta, const float* gr
                      int64_t n, int32_t step, float lr, float beta1, float beta2, float eps,
                      float weight_decay, float max_norm, float* norm_out);
 
+/* Regional adaptation (adapt_hybrid_v5.adaptModel, adapt_hybrid_v5.py:182-203): `nsteps`
+ * sequential fine-tuning steps on task 0 of smaml_set_tasks, each on `batch` windows
+ * (windows_host [nsteps][batch]; the reference uses batch 1, shuffled): forward, MSE,
+ * backward, clip_grad_norm_(max_norm), torch.optim.Adam with coupled L2 weight decay
+ * (create_climate_optimizer, adaptive_scheduler.py:68-94) at learning rate lr_dev[k]
+ * (device floats; ClimateAwareLRScheduler values) and Adam step step0+k+1.
+ * theta, m, v: flat trainable vectors (device). losses [nsteps] (device): per-step MSE. */
+int smaml_adapt_steps(smaml_ctx* ctx, void* stream, float* theta, float* m, float* v, int32_t step0,
+                      int32_t nsteps, int32_t batch, const int32_t* windows_host, const float* lr_dev,
+                      float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                      float* losses);
+
 /* ---- measurement (no reference counterpart; bench / profiling only) ------------------ */
 
 /* Enable/disable per-kernel-category HIP-event timing of the launches this context

@@ -284,3 +284,61 @@ class ReferencePort:
         torch.nn.utils.clip_grad_norm_(self.params, max_norm=1.0)
         self.opt.step()
         return float(loss)
+
+
+# ----------------------------------------------------------------------------- adaptation
+def climate_lr(region_name, epoch_idx, base_lr, epoch_loss):
+    """adaptive_scheduler.ClimateAwareLRScheduler.step (adaptive_scheduler.py:29-55) after
+    ``epoch_idx`` (1-based) epochs; base_lr already includes the climate factor of
+    create_climate_optimizer, the multiplier is applied again as the reference does."""
+    mult = 0.9 if region_name in ("Indonesia", "Thailand", "QueensAustralia") else (
+        1.1 if region_name in ("Moscow", "NorthSiberia", "Afghanistan") else 1.0)
+    prog = (epoch_idx - 1) % 5 / 5
+    lr = base_lr * mult * 0.5 * (1 + np.cos(np.pi * prog))
+    if epoch_loss is not None and epoch_idx > 3:
+        if epoch_loss > 1.0:
+            lr *= 1.1
+        elif epoch_loss < 0.2:
+            lr *= 0.95
+    return lr
+
+
+def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_samples: int = 1200,
+                    base_lr: float = 0.0006):
+    """adapt_hybrid_v5.adaptModel's fine-tuning loop (adapt_hybrid_v5.py:152-231): batch-1
+    samples in DataLoader(shuffle=True) order, MSE, backward, clip_grad_norm_(1.0),
+    torch.optim.Adam(lr, weight_decay) from create_climate_optimizer, scheduler per epoch,
+    then the validation MSE. Returns (params, epoch_losses, lrs, val_loss)."""
+    n_all = task.features.shape[0] - task.dims.window_size - task.dims.forecast_horizon
+    n_max = min(max_samples, n_all)
+    n_train = int(0.8 * n_max)
+    zone_mult = 0.9 if region_name in ("Indonesia", "Thailand", "QueensAustralia") else (
+        1.1 if region_name in ("Moscow", "NorthSiberia", "Afghanistan") else 1.0)
+    wd = 1e-5 if zone_mult == 0.9 else (5e-5 if zone_mult == 1.1 else 1e-4)
+    lr0 = base_lr * zone_mult
+    names = list(Pt.keys())
+    leaves = [Pt[k].detach().clone().requires_grad_(True) for k in names]
+    opt = torch.optim.Adam(leaves, lr=lr0, weight_decay=wd)
+    epoch_losses, lrs = [], []
+    for ep in range(epochs):
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())
+        g = torch.Generator()
+        g.manual_seed(seed)
+        order = torch.randperm(n_train, generator=g).tolist()
+        ls = []
+        lrs.append(opt.param_groups[0]["lr"])
+        for i in order:
+            opt.zero_grad()
+            loss, _ = batch_loss(dict(zip(names, leaves)), Pg, task, [i])
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(leaves, max_norm=1.0)
+            opt.step()
+            ls.append(float(loss.detach()))
+        avg = sum(ls) / len(ls)
+        epoch_losses.append(avg)
+        new_lr = climate_lr(region_name, ep + 1, lr0, avg)
+        for pg in opt.param_groups:
+            pg["lr"] = new_lr
+    with torch.no_grad():
+        vals = [float(batch_loss(dict(zip(names, leaves)), Pg, task, [i])[0]) for i in range(n_train, n_max)]
+    return dict(zip(names, [l.detach() for l in leaves])), epoch_losses, lrs, sum(vals) / max(len(vals), 1)

@@ -19,7 +19,7 @@ EXPORTS = (
     "smaml_last_error", "smaml_abi_version", "smaml_param_layout", "smaml_graph_ell",
     "smaml_create", "smaml_destroy", "smaml_set_graph", "smaml_set_gcn_params", "smaml_reserve",
     "smaml_workspace_bytes", "smaml_gcn_conv", "smaml_forward", "smaml_set_tasks",
-    "smaml_meta_step", "smaml_adamw_step", "smaml_timing", "smaml_timing_collect",
+    "smaml_meta_step", "smaml_adamw_step", "smaml_adapt_steps", "smaml_timing", "smaml_timing_collect",
 )
 
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "head_loss", "head_dh", "lstm_bwd_step",
@@ -73,6 +73,7 @@ _SIGS = {
     "smaml_set_tasks": ([P, I32, ctypes.POINTER(P), PI32], I32),
     "smaml_meta_step": ([P, P, P, I32, I32, I32, PI32, F32, F32, F32, P, P, P, P], I32),
     "smaml_adamw_step": ([P, P, P, P, P, P, I64, I32, F32, F32, F32, F32, F32, F32, P], I32),
+    "smaml_adapt_steps": ([P, P, P, P, P, I32, I32, I32, PI32, P, F32, F32, F32, F32, F32, P], I32),
     "smaml_timing": ([P, I32], I32),
     "smaml_timing_collect": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               PI64, I32], I32),
@@ -199,6 +200,13 @@ class Context:
             ptr(losses) if losses is not None else None,
             ptr(norms) if norms is not None else None,
             ptr(fast_out) if fast_out is not None else None))
+
+    def adapt_steps(self, stream, theta, m, v, step0, windows: np.ndarray, lr_dev, betas, eps, wd, max_norm,
+                    losses):
+        w = np.ascontiguousarray(windows, dtype=np.int32)
+        check(self._L.smaml_adapt_steps(self._h, stream, ptr(theta), ptr(m), ptr(v), int(step0), w.shape[0],
+                                        w.shape[1], w.ctypes.data_as(PI32), ptr(lr_dev), float(betas[0]),
+                                        float(betas[1]), float(eps), float(wd), float(max_norm), ptr(losses)))
 
     def timing(self, enable: bool):
         check(self._L.smaml_timing(self._h, 1 if enable else 0))

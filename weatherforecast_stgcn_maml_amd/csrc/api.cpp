@@ -803,6 +803,42 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   return SMAML_OK;
 }
 
+int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float* v, int32_t step0, int32_t nsteps,
+                      int32_t batch, const int32_t* windows_host, const float* lr_dev, float beta1, float beta2,
+                      float eps, float weight_decay, float max_norm, float* losses) {
+  TRY(require_ready(c));
+  if (c->feats.empty()) return fail(SMAML_ESTATE, "smaml_set_tasks not called");
+  if (!theta || !m || !v || nsteps <= 0 || batch <= 0 || !windows_host || !lr_dev || !losses || step0 < 0)
+    return fail(SMAML_EINVAL, "bad adapt_steps arguments");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  const Dims& d = c->d;
+  const int B = batch;
+  TRY(reserve(c, 1, B));
+  set_work(c, 1, B);
+  const int64_t nptr = (int64_t)nsteps * B;
+  std::vector<const float*> ptrs(nptr);
+  for (int64_t i = 0; i < nptr; ++i) {
+    const int wv = windows_host[i];
+    if (wv < 0 || wv + d.T + d.Hf >= c->t_total[0]) return fail(SMAML_EINVAL, "window start out of range");
+    ptrs[i] = c->feats[0] + (int64_t)wv * d.N * d.Cin0;
+  }
+  TRY(upload_xtab(c, s, ptrs.data(), nptr));
+  const int64_t P = c->po.P;
+  const float inv = 1.f / ((float)d.N * d.HfC * B);
+  for (int k = 0; k < nsteps; ++k) {
+    const float* const* xt = c->xtab + (int64_t)k * B;
+    TRY(run_forward(c, s, theta, 0, xt));
+    launch_head_loss(s, d, c->w, theta, 0, c->po, xt, 2.f * inv, true);
+    launch_loss_final(s, c->w, inv, losses + k);
+    TRY(run_backward(c, s, theta, 0, c->grad));
+    launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
+                   weight_decay, max_norm);
+  }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
 int smaml_timing(smaml_ctx* c, int32_t enable) {
   if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
   c->tm.on = enable != 0;

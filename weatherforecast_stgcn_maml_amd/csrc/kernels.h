@@ -90,6 +90,9 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
                   float lr, float b1, float b2, float eps, float wd, float step_size, float bc2_sqrt,
                   float max_norm, float* norm_out);
 
+void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm);
+
 // ---- second-order launchers (kernels_dual.hip) ----
 void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
                           const float* U, int64_t tstride, const LayerOff& lo);

@@ -388,7 +388,10 @@ void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, 
 //   dc = dc_carry + dh * o * (1 - tanh(c_t)^2)
 //   dG_t = [dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tanh(c_t)*o(1-o)]
 //   dc_carry = dc * f
-template <int H>
+// 64x64 tiles for small per-GPU batches (e.g. 2 tasks per rank at 8 GPUs) so the grid fills the chip.
+using CfgNNs = GemmCfg<64, 64, 2, 2, true, false, SMAML_NN_BK>;
+
+template <int H, class CfgNN>
 __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, const float* __restrict__ dH,
                                                       float* __restrict__ dc, const float* __restrict__ Gs,
                                                       const float* __restrict__ Cs,
@@ -446,12 +449,20 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, co
 void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
                           int64_t tstride, const LayerOff& lo) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-  dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
   // the top layer's dH is zero except at t = T-1 (written by the head backward)
   const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
-  SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT><<<grid, CfgNN::NTH, 0, s>>>(
-                            w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz, theta, tstride,
-                            lo, d.T, w.M, t, dh_zero));
+  const int64_t wgs = (int64_t)((w.M + CfgNN::BM - 1) / CfgNN::BM) * ((d.H + CfgNN::BN - 1) / CfgNN::BN) * w.Z;
+  if (wgs >= 3 * 256) {
+    dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNN><<<grid, CfgNN::NTH, 0, s>>>(
+                              w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz, theta,
+                              tstride, lo, d.T, w.M, t, dh_zero));
+  } else {
+    dim3 grid((w.M + CfgNNs::BM - 1) / CfgNNs::BM, (d.H + CfgNNs::BN - 1) / CfgNNs::BN, w.Z);
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
+                              w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz, theta,
+                              tstride, lo, d.T, w.M, t, dh_zero));
+  }
 }
 
 // ====================================================================================
@@ -689,6 +700,36 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
   int nb = (int)((n + NT - 1) / NT);
   if (nb > 2048) nb = 2048;
   k_adamw<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr, b1, b2, eps, wd, step_size, bc2_sqrt, max_norm, norm_out);
+}
+
+// ====================================================================================
+// Regional adaptation step (adapt_hybrid_v5.py:196-201): clip_grad_norm_(max_norm) then
+// torch.optim.Adam with coupled L2 weight decay (g += wd * p), per-step learning rate.
+__global__ void k_adam_l2(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                          float* __restrict__ v, int64_t n, const double* __restrict__ part, const float* __restrict__ lr_dev,
+                          int step, float b1, float b2, float eps, float wd, float max_norm) {
+  float total;
+  const float coef = clip_coef_from(part, max_norm, &total);
+  const float lr = *lr_dev;
+  const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = fmaf(wd, p[i], g[i] * coef);
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    p[i] = p[i] - step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm) {
+  k_sqsum<<<dim3(SQB, 1), NT, 0, s>>>(g, n, part);
+  int nb = (int)((n + NT - 1) / NT);
+  if (nb > 2048) nb = 2048;
+  k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, step, b1, b2, eps, wd, max_norm);
 }
 
 }  // namespace smaml

@@ -261,7 +261,9 @@ void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* th
 }
 
 // ====================================================================================
-template <int H>
+using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
+
+template <int H, class CfgNND>
 __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, float* __restrict__ RdG,
                                                       const float* __restrict__ dH, const float* __restrict__ RdH,
                                                       float* __restrict__ dc, float* __restrict__ Rdc,
@@ -346,11 +348,19 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, fl
 void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
                           const float* U, int64_t tstride, const LayerOff& lo) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-  dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
   const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
-  SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT><<<grid, CfgNND::NTH, 0, s>>>(
-                            w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
-                            w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, t, dh_zero));
+  const int64_t wgs = (int64_t)((w.M + CfgNND::BM - 1) / CfgNND::BM) * ((d.H + CfgNND::BN - 1) / CfgNND::BN) * w.Z;
+  if (wgs >= 3 * 256) {
+    dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgNND><<<grid, CfgNND::NTH, 0, s>>>(
+                              w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
+                              w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, t, dh_zero));
+  } else {
+    dim3 grid((w.M + CfgNNDs::BM - 1) / CfgNNDs::BM, (d.H + CfgNNDs::BN - 1) / CfgNNDs::BN, w.Z);
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgNNDs><<<grid, CfgNNDs::NTH, 0, s>>>(
+                              w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
+                              w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, t, dh_zero));
+  }
 }
 
 // ====================================================================================
