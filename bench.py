@@ -79,6 +79,27 @@ def cpu_baseline(d, n_steps, P, ei, feats):
     return (time.perf_counter() - t0) / n_steps, torch.get_num_threads()
 
 
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
+
+
+def measured_traffic(category, workload, world):
+    """Per-launch HBM bytes of a timing category from the committed PMC profile
+    (tools/prof_summary.py output), only when it was taken on this exact workload. PMC
+    counters cannot be read from inside a timed run, so the figure comes from the separate
+    rocprofv3 --pmc passes of the same bench command (profiles/, tools/gpu_profile.sh)."""
+    if world != 1 or not os.path.exists(TRAFFIC_JSON):
+        return None
+    try:
+        t = json.load(open(TRAFFIC_JSON))
+    except (OSError, ValueError):
+        return None
+    if t.get("workload") != workload or category not in t.get("categories", {}):
+        return None
+    c = dict(t["categories"][category])
+    c["source"] = t.get("profile") or "profiles/traffic.json"
+    return c
+
+
 def main():
     args = parse()
     import torch
@@ -173,12 +194,17 @@ def main():
         dom = max((k for k in kern if k != "misc"), key=lambda k: kern[k]["ms"])
         kd = kern[dom]
         ach = kd["flops"] / (kd["ms"] * 1e-3) / 1e12 if kd["ms"] > 0 else 0.0
+        traffic = measured_traffic(dom, out["config"]["workload"], world)
         out["roofline"] = {
             "kernel": dom, "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS,
-            "unit": "TFLOP/s", "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+            "unit": "TFLOP/s", "frac": ach / PEAK_FP32_MFMA_TFLOPS,
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
             "avg_launch_us": kd["ms"] * 1e3 / max(kd["launches"], 1),
             "flops_per_launch": kd["flops"] / max(kd["launches"], 1),
         }
+        if traffic:
+            out["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            out["roofline"]["traffic_source"] = traffic["source"]
         out["kernels"] = {k: {"ms_per_step": v["ms"] / args.steps,
                               "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                               "launches_per_step": v["launches"] / args.steps}

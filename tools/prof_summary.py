@@ -1,49 +1,119 @@
-"""Summarise a rocprofv3 run (kernel stats + FETCH_SIZE/WRITE_SIZE PMC passes) into markdown.
+"""Summarise a rocprofv3 run (kernel stats + FETCH_SIZE/WRITE_SIZE PMC passes) into markdown,
+and optionally write the per-launch HBM traffic of each bench timing category as JSON
+(``bench.py`` reads it into ``roofline.traffic`` when the workload matches).
 
 FETCH_SIZE on gfx950 reports half the bytes of wide coalesced streaming reads
-(MI355X_MICROARCH.md §HBM): the 'corrected' column doubles it. Units are KB.
+(MI355X_MICROARCH.md §HBM, 16 B/lane loads as all our operand loads are): the corrected
+figure doubles it. WRITE_SIZE is exact for 16-B streaming stores; our epilogue stores are
+4-B scattered stores (uncalibrated width), so the write column is indicative. Units: KB.
+
+Usage: prof_summary.py RUN_DIR TITLE [TRAFFIC_JSON PROFILE_MD]
+(the workload string is taken from the profiled bench's JSON line in RUN_DIR/prof_kt.log)
 """
 import collections
 import csv
+import json
 import os
+import re
 import sys
+
+# bench.py timing categories (api.cpp TIMED(...)) -> the kernels each category launches
+CATEGORIES = {
+    "gcn_layer": r"k_gcn_layer",
+    "lstm_fwd_step": r"k_lstm_fwd_(step|dual)",
+    "lstm_bwd_step": r"k_lstm_bwd_(step|dual)",
+    "wgrad": r"k_wgrad",
+    "dx": r"k_gemm_nn",
+    "head": r"k_head_(loss|dual)",
+}
+
+
+def short(name):
+    return name.split("(")[0].replace("smaml::", "").replace("void ", "")
 
 
 def kstats(d):
     p = os.path.join(d, "prof_kt", "run_kernel_stats.csv")
     out = []
     for r in csv.DictReader(open(p)):
-        out.append((r["Name"].split("(")[0].replace("smaml::", ""), int(r["Calls"]),
-                    float(r["TotalDurationNs"]) / 1e6, float(r["AverageNs"]) / 1e3, float(r["Percentage"])))
+        out.append((r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) / 1e6,
+                    float(r["AverageNs"]) / 1e3, float(r["Percentage"])))
     return out
 
 
 def pmc(d, c):
+    """kernel full name -> list of per-dispatch counter values (KB)."""
     p = os.path.join(d, f"prof_pmc_{c}", "run_counter_collection.csv")
     if not os.path.exists(p):
         return {}
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(p)):
-        agg[r["Kernel_Name"].split("(")[0].replace("smaml::", "")].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return agg
 
 
-def main(d, title):
+def bench_line(d):
+    for line in reversed(open(os.path.join(d, "prof_kt.log")).read().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
+def main(d, title, traffic_out=None, profile_md=None):
+    ks = kstats(d)
     print(f"# {title}\n")
-    print("rocprofv3 --kernel-trace --stats (bench.py, config 2); times summed over the profiled run.\n")
+    print("rocprofv3 --kernel-trace --stats of `bench.py` (config 2); times summed over the profiled run.\n")
     print("| kernel | calls | total ms | avg us | % |")
     print("|---|---|---|---|---|")
-    for n, c, t, a, p in kstats(d):
+    for n, c, t, a, p in ks:
         if p >= 0.01:
-            print(f"| {n} | {c} | {t:.1f} | {a:.1f} | {p:.2f} |")
+            print(f"| {short(n)} | {c} | {t:.1f} | {a:.1f} | {p:.2f} |")
+
+    print("\nPer bench timing category (the same kernels `bench.py`'s HIP events bracket):\n")
+    print("| category | kernels | calls | total ms | avg us per launch |")
+    print("|---|---|---|---|---|")
+    cat_stats = {}
+    for cat, rx in CATEGORIES.items():
+        sel = [(n, c, t) for n, c, t, _, _ in ks if re.search(rx, n)]
+        if not sel:
+            continue
+        calls = sum(c for _, c, _ in sel)
+        tot = sum(t for _, _, t in sel)
+        cat_stats[cat] = (calls, tot)
+        print(f"| {cat} | {', '.join(sorted({short(n) for n, _, _ in sel}))} | {calls} | {tot:.1f} | "
+              f"{tot * 1e3 / calls:.1f} |")
+
     f, w = pmc(d, "FETCH_SIZE"), pmc(d, "WRITE_SIZE")
-    if f:
-        print("\nPMC (separate passes, per dispatch average, MB = KB/1024):\n")
-        print("| kernel | FETCH_SIZE MB | x2 corrected MB | WRITE_SIZE MB |")
-        print("|---|---|---|---|")
-        for k in f:
-            print(f"| {k} | {f[k] / 1024:.1f} | {2 * f[k] / 1024:.1f} | {w.get(k, 0) / 1024:.1f} |")
+    if not f:
+        return
+    print("\nPMC (separate `--pmc` passes, per-dispatch average; FETCH x2 = gfx950 correction):\n")
+    print("| kernel | dispatches | FETCH_SIZE MB | FETCH x2 MB | WRITE_SIZE MB |")
+    print("|---|---|---|---|---|")
+    for k in f:
+        fa = sum(f[k]) / len(f[k])
+        wa = sum(w.get(k, [0])) / max(len(w.get(k, [0])), 1)
+        print(f"| {short(k)} | {len(f[k])} | {fa / 1024:.1f} | {2 * fa / 1024:.1f} | {wa / 1024:.1f} |")
+    traffic = {}
+    print("\nHBM traffic per category launch (FETCH x2 + WRITE, dispatch-weighted):\n")
+    print("| category | dispatches | read MB | write MB | total MB |")
+    print("|---|---|---|---|---|")
+    for cat, rx in CATEGORIES.items():
+        fr = [v for k, vs in f.items() if re.search(rx, k) for v in vs]
+        wr = [v for k, vs in w.items() if re.search(rx, k) for v in vs]
+        if not fr:
+            continue
+        rd = 2 * sum(fr) / len(fr) * 1024
+        wt = (sum(wr) / len(wr) * 1024) if wr else 0.0
+        # wgrad's timed launch is two dispatches (split-K GEMM + fixed-order reduce)
+        per = 2.0 if cat == "wgrad" else 1.0
+        traffic[cat] = {"read_bytes": rd * per, "write_bytes": wt * per, "bytes_per_launch": (rd + wt) * per}
+        print(f"| {cat} | {len(fr)} | {rd * per / 1e6:.1f} | {wt * per / 1e6:.1f} | {(rd + wt) * per / 1e6:.1f} |")
+    if traffic_out:
+        b = bench_line(d)
+        json.dump({"workload": b["config"]["workload"] if b else None, "profile": profile_md, "unit": "bytes",
+                   "categories": traffic}, open(traffic_out, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "profile")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "profile",
+         sys.argv[3] if len(sys.argv) > 3 else None, sys.argv[4] if len(sys.argv) > 4 else None)

@@ -386,10 +386,11 @@ int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride
                            rps, d.N));
     src = dst;
   }
-  for (int l = 0; l < d.L; ++l)
-    for (int t = 0; t < d.T; ++t)
-      TIMED(c, s, C_FWD, 2.0 * w.Z * w.M * 4 * d.H * (c->po.lay[l].cin + (t > 0 ? d.H : 0)),
-            launch_lstm_fwd_step(s, d, w, l, t, theta, tstride, c->po.lay[l]));
+  for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
+    FwdWave wv{};
+    const double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
+    TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
+  }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -439,14 +440,10 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
                            rps, d.N));
     src = dst;
   }
-  for (int l = 0; l < d.L; ++l) {
-    const LayerOff& lo = c->po.lay[l];
-    for (int t = 0; t < d.T; ++t) {
-      const double k1 = lo.cin + (t > 0 ? d.H : 0);
-      const double k2 = (l > 0 ? 2.0 : 1.0) * lo.cin + (t > 0 ? 2.0 * d.H : 0.0);
-      TIMED(c, s, C_FWD, 2.0 * w.Z * w.M * 4 * d.H * (k1 + k2),
-            launch_lstm_fwd_dual(s, d, w, l, t, theta, U, tstride, lo));
-    }
+  for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
+    FwdWave wv{};
+    const double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
+    TIMED(c, s, C_FWD, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;

@@ -60,13 +60,27 @@ struct Work {
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
 
+// One anti-diagonal of the (layer, step) grid of the LSTM forward: the problems (l, t) with
+// l + t = diag are independent ((l, t) reads only (l-1, t) and (l, t-1), both on the previous
+// diagonal), so they share one launch: T + L - 1 launches per sweep instead of T * L, each up
+// to L times wider (fills the chip when a rank holds few tasks). Problem p owns blocks
+// [off[p], off[p+1]) (multiples of 8, keeping the XCD-aware gate tile mapping).
+struct FwdWave {
+  int n;
+  int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
+  LayerOff lo[MAX_LAYERS];
+};
+// Fills wv for diagonal diag; returns its algorithmic flops (dual: primal + tangent GEMMs).
+double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
+                FwdWave& wv);
+
 // ---- launchers (kernels.hip) ----
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
                       const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
                       const float* b, int cin, int cout, const int* ell_c, const float* ell_v, int rows_per_sample,
                       int ell_rows);
-void launch_lstm_fwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          int64_t tstride, const LayerOff& lo);
+void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
+                          int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                       const ParamOff& po, const float* const* xtab, float dscale, bool want_loss);
 void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
@@ -94,8 +108,8 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
                     const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm);
 
 // ---- second-order launchers (kernels_dual.hip) ----
-void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          const float* U, int64_t tstride, const LayerOff& lo);
+void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
+                               const float* U, int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
                       int64_t tstride, const ParamOff& po, const float* const* xtab, float dscale);
 void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,

@@ -186,11 +186,18 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
 template <int H>
-__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ X, float* __restrict__ Hs,
-                                                      float* __restrict__ Cs, float* __restrict__ Gs,
-                                                      const float* __restrict__ theta, int64_t tstride,
-                                                      LayerOff lo, int T, int M, int t) {
+__global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
+                                                      float* __restrict__ CsAll, float* __restrict__ GsAll,
+                                                      int64_t lsz, const float* __restrict__ theta, int64_t tstride,
+                                                      FwdWave wv, int T, int M) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
+  int l, t, b0;
+  LayerOff lo;
+  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  const float* X = l == 0 ? F : HsAll + (int64_t)(l - 1) * lsz;
+  float* Hs = HsAll + (int64_t)l * lsz;
+  float* Cs = CsAll + (int64_t)l * lsz;
+  float* Gs = GsAll + (int64_t)l * lsz * 4;
   const int z = blockIdx.z;
   const float* th = theta + (int64_t)z * tstride;
   const int cin = lo.cin;
@@ -206,7 +213,8 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __r
   LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
   int tm, ug;
   constexpr int UPB = CfgGate::WAVES_N;  // 32-unit groups per workgroup
-  if (!gate_tile((M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug)) return;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+    return;
   const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
   acc.zero();
@@ -243,17 +251,42 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __r
   }
 }
 
-void launch_lstm_fwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          int64_t tstride, const LayerOff& lo) {
+double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
+                FwdWave& wv) {
+  double fl = 0.0;
+  int n = 0, off = 0;
+  for (int l = 0; l < d.L; ++l) {
+    const int t = diag - l;
+    if (t < 0 || t >= d.T) continue;
+    const LayerOff& lo = po.lay[l];
+    wv.l[n] = l;
+    wv.t[n] = t;
+    wv.lo[n] = lo;
+    wv.off[n] = off;
+    off += blocks_per_problem;
+    ++n;
+    const double k1 = lo.cin + (t > 0 ? d.H : 0);
+    const double k2 = (l > 0 ? 2.0 : 1.0) * lo.cin + (t > 0 ? 2.0 * d.H : 0.0);
+    fl += 2.0 * w.Z * w.M * 4 * d.H * (dual ? k1 + k2 : k1);
+  }
+  wv.n = n;
+  wv.off[n] = off;
+  for (int q = n + 1; q <= MAX_LAYERS; ++q) wv.off[q] = off;
+  return fl;
+}
+
+void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
+                          int64_t tstride, const ParamOff& po, double* flops) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-  const float* X = (l == 0) ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
-  float* Hs = w.Hs + (int64_t)l * lsz;
-  float* Cs = w.Cs + (int64_t)l * lsz;
-  float* Gs = w.Gs + (int64_t)l * lsz * 4;
   const int ntm = (w.M + CfgGate::BM - 1) / CfgGate::BM;
   const int ngrp = (d.H + 32 * CfgGate::WAVES_N - 1) / (32 * CfgGate::WAVES_N);
-  dim3 grid((ntm + 7) / 8 * 8 * ngrp, 1, w.Z);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(X, Hs, Cs, Gs, theta, tstride, lo, d.T, w.M, t));
+  FwdWave wv{};
+  const double fl = fwd_wave(d, w, po, diag, (ntm + 7) / 8 * 8 * ngrp, false, wv);
+  if (flops) *flops = fl;
+  if (wv.n == 0) return;
+  dim3 grid(wv.off[wv.n], 1, w.Z);
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
+                                                                           wv, d.T, w.M));
 }
 
 // ====================================================================================
@@ -485,10 +518,16 @@ struct ColSumHook {
 
 __global__ __launch_bounds__(NT) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
-                                              int ntn, float* __restrict__ part, int ldp, int with_bias) {
+                                              int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
+                                              int ldp, int with_bias) {
   __shared__ float smem[CfgTN::SMEM_FLOATS];
-  const int z = blockIdx.z, split = blockIdx.y, nsplit = gridDim.y;
-  const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+  // XCD-aware: the ntile output tiles of one (split, task) group stream the same K rows of
+  // A and B, so they are placed on one XCD (blocks 8 apart) to share its L2. Speed only.
+  const int L = blockIdx.x, j = L >> 3;
+  const int g = (j / ntile) * 8 + (L & 7), tile = j - (j / ntile) * ntile;
+  if (g >= ngroups) return;
+  const int z = g / nsplit, split = g - z * nsplit;
+  const int tm = tile / ntn, tn = tile - tm * ntn;
   RowMajorMC la{A + (int64_t)z * a_zstride, lb.K, Mrows};
   WgB b = lb;
   if (b.B1) b.B1 += (int64_t)z * b1_zstride;
@@ -580,9 +619,11 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
   lb.c2 = c2;
   lb.K = K;
   lb.Mshift = Mshift;
-  dim3 grid(ntm * ntn, (unsigned)nsplit, w.Z);
-  k_wgrad<<<grid, NT, 0, s>>>(A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, w.wpart, ldp,
-                              with_bias ? 1 : 0);
+  const int ntile = ntm * ntn;
+  const int ngroups = (int)nsplit * w.Z;
+  dim3 grid((unsigned)(((ngroups + 7) / 8) * 8 * ntile));
+  k_wgrad<<<grid, NT, 0, s>>>(A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, (int)nsplit,
+                              ngroups, w.wpart, ldp, with_bias ? 1 : 0);
   const int64_t total = (int64_t)Mrows * ldp;
   dim3 g2((unsigned)((total + 255) / 256), w.Z);
   k_wgrad_reduce<<<g2, 256, 0, s>>>(w.wpart, (int)nsplit, Mrows, ldp, c1, c2, grad, P, off_w1, off_w2, off_b1,

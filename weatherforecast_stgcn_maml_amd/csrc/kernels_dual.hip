@@ -39,14 +39,26 @@ __device__ __forceinline__ float block_sum_f(float v, float* red) {
 
 // ====================================================================================
 template <int H>
-__global__ __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ X, const float* __restrict__ RX,
-                                                      float* __restrict__ Hs, float* __restrict__ Cs,
-                                                      float* __restrict__ Gs, float* __restrict__ RHs,
-                                                      float* __restrict__ RCs, float* __restrict__ RGs,
-                                                      const float* __restrict__ theta, const float* __restrict__ U,
-                                                      int64_t tstride, LayerOff lo, int T, int M, int t) {
+__global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
+                                                      float* __restrict__ HsAll, float* __restrict__ CsAll,
+                                                      float* __restrict__ GsAll, float* __restrict__ RHsAll,
+                                                      float* __restrict__ RCsAll, float* __restrict__ RGsAll,
+                                                      int64_t lsz, const float* __restrict__ theta,
+                                                      const float* __restrict__ U, int64_t tstride, FwdWave wv,
+                                                      int T, int M) {
   __shared__ float smem[CfgGateD::SMEM_FLOATS];
   constexpr int G4 = 4 * H;
+  int l, t, b0;
+  LayerOff lo;
+  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  const float* X = l == 0 ? F : HsAll + (int64_t)(l - 1) * lsz;
+  const float* RX = l == 0 ? nullptr : RHsAll + (int64_t)(l - 1) * lsz;
+  float* Hs = HsAll + (int64_t)l * lsz;
+  float* Cs = CsAll + (int64_t)l * lsz;
+  float* Gs = GsAll + (int64_t)l * lsz * 4;
+  float* RHs = RHsAll + (int64_t)l * lsz;
+  float* RCs = RCsAll + (int64_t)l * lsz;
+  float* RGs = RGsAll + (int64_t)l * lsz * 4;
   const int z = blockIdx.z;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
@@ -65,7 +77,9 @@ __global__ __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __
   const int wh = hp ? H : 0;
   int tm, ug;
   constexpr int UPB = CfgGateD::WAVES_N;  // 32-unit groups per workgroup
-  if (!gate_tile((M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug)) return;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm,
+                 ug))
+    return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
 
   Acc<CfgGateD> ap, at;
@@ -130,18 +144,18 @@ __global__ __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __
   }
 }
 
-void launch_lstm_fwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          const float* U, int64_t tstride, const LayerOff& lo) {
+void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
+                               const float* U, int64_t tstride, const ParamOff& po, double* flops) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-  const float* X = (l == 0) ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
-  const float* RX = (l == 0) ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
   const int ntm = (w.M + CfgGateD::BM - 1) / CfgGateD::BM;
   const int ngrp = (d.H + 32 * CfgGateD::WAVES_N - 1) / (32 * CfgGateD::WAVES_N);
-  dim3 grid((ntm + 7) / 8 * 8 * ngrp, 1, w.Z);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT><<<grid, CfgGateD::NTH, 0, s>>>(X, RX, w.Hs + l * lsz, w.Cs + l * lsz,
-                                                                w.Gs + l * lsz * 4, w.RHs + l * lsz, w.RCs + l * lsz,
-                                                                w.RGs + l * lsz * 4, theta, U, tstride, lo, d.T,
-                                                                w.M, t));
+  FwdWave wv{};
+  const double fl = fwd_wave(d, w, po, diag, (ntm + 7) / 8 * 8 * ngrp, true, wv);
+  if (flops) *flops = fl;
+  if (wv.n == 0) return;
+  dim3 grid(wv.off[wv.n], 1, w.Z);
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT><<<grid, CfgGateD::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs,
+                                                                            lsz, theta, U, tstride, wv, d.T, w.M));
 }
 
 // ====================================================================================
@@ -264,7 +278,7 @@ void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* th
 using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
 
 template <int H, class CfgNND>
-__global__ __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, float* __restrict__ RdG,
+__global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, float* __restrict__ RdG,
                                                       const float* __restrict__ dH, const float* __restrict__ RdH,
                                                       float* __restrict__ dc, float* __restrict__ Rdc,
                                                       const float* __restrict__ Gs, const float* __restrict__ Cs,

@@ -23,6 +23,33 @@
 #define SMAML_TN_BK 32
 #endif
 
+// Minimum resident waves per SIMD requested from the register allocator for the LSTM gate
+// kernels (0 = compiler default). A/B-able at build time.
+#ifndef SMAML_GATE_WPE
+#define SMAML_GATE_WPE 4
+#endif
+#ifndef SMAML_GATED_WPE
+#define SMAML_GATED_WPE 0  // same, for the tangent (dual) gate kernel
+#endif
+#ifndef SMAML_BWDD_WPE
+#define SMAML_BWDD_WPE 3  // same, for the tangent BPTT kernel (LDS caps it at 3 anyway)
+#endif
+#if SMAML_BWDD_WPE > 0
+#define SMAML_BWDD_ATTR __attribute__((amdgpu_waves_per_eu(SMAML_BWDD_WPE)))
+#else
+#define SMAML_BWDD_ATTR
+#endif
+#if SMAML_GATE_WPE > 0
+#define SMAML_GATE_ATTR __attribute__((amdgpu_waves_per_eu(SMAML_GATE_WPE)))
+#else
+#define SMAML_GATE_ATTR
+#endif
+#if SMAML_GATED_WPE > 0
+#define SMAML_GATED_ATTR __attribute__((amdgpu_waves_per_eu(SMAML_GATED_WPE)))
+#else
+#define SMAML_GATED_ATTR
+#endif
+
 namespace smaml {
 
 struct RowMajorKC {  // [rows][K] with K contiguous
@@ -168,13 +195,35 @@ __device__ __forceinline__ void stb(float* base, uint32_t byteoff, float v) {
 // are dispatched 8 apart (same XCD under round-robin placement: L2 sharing of the A rows)
 // and within 32 consecutive blocks. Grid: gridDim.x = ceil(ntm/8)*8 * ngrp (ngrp = 4H/128).
 // Speed-only: a different placement changes nothing but speed. Returns false for padding.
-__device__ __forceinline__ bool gate_tile(int ntm, int ngrp, int& tm, int& ug) {
-  const int L = blockIdx.x;
+__device__ __forceinline__ bool gate_tile(int L, int ntm, int ngrp, int& tm, int& ug) {
   const int per = 8 * ngrp;
   const int q = L / per, rem = L - q * per;
   ug = rem >> 3;
   tm = q * 8 + (rem & 7);
   return tm < ntm;
+}
+
+__device__ __forceinline__ bool gate_tile(int ntm, int ngrp, int& tm, int& ug) {
+  return gate_tile((int)blockIdx.x, ntm, ngrp, tm, ug);
+}
+
+// The wavefront problem (kernels.h FwdWave) owning block bx, selected with scalar compares
+// (no dynamic indexing into the by-value kernel argument).
+template <class WV, class LO>
+__device__ __forceinline__ void wave_problem(const WV& wv, int bx, int& l, int& t, LO& lo, int& b0) {
+  constexpr int NQ = (int)(sizeof(wv.l) / sizeof(wv.l[0]));
+  l = wv.l[0];
+  t = wv.t[0];
+  lo = wv.lo[0];
+  b0 = 0;
+#pragma unroll
+  for (int q = 1; q < NQ; ++q)
+    if (q < wv.n && bx >= wv.off[q]) {
+      l = wv.l[q];
+      t = wv.t[q];
+      lo = wv.lo[q];
+      b0 = wv.off[q];
+    }
 }
 
 // Row offset (within the 32-row tile) of accumulator register r: (r&3) + 8*(r>>2).
