@@ -209,17 +209,16 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   int max_cin = std::max(d.Hc, d.H);
   const int64_t wpart = std::max<int64_t>((int64_t)zc * G * (max_cin + d.H + 1) * 32, 1 << 24);
   const int64_t lblk = (int64_t)zc * ((seq + 127) / 128 + 1);
-  const bool alias_gcn = G >= 2 * d.Hc;
   std::vector<std::pair<void**, int64_t>> parts;  // (dst, bytes)
   Work w{};
-  float* dummy = nullptr;
   parts.push_back({(void**)&w.F, rows * d.Hc * 4});
   parts.push_back({(void**)&w.Hs, rows * d.L * d.H * 4});
   parts.push_back({(void**)&w.Cs, rows * d.L * d.H * 4});
-  parts.push_back({(void**)&w.Gs, rows * d.L * G * 4});
-  parts.push_back({(void**)&w.dG, rows * G * 4});
-  parts.push_back({(void**)&w.dH, rows * d.H * 4});
-  parts.push_back({(void**)&w.dc, seq * d.H * 4});
+  parts.push_back({(void**)&w.Gs, rows * d.L * G * 4});  // gates, then dG in place (BPTT)
+  parts.push_back({(void**)&w.dH, seq * d.H * 4});
+  parts.push_back({(void**)&w.dc, seq * d.L * d.H * 4});
+  parts.push_back({(void**)&w.gcnA, rows * d.Hc * 4});
+  parts.push_back({(void**)&w.gcnB, rows * d.Hc * 4});
   parts.push_back({(void**)&w.pred, seq * d.HfC * 4});
   parts.push_back({(void**)&w.dpred, seq * d.HfC * 4});
   parts.push_back({(void**)&w.wpart, wpart * 4});
@@ -228,23 +227,17 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   float *fast = nullptr, *grad = nullptr;
   parts.push_back({(void**)&fast, (int64_t)zc * c->po.P * 4});
   parts.push_back({(void**)&grad, (int64_t)zc * c->po.P * 4});
-  if (!alias_gcn) {
-    parts.push_back({(void**)&w.gcnA, rows * d.Hc * 4});
-    parts.push_back({(void**)&w.gcnB, rows * d.Hc * 4});
-  }
   float *so_u = nullptr, *so_hu = nullptr;
   if (so) {
     parts.push_back({(void**)&w.RHs, rows * d.L * d.H * 4});
     parts.push_back({(void**)&w.RCs, rows * d.L * d.H * 4});
     parts.push_back({(void**)&w.RGs, rows * d.L * G * 4});
-    parts.push_back({(void**)&w.RdG, rows * G * 4});
-    parts.push_back({(void**)&w.RdH, rows * d.H * 4});
-    parts.push_back({(void**)&w.Rdc, seq * d.H * 4});
+    parts.push_back({(void**)&w.RdH, seq * d.H * 4});
+    parts.push_back({(void**)&w.Rdc, seq * d.L * d.H * 4});
     parts.push_back({(void**)&w.Rdpred, seq * d.HfC * 4});
     parts.push_back({(void**)&so_u, (int64_t)zc * c->po.P * 4});
     parts.push_back({(void**)&so_hu, (int64_t)zc * c->po.P * 4});
   }
-  (void)dummy;
   int64_t total = 0;
   for (auto& p : parts) total += (p.second + 255) / 256 * 256;
   if (c->arena) {
@@ -262,10 +255,6 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   for (auto& p : parts) {
     *p.first = arena + off;
     off += (p.second + 255) / 256 * 256;
-  }
-  if (alias_gcn) {
-    w.gcnA = w.dG;
-    w.gcnB = w.dG + rows * d.Hc;
   }
   w.wpart_floats = wpart;
   HIP_TRY(hipMemset(grad, 0, (size_t)zc * c->po.P * 4));
@@ -407,16 +396,19 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
         launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, top + (int64_t)(d.T - 1) * w.M * d.H,
                      TM * d.H, d.H, nullptr, 0, 0, w.M, 0, grad, po.P, po.wo, -1, po.bo, -1));
-  for (int l = d.L - 1; l >= 0; --l) {
+  // BPTT as reverse anti-diagonals; layer l's weight gradient as soon as its t = 0 step is done
+  for (int e = 0; e < d.T + d.L - 1; ++e) {
+    BwdWave wv{};
+    const double fl = bwd_wave(d, w, po, e, 0, false, wv);
+    TIMED(c, s, C_BWD, fl, launch_lstm_bwd_wave(s, d, w, e, theta, tstride, po));
+    const int l = d.L - 1 - (e - (d.T - 1));
+    if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
-    for (int t = d.T - 1; t >= 0; --t)
-      TIMED(c, s, C_BWD, t + 1 < d.T ? 2.0 * w.Z * w.M * 4 * d.H * d.H : 0.0,
-            launch_lstm_bwd_step(s, d, w, l, t, theta, tstride, lo));
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H),
-          launch_wgrad(s, d, w, w.dG, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
-                       TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih, lo.bhh));
-    if (l > 0) TIMED(c, s, C_DX, 2.0 * w.Z * TM * 4 * d.H * lo.cin, launch_dx(s, d, w, theta, tstride, lo));
+          launch_wgrad(s, d, w, w.Gs + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
+                       w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
+                       lo.bhh));
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -464,22 +456,24 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
         launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, w.RHs + toff, TM * d.H, d.H, nullptr, 0, 0,
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true));
-  for (int l = d.L - 1; l >= 0; --l) {
+  for (int e = 0; e < d.T + d.L - 1; ++e) {
+    BwdWave wv{};
+    const double fl = bwd_wave(d, w, po, e, 0, true, wv);
+    TIMED(c, s, C_BWD, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
+    const int l = d.L - 1 - (e - (d.T - 1));
+    if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
-    for (int t = d.T - 1; t >= 0; --t)
-      TIMED(c, s, C_BWD, t + 1 < d.T ? 3.0 * 2.0 * w.Z * w.M * 4 * d.H * d.H : 0.0,
-            launch_lstm_bwd_dual(s, d, w, l, t, theta, U, tstride, lo));
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
+    const float* dGl = w.Gs + (int64_t)l * lsz * 4;
+    const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
     TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H),
-          launch_wgrad(s, d, w, w.RdG, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
+          launch_wgrad(s, d, w, RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
                        TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false));
     TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H),
-          launch_wgrad(s, d, w, w.dG, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
+          launch_wgrad(s, d, w, dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
                        w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh,
                        false, true));
-    if (l > 0)
-      TIMED(c, s, C_DX, 3.0 * 2.0 * w.Z * TM * 4 * d.H * lo.cin, launch_dx_dual(s, d, w, theta, U, tstride, lo));
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;

@@ -45,7 +45,8 @@ struct Work {
   float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
   float* F;                // [Z][T][M][Hc] LSTM layer-0 input
   float *Hs, *Cs, *Gs;     // [L][Z][T][M][H] / [L][Z][T][M][H] / [L][Z][T][M][4H]
-  float *dG, *dH, *dc;     // [Z][T][M][4H], [Z][T][M][H], [Z][M][H]
+  float *dH, *dc;          // head's dh_T [Z][M][H]; cell-state carry per layer [L][Z][M][H]
+                           // (the BPTT writes dG in place over Gs: [L][Z][T][M][4H])
   float *pred, *dpred;     // [Z][M][HfC]
   float* wpart;            // split-K partial slabs
   int64_t wpart_floats;
@@ -54,7 +55,7 @@ struct Work {
   double* sqpart;          // [Z][SQB]
   // second-order (tangent) buffers; null unless reserved with so = true
   float *RHs, *RCs, *RGs;  // like Hs, Cs, Gs
-  float *RdG, *RdH, *Rdc;  // like dG, dH, dc
+  float *RdH, *Rdc;        // like dH, dc (R(dG) is written in place over RGs)
   float* Rdpred;           // like dpred
 };
 
@@ -70,6 +71,17 @@ struct FwdWave {
   int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
   LayerOff lo[MAX_LAYERS];
 };
+// Backward counterpart: problems (l, t) with (L-1-l) + (T-1-t) = e. Step (l, t) forms
+//   dh = [dG(l+1, t) | dG(l, t+1)] . [W_ih(l+1) ; W_hh(l)]   (one K = 8H GEMM; the dX of the
+// layer above is fused here instead of a separate GEMM), reading only the previous diagonal.
+struct BwdWave {
+  int n;
+  int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
+  LayerOff lo[MAX_LAYERS];
+  int64_t wih_up[MAX_LAYERS];  // W_ih offset of layer l+1 (unused at the top layer)
+};
+double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
+                BwdWave& wv);
 // Fills wv for diagonal diag; returns its algorithmic flops (dual: primal + tangent GEMMs).
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
                 FwdWave& wv);
@@ -86,10 +98,8 @@ void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* 
 void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
 void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                     const ParamOff& po);
-void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          int64_t tstride, const LayerOff& lo);
-void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
-               const LayerOff& lo);
+void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
+                          const ParamOff& po);
 void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
                   int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
                   int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
@@ -114,10 +124,8 @@ void launch_head_dual(hipStream_t s, const Dims& d, const Work& w, const float* 
                       int64_t tstride, const ParamOff& po, const float* const* xtab, float dscale);
 void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
                          int64_t tstride, const ParamOff& po);
-void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U, int64_t tstride,
-                    const LayerOff& lo);
-void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          const float* U, int64_t tstride, const LayerOff& lo);
+void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
+                               const float* U, int64_t tstride, const ParamOff& po);
 void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,
                    const float* coefs, float max_norm, float* U);
 void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha);

@@ -400,54 +400,79 @@ __global__ __launch_bounds__(NT) void k_gemm_nn(const float* __restrict__ A, int
 
 void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                     const ParamOff& po) {
-  // dH (top layer) holds zeros for t < T-1 (memset by the driver); write t = T-1.
-  float* out = w.dH + (int64_t)(d.T - 1) * w.M * d.H;
+  // dh_T of the top layer: [Z][M][H], added by the BPTT step (L-1, T-1)
   dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
   k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(w.dpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, tstride, po.wo, d.H,
-                                out, (int64_t)d.T * w.M * d.H);
-}
-
-void launch_dx(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
-               const LayerOff& lo) {
-  const int rows = d.T * w.M;
-  dim3 grid((rows + CfgNN::BM - 1) / CfgNN::BM, (lo.cin + CfgNN::BN - 1) / CfgNN::BN, w.Z);
-  k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(w.dG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, tstride, lo.wih,
-                                lo.cin, w.dH, (int64_t)rows * lo.cin);
+                                w.dH, (int64_t)w.M * d.H);
 }
 
 // ====================================================================================
-// LSTM backward step (layer l, time t):
-//   dh = dG_{t+1} . W_hh  (+ dH_above[t])          [fp32 MFMA, K = 4H]
+// LSTM backward step (layer l, time t), one anti-diagonal of (l, t) per launch (BwdWave):
+//   dh = [dG(l+1,t) | dG(l,t+1)] . [W_ih(l+1) ; W_hh(l)]  (+ head dh_T at l = L-1, t = T-1)
+//                                                   [fp32 MFMA, K = 8H, 4H at the borders]
 //   dc = dc_carry + dh * o * (1 - tanh(c_t)^2)
-//   dG_t = [dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tanh(c_t)*o(1-o)]
+//   dG_t = [dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tanh(c_t)*o(1-o)]  (in place over G_t)
 //   dc_carry = dc * f
-// 64x64 tiles for small per-GPU batches (e.g. 2 tasks per rank at 8 GPUs) so the grid fills the chip.
+// In place is safe: a workgroup reads G_t only for its own rows and units before writing them,
+// and its GEMM reads other (l, t) slabs finished on the previous diagonal.
+// 64x64 tiles for small grids (few tasks per rank) so the launch fills the chip.
 using CfgNNs = GemmCfg<64, 64, 2, 2, true, false, SMAML_NN_BK>;
 
+double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
+                BwdWave& wv) {
+  double fl = 0.0;
+  int n = 0, off = 0;
+  for (int l = d.L - 1; l >= 0; --l) {
+    const int t = d.T - 1 - (e - (d.L - 1 - l));
+    if (t < 0 || t >= d.T) continue;
+    wv.l[n] = l;
+    wv.t[n] = t;
+    wv.lo[n] = po.lay[l];
+    wv.wih_up[n] = l + 1 < d.L ? po.lay[l + 1].wih : 0;
+    wv.off[n] = off;
+    off += blocks_per_problem;
+    ++n;
+    const int segs = (l + 1 < d.L ? 1 : 0) + (t + 1 < d.T ? 1 : 0);
+    fl += (dual ? 3.0 : 1.0) * 2.0 * w.Z * w.M * 4 * d.H * d.H * segs;
+  }
+  wv.n = n;
+  for (int q = n; q <= MAX_LAYERS; ++q) wv.off[q] = off;
+  return fl;
+}
+
 template <int H, class CfgNN>
-__global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, const float* __restrict__ dH,
-                                                      float* __restrict__ dc, const float* __restrict__ Gs,
-                                                      const float* __restrict__ Cs,
-                                                      const float* __restrict__ theta, int64_t tstride,
-                                                      LayerOff lo, int T, int M, int t, int dh_zero) {
+__global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ GsAll, const float* __restrict__ CsAll,
+                                                      const float* __restrict__ dHhead, float* __restrict__ dcAll,
+                                                      int64_t lsz, const float* __restrict__ theta, int64_t tstride,
+                                                      BwdWave wv, int L, int T, int M) {
   __shared__ float smem[CfgNN::SMEM_FLOATS];
   constexpr int G4 = 4 * H;
+  const int p = wave_index(wv, (int)blockIdx.x);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const LayerOff lo = wave_sel(wv.lo, p);
+  const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int z = blockIdx.z;
-  const int m0 = blockIdx.x * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
+  const int m0 = ((int)blockIdx.x - b0) * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
   const int64_t slab = (int64_t)z * T * M;
-  float* dGz = dG + slab * G4;
-  const float* dHz = dH + slab * H;
-  const float* Gz = Gs + slab * G4;
-  const float* Cz = Cs + slab * H;
-  float* dcz = dc + (int64_t)z * M * H;
+  const float* th = theta + (int64_t)z * tstride;
+  float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in, dG out
+  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
   Acc<CfgNN> acc;
   acc.zero();
-  if (t + 1 < T) {
-    RowMajorKC la{dGz + (int64_t)(t + 1) * M * G4, M, G4};
-    RowMajorMC lb{theta + (int64_t)z * tstride + lo.whh, G4, H};
-    gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, G4, acc, smem);
+  {
+    // segments [above | next], compacted with selects (static indices keep the loaders in registers)
+    const bool up = l + 1 < L, nx = t + 1 < T;
+    const float* pa = GsAll + (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
+    const float* pn = Gz + (int64_t)(t + 1) * M * G4;
+    const int ns = (up ? 1 : 0) + (nx ? 1 : 0);
+    SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
+    SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
+    if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
   }
   const bool first = (t == T - 1);
+  const bool head = first && l == L - 1;
+  const float* dHz = dHhead + (int64_t)z * M * H;
   const bool full = m0 + CfgNN::BM <= M;
   const int rb = m0 + acc_row<CfgNN>(0, 0);
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
@@ -463,38 +488,39 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ dG, co
       const uint32_t oh = row * H + j;
       const uint32_t og = row * G4 + j;
       const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = acc.v[0][jj][r] + (dh_zero ? 0.f : ldb(dHz, 4u * (oh)));
+      const float dh = acc.v[0][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
       const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
       const float c = ldb(Cz, 4u * (oh));
       const float tc = tanhf_(c);
       const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
       const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
       const float dct = dcin + dh * go * (1.f - tc * tc);
-      stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
-      stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
-      stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
-      stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
+      stb(Gz, 4u * (og), dct * gg * gi * (1.f - gi));
+      stb(Gz, 4u * (og + H), dct * cp * gf * (1.f - gf));
+      stb(Gz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
+      stb(Gz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
       stb(dcz, 4u * (oc), dct * gf);
     }
   }
 }
 
-void launch_lstm_bwd_step(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          int64_t tstride, const LayerOff& lo) {
+void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
+                          const ParamOff& po) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-  // the top layer's dH is zero except at t = T-1 (written by the head backward)
-  const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
-  const int64_t wgs = (int64_t)((w.M + CfgNN::BM - 1) / CfgNN::BM) * ((d.H + CfgNN::BN - 1) / CfgNN::BN) * w.Z;
-  if (wgs >= 3 * 256) {
-    dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
+  BwdWave wv{};
+  const int ntm = (w.M + CfgNN::BM - 1) / CfgNN::BM, ntn = (d.H + CfgNN::BN - 1) / CfgNN::BN;
+  bwd_wave(d, w, po, e, ntm, false, wv);
+  if (wv.n == 0) return;
+  if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
+    dim3 grid(wv.off[wv.n], ntn, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNN><<<grid, CfgNN::NTH, 0, s>>>(
-                              w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz, theta,
-                              tstride, lo, d.T, w.M, t, dh_zero));
+                              w.Gs, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
   } else {
-    dim3 grid((w.M + CfgNNs::BM - 1) / CfgNNs::BM, (d.H + CfgNNs::BN - 1) / CfgNNs::BN, w.Z);
+    const int ntms = (w.M + CfgNNs::BM - 1) / CfgNNs::BM, ntns = (d.H + CfgNNs::BN - 1) / CfgNNs::BN;
+    bwd_wave(d, w, po, e, ntms, false, wv);
+    dim3 grid(wv.off[wv.n], ntns, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
-                              w.dG, w.dH, w.dc, w.Gs + (int64_t)l * lsz * 4, w.Cs + (int64_t)l * lsz, theta,
-                              tstride, lo, d.T, w.M, t, dh_zero));
+                              w.Gs, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
   }
 }
 

@@ -260,61 +260,62 @@ __global__ __launch_bounds__(NT) void k_gemm_nn_dual(const float* __restrict__ A
 
 void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
                          int64_t tstride, const ParamOff& po) {
-  const int64_t off = (int64_t)(d.T - 1) * w.M * d.H;
   dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
   k_gemm_nn_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dpred, w.Rdpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, U, tstride, po.wo,
-                                     d.H, w.dH + off, w.RdH + off, (int64_t)d.T * w.M * d.H);
-}
-
-void launch_dx_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U, int64_t tstride,
-                    const LayerOff& lo) {
-  const int rows = d.T * w.M;
-  dim3 grid((rows + CfgNND::BM - 1) / CfgNND::BM, (lo.cin + CfgNND::BN - 1) / CfgNND::BN, w.Z);
-  k_gemm_nn_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dG, w.RdG, (int64_t)rows * 4 * d.H, rows, 4 * d.H, theta, U, tstride,
-                                     lo.wih, lo.cin, w.dH, w.RdH, (int64_t)rows * lo.cin);
+                                     d.H, w.dH, w.RdH, (int64_t)w.M * d.H);
 }
 
 // ====================================================================================
 using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
 
+// Tangent BPTT step, one anti-diagonal per launch (kernels.hip k_lstm_bwd_step; BwdWave):
+//   dh  = A . B,   R(dh) = A2 . B + A . B2   with  A = [dG(l+1,t) | dG(l,t+1)],
+//   A2 = [R dG(l+1,t) | R dG(l,t+1)],  B = [W_ih(l+1) ; W_hh(l)],  B2 = [U_ih(l+1) ; U_hh(l)]
+// then the cell backward and its product-rule tangent; dG / R(dG) overwrite G / R(G) in place.
 template <int H, class CfgNND>
-__global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ dG, float* __restrict__ RdG,
-                                                      const float* __restrict__ dH, const float* __restrict__ RdH,
-                                                      float* __restrict__ dc, float* __restrict__ Rdc,
-                                                      const float* __restrict__ Gs, const float* __restrict__ Cs,
-                                                      const float* __restrict__ RGs, const float* __restrict__ RCs,
-                                                      const float* __restrict__ theta, const float* __restrict__ U,
-                                                      int64_t tstride, LayerOff lo, int T, int M, int t,
-                                                      int dh_zero) {
+__global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ GsAll, float* __restrict__ RGsAll,
+                                                      const float* __restrict__ CsAll, const float* __restrict__ RCsAll,
+                                                      const float* __restrict__ dHhead, const float* __restrict__ RdHhead,
+                                                      float* __restrict__ dcAll, float* __restrict__ RdcAll,
+                                                      int64_t lsz, const float* __restrict__ theta,
+                                                      const float* __restrict__ U, int64_t tstride, BwdWave wv, int L,
+                                                      int T, int M) {
   __shared__ float smem[DualStage<CfgNND>::FLOATS];
   constexpr int G4 = 4 * H;
+  const int p = wave_index(wv, (int)blockIdx.x);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const LayerOff lo = wave_sel(wv.lo, p);
+  const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int z = blockIdx.z;
-  const int m0 = blockIdx.x * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
+  const int m0 = ((int)blockIdx.x - b0) * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
   const int64_t slab = (int64_t)z * T * M;
-  float* dGz = dG + slab * G4;
-  float* RdGz = RdG + slab * G4;
-  const float* dHz = dH + slab * H;
-  const float* RdHz = RdH + slab * H;
-  const float* Gz = Gs + slab * G4;
-  const float* RGz = RGs + slab * G4;
-  const float* Cz = Cs + slab * H;
-  const float* RCz = RCs + slab * H;
-  float* dcz = dc + (int64_t)z * M * H;
-  float* rdcz = Rdc + (int64_t)z * M * H;
+  const float* th = theta + (int64_t)z * tstride;
+  const float* u = U + (int64_t)z * tstride;
+  float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;    // gates in, dG out
+  float* RGz = RGsAll + (int64_t)l * lsz * 4 + slab * G4;  // R(gates) in, R(dG) out
+  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  const float* RCz = RCsAll + (int64_t)l * lsz + slab * H;
+  float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
+  float* rdcz = RdcAll + ((int64_t)l * gridDim.z + z) * M * H;
   Acc<CfgNND> ap, at;
   ap.zero();
   at.zero();
-  if (t + 1 < T) {
-    const int64_t nx = (int64_t)(t + 1) * M * G4;
-    const float* W = theta + (int64_t)z * tstride + lo.whh;
-    const float* UW = U + (int64_t)z * tstride + lo.whh;
-    RowMajorKC la{dGz + nx, M, G4};
-    RowMajorKC la2{RdGz + nx, M, G4};
-    RowMajorMC lb{W, G4, H};
-    RowMajorMC lb2{UW, G4, H};
-    gemm_dual_mainloop<CfgNND>(la, la2, lb, lb2, m0, n0, G4, 0, ap, at, smem);
+  {
+    const bool up = l + 1 < L, nx = t + 1 < T;
+    const int64_t oa = (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
+    const int64_t on = (int64_t)(t + 1) * M * G4;
+    const int ns = (up ? 1 : 0) + (nx ? 1 : 0);
+    const int w0 = ns >= 1 ? G4 : 0, w1 = ns >= 2 ? G4 : 0;
+    SegKC la{{up ? GsAll + oa : Gz + on, up ? Gz + on : nullptr, nullptr, nullptr}, {w0, w1, 0, 0}, M};
+    SegKC la2{{up ? RGsAll + oa : RGz + on, up ? RGz + on : nullptr, nullptr, nullptr}, {w0, w1, 0, 0}, M};
+    SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {w0, w1}, H};
+    SegMC lb2{{up ? u + wih_up : u + lo.whh, u + lo.whh}, {w0, w1}, H};
+    if (ns) gemm_dual_mainloop<CfgNND>(la, la2, lb, lb2, m0, n0, ns * G4, 0, ap, at, smem);
   }
   const bool first = (t == T - 1);
+  const bool head = first && l == L - 1;
+  const float* dHz = dHhead + (int64_t)z * M * H;
+  const float* RdHz = RdHhead + (int64_t)z * M * H;
   const bool full = m0 + CfgNND::BM <= M;
   const int rb = m0 + acc_row<CfgNND>(0, 0);
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
@@ -330,8 +331,8 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __r
       const uint32_t oh = row * H + j;
       const uint32_t og = row * G4 + j;
       const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = ap.v[0][jj][r] + (dh_zero ? 0.f : ldb(dHz, 4u * (oh)));
-      const float rdh = at.v[0][jj][r] + (dh_zero ? 0.f : ldb(RdHz, 4u * (oh)));
+      const float dh = ap.v[0][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
+      const float rdh = at.v[0][jj][r] + (head ? ldb(RdHz, 4u * oc) : 0.f);
       const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
       const float ri = ldb(RGz, 4u * (og)), rf = ldb(RGz, 4u * (og + H)), rgg = ldb(RGz, 4u * (og + 2 * H)), ro = ldb(RGz, 4u * (og + 3 * H));
       const float c = ldb(Cz, 4u * (oh)), rc = ldb(RCz, 4u * (oh));
@@ -345,35 +346,39 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __r
       const float dct = dcin + dh * go * s2;
       const float rdct = rdcin + rdh * go * s2 + dh * ro * s2 - 2.f * dh * go * tc * rtc;
       const float si = gi * (1.f - gi), sf = gf * (1.f - gf), so = go * (1.f - go), sg = 1.f - gg * gg;
-      stb(dGz, 4u * (og), dct * gg * si);
-      stb(dGz, 4u * (og + H), dct * cp * sf);
-      stb(dGz, 4u * (og + 2 * H), dct * gi * sg);
-      stb(dGz, 4u * (og + 3 * H), dh * tc * so);
-      stb(RdGz, 4u * (og), rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri);
-      stb(RdGz, 4u * (og + H), rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf);
-      stb(RdGz, 4u * (og + 2 * H), rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg);
-      stb(RdGz, 4u * (og + 3 * H), rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro);
+      stb(Gz, 4u * (og), dct * gg * si);
+      stb(Gz, 4u * (og + H), dct * cp * sf);
+      stb(Gz, 4u * (og + 2 * H), dct * gi * sg);
+      stb(Gz, 4u * (og + 3 * H), dh * tc * so);
+      stb(RGz, 4u * (og), rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri);
+      stb(RGz, 4u * (og + H), rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf);
+      stb(RGz, 4u * (og + 2 * H), rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg);
+      stb(RGz, 4u * (og + 3 * H), rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro);
       stb(dcz, 4u * (oc), dct * gf);
       stb(rdcz, 4u * (oc), rdct * gf + dct * rf);
     }
   }
 }
 
-void launch_lstm_bwd_dual(hipStream_t s, const Dims& d, const Work& w, int l, int t, const float* theta,
-                          const float* U, int64_t tstride, const LayerOff& lo) {
+void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
+                               const float* U, int64_t tstride, const ParamOff& po) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-  const int dh_zero = (l == d.L - 1 && t < d.T - 1) ? 1 : 0;
-  const int64_t wgs = (int64_t)((w.M + CfgNND::BM - 1) / CfgNND::BM) * ((d.H + CfgNND::BN - 1) / CfgNND::BN) * w.Z;
-  if (wgs >= 3 * 256) {
-    dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
+  BwdWave wv{};
+  const int ntm = (w.M + CfgNND::BM - 1) / CfgNND::BM, ntn = (d.H + CfgNND::BN - 1) / CfgNND::BN;
+  bwd_wave(d, w, po, e, ntm, true, wv);
+  if (wv.n == 0) return;
+  if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
+    dim3 grid(wv.off[wv.n], ntn, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgNND><<<grid, CfgNND::NTH, 0, s>>>(
-                              w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
-                              w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, t, dh_zero));
+                              w.Gs, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv, d.L,
+                              d.T, w.M));
   } else {
-    dim3 grid((w.M + CfgNNDs::BM - 1) / CfgNNDs::BM, (d.H + CfgNNDs::BN - 1) / CfgNNDs::BN, w.Z);
+    const int ntms = (w.M + CfgNNDs::BM - 1) / CfgNNDs::BM, ntns = (d.H + CfgNNDs::BN - 1) / CfgNNDs::BN;
+    bwd_wave(d, w, po, e, ntms, true, wv);
+    dim3 grid(wv.off[wv.n], ntns, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgNNDs><<<grid, CfgNNDs::NTH, 0, s>>>(
-                              w.dG, w.RdG, w.dH, w.RdH, w.dc, w.Rdc, w.Gs + l * lsz * 4, w.Cs + l * lsz,
-                              w.RGs + l * lsz * 4, w.RCs + l * lsz, theta, U, tstride, lo, d.T, w.M, t, dh_zero));
+                              w.Gs, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv, d.L,
+                              d.T, w.M));
   }
 }
 

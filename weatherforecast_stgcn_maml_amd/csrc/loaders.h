@@ -207,23 +207,32 @@ __device__ __forceinline__ bool gate_tile(int ntm, int ngrp, int& tm, int& ug) {
   return gate_tile((int)blockIdx.x, ntm, ngrp, tm, ug);
 }
 
-// The wavefront problem (kernels.h FwdWave) owning block bx, selected with scalar compares
-// (no dynamic indexing into the by-value kernel argument).
-template <class WV, class LO>
-__device__ __forceinline__ void wave_problem(const WV& wv, int bx, int& l, int& t, LO& lo, int& b0) {
+// Wavefront problems (kernels.h FwdWave / BwdWave): the problem owning block bx, and a field
+// of it, selected with scalar compares (no dynamic indexing into the by-value kernel argument).
+template <class WV>
+__device__ __forceinline__ int wave_index(const WV& wv, int bx) {
   constexpr int NQ = (int)(sizeof(wv.l) / sizeof(wv.l[0]));
-  l = wv.l[0];
-  t = wv.t[0];
-  lo = wv.lo[0];
-  b0 = 0;
+  int p = 0;
 #pragma unroll
   for (int q = 1; q < NQ; ++q)
-    if (q < wv.n && bx >= wv.off[q]) {
-      l = wv.l[q];
-      t = wv.t[q];
-      lo = wv.lo[q];
-      b0 = wv.off[q];
-    }
+    if (q < wv.n && bx >= wv.off[q]) p = q;
+  return p;
+}
+template <class T, int N>
+__device__ __forceinline__ T wave_sel(const T (&a)[N], int p) {
+  T v = a[0];
+#pragma unroll
+  for (int q = 1; q < N; ++q)
+    if (q == p) v = a[q];
+  return v;
+}
+template <class WV, class LO>
+__device__ __forceinline__ void wave_problem(const WV& wv, int bx, int& l, int& t, LO& lo, int& b0) {
+  const int p = wave_index(wv, bx);
+  l = wave_sel(wv.l, p);
+  t = wave_sel(wv.t, p);
+  lo = wave_sel(wv.lo, p);
+  b0 = wave_sel(wv.off, p);
 }
 
 // Row offset (within the 32-row tile) of accumulator register r: (r&3) + 8*(r>>2).
