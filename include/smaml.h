@@ -141,6 +141,62 @@ int smaml_adapt_steps(smaml_ctx* ctx, void* stream, float* theta, float* m, floa
                       float beta1, float beta2, float eps, float weight_decay, float max_norm,
                       float* losses);
 
+/* ---- finer-grained operators (the module pieces callers compose) -------- */
+
+/* Backward of the most recent smaml_forward (same theta): dpred [nsamples][N*Hf][C]
+ * (device) = dLoss/dpred -> grad [P] (trainable layout, overwritten; GCN gets none: F2).
+ * What loss.backward() computes through HybridSTGCN_LSTM.forward (hybrid_model.py:80-117,
+ * train_hybrid_maml_v5.py:134). Consumes the saved activations (ESTATE if there are none). */
+int smaml_backward(smaml_ctx* ctx, void* stream, const float* theta, const float* dpred, float* grad);
+
+/* GCN x4 of extract_base_features (hybrid_model.py:60-78, no_grad): x_host[s] = device
+ * pointer to sample s's window [T*N][Cin0] -> feats [nsamples][T*N][Hc] (device). */
+int smaml_gcn_forward(smaml_ctx* ctx, void* stream, const float* const* x_host, int32_t nsamples, float* feats);
+
+/* nn.LSTM stack (hybrid_model.py:93-102) over layer-0 inputs feats [nsamples][T*N][Hc]
+ * (device, row t*N+n) -> hT [nsamples][N][H] (top layer, t = T-1). Saves the activations
+ * for smaml_lstm_backward. */
+int smaml_lstm_forward(smaml_ctx* ctx, void* stream, const float* theta, const float* feats, int32_t nsamples,
+                       float* hT);
+
+/* BPTT after smaml_lstm_forward: dhT [nsamples][N][H] (device) -> the LSTM entries of
+ * grad [P] (overwritten; head entries zero). */
+int smaml_lstm_backward(smaml_ctx* ctx, void* stream, const float* theta, const float* dhT, float* grad);
+
+/* Head + MSELoss with the F4 row pairing (hybrid_model.py:105-115, train_hybrid_maml_v5.py:
+ * 119,133): hT [nsamples][N][H] -> pred [nsamples][N*Hf][C]. With targets (y_host[s] = device
+ * pointer to y [Hf*N][C], dataset.py:40-48): loss (1 device float, mean over samples and
+ * elements) and dpred = dloss/dpred [nsamples][N*Hf][C]. y_host NULL: prediction only. */
+int smaml_head_loss(smaml_ctx* ctx, void* stream, const float* theta, const float* hT, const float* const* y_host,
+                    int32_t nsamples, float* pred, float* loss, float* dpred);
+
+/* clip_grad_norm_(max_norm) + SGD(lr) (train_hybrid_maml_v5.py:135-139) on ntasks flat
+ * vectors theta/grad [ntasks][P] (device), theta in place; norms [ntasks] (optional). */
+int smaml_clip_sgd(smaml_ctx* ctx, void* stream, float* theta, const float* grad, int32_t ntasks, float lr,
+                   float max_norm, float* norms);
+
+/* inner_loop_v4 (train_hybrid_maml_v5.py:110-141) for every task of smaml_set_tasks:
+ * `steps` support steps of `batch` windows (windows_host [steps+1][ntasks][batch], the last
+ * row is the query batch, evaluated but not trained on) -> fast_out [ntasks][P]; losses /
+ * norms as in smaml_meta_step. */
+int smaml_inner_loop(smaml_ctx* ctx, void* stream, const float* theta, int32_t steps, int32_t batch,
+                     const int32_t* windows_host, float inner_lr, float max_norm, float* fast_out, float* losses,
+                     float* norms);
+
+/* Device memory on the context's GPU (for hosts without their own allocator). */
+int smaml_alloc(smaml_ctx* ctx, int64_t bytes, void** out);
+int smaml_free(smaml_ctx* ctx, void* p);
+
+/* ---- RCCL communicator (one process per GPU) ---------------------------- *
+ * librccl is loaded on first use. Rank 0 calls smaml_comm_unique_id and ships the 128 bytes
+ * to the other ranks (env/file/store); every rank then calls smaml_comm_init. The meta-
+ * gradient all-reduce of one meta-step is smaml_comm_allreduce(meta_grad, P) (in-place sum,
+ * fp32, on the given stream). The Python path uses torch.distributed's RCCL instead. */
+int smaml_comm_unique_id(uint8_t* id_out /* 128 bytes */);
+int smaml_comm_init(smaml_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id /* 128 bytes */);
+int smaml_comm_allreduce(smaml_ctx* ctx, void* stream, float* buf, int64_t n);
+int smaml_comm_destroy(smaml_ctx* ctx);
+
 /* ---- measurement (no reference counterpart; bench / profiling only) ------------------ */
 
 /* Enable/disable per-kernel-category HIP-event timing of the launches this context

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
     assert decl == sorted(_capi.EXPORTS)
     for name in decl:
         assert hasattr(L, name), name
-    assert L.smaml_abi_version() == 1
+    assert L.smaml_abi_version() == _capi.ABI_VERSION
 
 
 @pytest.mark.parametrize("d", [CONFIG1, CONFIG2])

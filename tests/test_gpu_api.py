@@ -1,0 +1,234 @@
+"""GPU parity of the finer-grained C ABI and of the torch.autograd shim
+(§8(f) rank 2) against the CPU oracle (torch autograd through oracle/refcpu.py).
+
+Tolerances (fp32): predictions, losses, parameters after training steps <= 1e-5 rel-L2
+(SURVEY §8c); gradients <= 1e-4 rel-L2 (BPTT sums over T*N*B rows in a different order).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import refcpu
+from weatherforecast_stgcn_maml_amd import _capi, params, synth
+from weatherforecast_stgcn_maml_amd.config import CONFIG1, CONFIG2, MamlConfig
+from weatherforecast_stgcn_maml_amd.maml import window_table
+
+from test_gpu_parity import DEV, build_hybrid, grid_edges, rel, split
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_grads(P, x, y, ei, d):
+    """loss and d loss / d (LSTM, head) of one sample through the oracle (CPU autograd)."""
+    Pt = {k: torch.from_numpy(v).clone().requires_grad_(k.startswith(("lstm.", "output_layer.")))
+          for k, v in P.items()}
+    pred = refcpu.hybrid_forward(Pt, torch.from_numpy(x), torch.from_numpy(ei).long(), d)
+    loss = refcpu.mse(pred, torch.from_numpy(y))
+    loss.backward()
+    return float(loss), pred.detach().numpy(), {k: v.grad.numpy() for k, v in Pt.items() if v.grad is not None}
+
+
+@pytest.mark.parametrize("d", [CONFIG1, CONFIG2])
+def test_autograd_shim_grads_match_oracle(d):
+    P = synth.init_params(7, d, gcn_bias_scale=0.1)
+    ei = grid_edges(d)
+    feats = synth.make_features(synth.task_seed(3), d.num_nodes, synth.t_total_for(4))
+    x, y = synth.sample_xy(feats, 2)
+    loss_o, pred_o, g_o = oracle_grads(P, x, y, ei, d)
+
+    m = build_hybrid(d, P).train()
+    xg = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    pred = m(xg, torch.from_numpy(ei).to(DEV))
+    assert pred.grad_fn is not None
+    loss = torch.nn.functional.mse_loss(pred, torch.from_numpy(y).to(DEV))
+    loss.backward()
+    assert rel(pred.detach().cpu(), pred_o) < 1e-5
+    assert abs(float(loss) - loss_o) < 1e-5 * loss_o
+    sd = dict(m.named_parameters())
+    for k, g in g_o.items():
+        assert sd[k].grad is not None, k
+        assert rel(sd[k].grad.cpu(), g) < 1e-4, (k, rel(sd[k].grad.cpu(), g))
+    for k in sd:  # the reference runs the GCN under no_grad (F2)
+        if k.startswith("base_stgcn."):
+            assert sd[k].grad is None
+
+
+def test_unmodified_sgd_loop_matches_oracle():
+    """The reference's inner loop body (train_hybrid_maml_v5.py:130-139) written with plain
+    torch calls -- loss.backward(), clip_grad_norm_, optim.SGD -- over the HIP module."""
+    d = CONFIG1
+    P = synth.init_params(11, d, gcn_bias_scale=0.1)
+    ei = grid_edges(d)
+    feats = synth.make_features(synth.task_seed(0), d.num_nodes, synth.t_total_for(6))
+
+    def run(model_params, forward, steps=6):
+        opt = torch.optim.SGD(model_params, lr=0.01)
+        losses = []
+        for i in range(steps):
+            x, y = synth.sample_xy(feats, i)
+            pred, yt = forward(x, y)
+            loss = torch.nn.functional.mse_loss(pred, yt)
+            opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model_params, 1.0)
+            opt.step()
+            losses.append(float(loss))
+        return losses
+
+    m = build_hybrid(d, P).train()
+    eig = torch.from_numpy(ei).to(DEV)
+    hip_losses = run(m.get_trainable_parameters(),
+                     lambda x, y: (m(torch.from_numpy(np.ascontiguousarray(x)).to(DEV), eig),
+                                   torch.from_numpy(y).to(DEV)))
+
+    Pt = {k: torch.from_numpy(v).clone().requires_grad_(k.startswith(("lstm.", "output_layer.")))
+          for k, v in P.items()}
+    tr = [v for k, v in Pt.items() if v.requires_grad]
+    eic = torch.from_numpy(ei).long()
+    ora_losses = run(tr, lambda x, y: (refcpu.hybrid_forward(Pt, torch.from_numpy(x), eic, d), torch.from_numpy(y)))
+    assert np.allclose(hip_losses, ora_losses, rtol=1e-5, atol=0)
+    sd = dict(m.named_parameters())
+    for k, v in Pt.items():
+        if v.requires_grad:
+            assert rel(sd[k].detach().cpu(), v.detach()) < 1e-5, k
+
+
+def test_lstm_and_head_operators_match_oracle():
+    d = CONFIG2
+    P = synth.init_params(5, d, gcn_bias_scale=0.1)
+    Ptr, Pg, names = split(P)
+    ei = grid_edges(d)
+    feats = synth.make_features(synth.task_seed(1), d.num_nodes, synth.t_total_for(3))
+    xs, ys = zip(*[synth.sample_xy(feats, i) for i in range(2)])
+    B, N, T, H = 2, d.num_nodes, d.window_size, d.lstm_hidden_size
+
+    ctx = _capi.Context(d, 0)
+    ctx.set_graph(ei)
+    ctx.set_gcn_params(params.pack({k: torch.from_numpy(v) for k, v in Pg.items()}, d, which=1, device=DEV))
+    theta = params.pack({k: torch.from_numpy(v) for k, v in Ptr.items()}, d, device=DEV)
+    st = _capi.stream_ptr(torch)
+    xg = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in xs]
+    yg = [torch.from_numpy(np.ascontiguousarray(y)).to(DEV) for y in ys]
+    F = torch.empty(B, T * N, d.hidden_channels, device=DEV)
+    ctx.gcn_forward(st, xg, F)
+    hT = torch.empty(B, N, H, device=DEV)
+    ctx.lstm_forward(st, theta, F, hT)
+    pred = torch.empty(B, N * d.forecast_horizon, d.output_channels, device=DEV)
+    loss = torch.empty(1, device=DEV)
+    dpred = torch.empty_like(pred)
+    ctx.head_loss(st, theta, hT, pred, yg, loss, dpred)
+    Wo = params.unpack(theta, d)["output_layer.weight"]
+    dhT = (dpred.view(B * N, -1) @ Wo).view(B, N, H).contiguous()
+    grad = torch.empty_like(theta)
+    ctx.lstm_backward(st, theta, dhT, grad)
+    torch.cuda.synchronize()
+
+    # oracle: per-sample MSE averaged over the batch (F9), autograd on CPU
+    Pt = {k: torch.from_numpy(v).clone().requires_grad_(k in names) for k, v in P.items()}
+    eic = torch.from_numpy(ei).long()
+    Fo = [refcpu.stgcn_features(torch.from_numpy(x), eic, Pt).detach() for x in xs]
+    seq = torch.cat([f.view(T, N, -1).permute(1, 0, 2) for f in Fo])
+    hTo = refcpu.lstm_stack(seq, Pt, d.lstm_num_layers)
+    predo = (hTo @ Pt["output_layer.weight"].t() + Pt["output_layer.bias"]).view(B, N * d.forecast_horizon, -1)
+    losso = torch.stack([refcpu.mse(predo[b], torch.from_numpy(ys[b])) for b in range(B)]).mean()
+    losso.backward()
+
+    assert rel(F.cpu(), torch.stack(Fo)) < 1e-5
+    assert rel(hT.cpu(), hTo.detach().view(B, N, H)) < 1e-5
+    assert rel(pred.cpu(), predo.detach()) < 1e-5
+    assert abs(float(loss) - float(losso)) < 1e-5 * float(losso)
+    g = params.unpack(grad, d)
+    for k in names:
+        if k.startswith("lstm."):
+            assert rel(g[k].cpu(), Pt[k].grad) < 1e-4, k
+        else:
+            assert float(g[k].abs().max()) == 0.0, k  # lstm_backward leaves the head to the caller
+    # prediction-only head
+    pred2 = torch.empty_like(pred)
+    ctx.head_loss(st, theta, hT, pred2)
+    torch.cuda.synchronize()
+    assert torch.equal(pred2, pred)
+
+
+def test_backward_requires_forward_and_is_consumed():
+    d = CONFIG1
+    P = synth.init_params(2, d)
+    Ptr, Pg, _ = split(P)
+    ctx = _capi.Context(d, 0)
+    ctx.set_graph(grid_edges(d))
+    ctx.set_gcn_params(params.pack({k: torch.from_numpy(v) for k, v in Pg.items()}, d, which=1, device=DEV))
+    theta = params.pack({k: torch.from_numpy(v) for k, v in Ptr.items()}, d, device=DEV)
+    grad = torch.empty_like(theta)
+    dpred = torch.zeros(d.num_nodes * d.forecast_horizon, d.output_channels, device=DEV)
+    st = _capi.stream_ptr(torch)
+    with pytest.raises(_capi.SmamlError, match="ESTATE"):
+        ctx.backward(st, theta, dpred, grad)
+    feats = synth.make_features(synth.task_seed(0), d.num_nodes, synth.t_total_for(1))
+    x, _ = synth.sample_xy(feats, 0)
+    pred = torch.empty_like(dpred)
+    ctx.forward(st, theta, [torch.from_numpy(np.ascontiguousarray(x)).to(DEV)], pred)
+    ctx.backward(st, theta, dpred, grad)
+    torch.cuda.synchronize()
+    assert float(grad.abs().max()) == 0.0  # zero upstream gradient
+    with pytest.raises(_capi.SmamlError, match="ESTATE"):  # activations consumed (dG in place)
+        ctx.backward(st, theta, dpred, grad)
+
+
+def test_clip_sgd_matches_torch():
+    d = CONFIG2
+    ctx = _capi.Context(d, 0)
+    P = params.trainable_layout(d)[1]
+    g = torch.Generator().manual_seed(0)
+    theta = torch.randn(3, P, generator=g).to(DEV)
+    grad = (torch.randn(3, P, generator=g) * torch.tensor([[0.001], [1.0], [30.0]])).to(DEV)
+    norms = torch.empty(3, device=DEV)
+    ref = theta.clone()
+    for z in range(3):
+        n = float(grad[z].double().norm())
+        coef = min(1.0 / (n + 1e-6), 1.0)
+        ref[z] -= 0.01 * grad[z] * coef
+    ctx.clip_sgd(_capi.stream_ptr(torch), theta, grad, 3, 0.01, 1.0, norms)
+    torch.cuda.synchronize()
+    assert rel(theta.cpu(), ref.cpu()) < 1e-6
+    assert np.allclose(norms.cpu().numpy(), grad.double().norm(dim=1).cpu().numpy(), rtol=1e-5)
+
+
+def test_inner_loop_equals_meta_step_fast_weights():
+    d = CONFIG1
+    P = synth.init_params(3, d)
+    Ptr, Pg, _ = split(P)
+    ctx = _capi.Context(d, 0)
+    ctx.set_graph(grid_edges(d))
+    ctx.set_gcn_params(params.pack({k: torch.from_numpy(v) for k, v in Pg.items()}, d, which=1, device=DEV))
+    theta = params.pack({k: torch.from_numpy(v) for k, v in Ptr.items()}, d, device=DEV)
+    streams = [torch.from_numpy(synth.make_features(synth.task_seed(j), d.num_nodes, synth.t_total_for(8))).to(DEV)
+               for j in range(2)]
+    ctx.set_tasks(streams)
+    K, B = 3, 2
+    w = window_table(MamlConfig(inner_steps=K, batch=B), 2)
+    st = _capi.stream_ptr(torch)
+    fa = torch.empty(2, theta.numel(), device=DEV)
+    fb = torch.empty_like(fa)
+    la = torch.empty(K + 1, 2, device=DEV)
+    lb = torch.empty_like(la)
+    ctx.inner_loop(st, theta, K, B, w, 0.01, 1.0, fa, la)
+    ctx.meta_step(st, theta, 0, K, B, w, 0.01, 1.0, 1.0, losses=lb, fast_out=fb)
+    torch.cuda.synchronize()
+    assert torch.equal(fa, fb) and torch.equal(la, lb)
+
+
+def test_alloc_free_and_world1_comm():
+    d = CONFIG1
+    ctx = _capi.Context(d, 0)
+    p = ctx.alloc(1 << 20)
+    assert p
+    ctx.free(p)
+    uid = _capi.comm_unique_id()
+    assert len(uid) == 128
+    ctx.comm_init(0, 1, uid)
+    buf = torch.arange(1000, dtype=torch.float32, device=DEV)
+    ref = buf.clone()
+    ctx.comm_allreduce(_capi.stream_ptr(torch), buf)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)  # world 1: sum over one rank
+    ctx.comm_destroy()

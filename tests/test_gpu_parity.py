@@ -66,7 +66,8 @@ def test_forward_matches_reference(golden_dir, d, name):
     x, y = synth.sample_xy(feats, 0)
     xg = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
     eig = torch.from_numpy(z["edge_index"]).to(DEV)
-    pred = m(xg, eig).cpu().numpy()
+    with torch.no_grad():  # eval-style call (the module is differentiable otherwise)
+        pred = m(xg, eig).cpu().numpy()
     assert pred.shape == z["pred0"].shape
     assert rel(pred, z["pred0"]) < 1e-5
     mse = float(((pred - y) ** 2).mean())

@@ -20,7 +20,11 @@ EXPORTS = (
     "smaml_create", "smaml_destroy", "smaml_set_graph", "smaml_set_gcn_params", "smaml_reserve",
     "smaml_workspace_bytes", "smaml_gcn_conv", "smaml_forward", "smaml_set_tasks",
     "smaml_meta_step", "smaml_adamw_step", "smaml_adapt_steps", "smaml_timing", "smaml_timing_collect",
+    "smaml_backward", "smaml_gcn_forward", "smaml_lstm_forward", "smaml_lstm_backward", "smaml_head_loss",
+    "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
+    "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy",
 )
+ABI_VERSION = 2
 
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "head_loss", "head_dh", "lstm_bwd_step",
                      "wgrad", "dx", "misc")
@@ -75,6 +79,19 @@ _SIGS = {
     "smaml_adamw_step": ([P, P, P, P, P, P, I64, I32, F32, F32, F32, F32, F32, F32, P], I32),
     "smaml_adapt_steps": ([P, P, P, P, P, I32, I32, I32, PI32, P, F32, F32, F32, F32, F32, P], I32),
     "smaml_timing": ([P, I32], I32),
+    "smaml_backward": ([P, P, P, P, P], I32),
+    "smaml_gcn_forward": ([P, P, ctypes.POINTER(P), I32, P], I32),
+    "smaml_lstm_forward": ([P, P, P, P, I32, P], I32),
+    "smaml_lstm_backward": ([P, P, P, P, P], I32),
+    "smaml_head_loss": ([P, P, P, P, ctypes.POINTER(P), I32, P, P, P], I32),
+    "smaml_clip_sgd": ([P, P, P, P, I32, F32, F32, P], I32),
+    "smaml_inner_loop": ([P, P, P, I32, I32, PI32, F32, F32, P, P, P], I32),
+    "smaml_alloc": ([P, I64, ctypes.POINTER(P)], I32),
+    "smaml_free": ([P, P], I32),
+    "smaml_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], I32),
+    "smaml_comm_init": ([P, I32, I32, ctypes.POINTER(ctypes.c_uint8)], I32),
+    "smaml_comm_allreduce": ([P, P, P, I64], I32),
+    "smaml_comm_destroy": ([P], I32),
     "smaml_timing_collect": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               PI64, I32], I32),
 }
@@ -88,6 +105,9 @@ def lib():
             if not os.path.exists(LIB_PATH):
                 raise SmamlError(-1, f"{LIB_PATH} not built; run __graft_entry__.build()")
             L = ctypes.CDLL(LIB_PATH)
+            L.smaml_abi_version.restype = I32
+            if L.smaml_abi_version() != ABI_VERSION:
+                raise SmamlError(-1, f"{LIB_PATH} has ABI {L.smaml_abi_version()}, expected {ABI_VERSION}; rebuild")
             for name, (args, res) in _SIGS.items():
                 fn = getattr(L, name)
                 fn.argtypes = args
@@ -128,6 +148,17 @@ def graph_ell(edge_index: np.ndarray, num_nodes: int):
 
 def ptr(t) -> int:
     return t.data_ptr()
+
+
+def _ptrs(ts):
+    return (P * len(ts))(*[ptr(t) for t in ts])
+
+
+def comm_unique_id() -> bytes:
+    """128-byte RCCL unique id (rank 0), to ship to the other ranks."""
+    buf = (ctypes.c_uint8 * 128)()
+    check(lib().smaml_comm_unique_id(buf))
+    return bytes(buf)
 
 
 def stream_ptr(torch_mod):
@@ -207,6 +238,53 @@ class Context:
         check(self._L.smaml_adapt_steps(self._h, stream, ptr(theta), ptr(m), ptr(v), int(step0), w.shape[0],
                                         w.shape[1], w.ctypes.data_as(PI32), ptr(lr_dev), float(betas[0]),
                                         float(betas[1]), float(eps), float(wd), float(max_norm), ptr(losses)))
+
+    def backward(self, stream, theta, dpred, grad):
+        check(self._L.smaml_backward(self._h, stream, ptr(theta), ptr(dpred), ptr(grad)))
+
+    def gcn_forward(self, stream, xs, feats):
+        check(self._L.smaml_gcn_forward(self._h, stream, _ptrs(xs), len(xs), ptr(feats)))
+
+    def lstm_forward(self, stream, theta, feats, hT):
+        check(self._L.smaml_lstm_forward(self._h, stream, ptr(theta), ptr(feats), int(feats.shape[0]), ptr(hT)))
+
+    def lstm_backward(self, stream, theta, dhT, grad):
+        check(self._L.smaml_lstm_backward(self._h, stream, ptr(theta), ptr(dhT), ptr(grad)))
+
+    def head_loss(self, stream, theta, hT, pred, ys=None, loss=None, dpred=None):
+        check(self._L.smaml_head_loss(self._h, stream, ptr(theta), ptr(hT), _ptrs(ys) if ys is not None else None,
+                                      int(hT.shape[0]), ptr(pred), ptr(loss) if loss is not None else None,
+                                      ptr(dpred) if dpred is not None else None))
+
+    def clip_sgd(self, stream, theta, grad, ntasks, lr, max_norm, norms=None):
+        check(self._L.smaml_clip_sgd(self._h, stream, ptr(theta), ptr(grad), int(ntasks), float(lr),
+                                     float(max_norm), ptr(norms) if norms is not None else None))
+
+    def inner_loop(self, stream, theta, steps, batch, windows: np.ndarray, inner_lr, max_norm, fast_out,
+                   losses=None, norms=None):
+        w = np.ascontiguousarray(windows, dtype=np.int32)
+        check(self._L.smaml_inner_loop(self._h, stream, ptr(theta), int(steps), int(batch), w.ctypes.data_as(PI32),
+                                       float(inner_lr), float(max_norm), ptr(fast_out),
+                                       ptr(losses) if losses is not None else None,
+                                       ptr(norms) if norms is not None else None))
+
+    def alloc(self, nbytes: int) -> int:
+        out = P()
+        check(self._L.smaml_alloc(self._h, int(nbytes), ctypes.byref(out)))
+        return out.value
+
+    def free(self, p: int):
+        check(self._L.smaml_free(self._h, P(p)))
+
+    def comm_init(self, rank: int, world: int, uid: bytes):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self._L.smaml_comm_init(self._h, int(rank), int(world), buf))
+
+    def comm_allreduce(self, stream, buf):
+        check(self._L.smaml_comm_allreduce(self._h, stream, ptr(buf), buf.numel()))
+
+    def comm_destroy(self):
+        check(self._L.smaml_comm_destroy(self._h))
 
     def timing(self, enable: bool):
         check(self._L.smaml_timing(self._h, 1 if enable else 0))

@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
+#include <dlfcn.h>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -185,6 +187,11 @@ struct smaml_ctx {
   float* so_F = nullptr;  // [K][Z][T][M][Hc] GCN features of every inner step (null: recompute)
   int64_t so_F_cap = 0;
   float* F_main = nullptr;  // the workspace's own F buffer
+  // activations of the last smaml_forward / smaml_lstm_forward (single task, act_B samples);
+  // -1 once anything else has used the workspace (the backward consumes them: dG in place)
+  int act_B = -1;
+  // RCCL communicator (smaml_comm_init), opaque
+  void* comm = nullptr;
 };
 
 namespace {
@@ -240,6 +247,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   }
   int64_t total = 0;
   for (auto& p : parts) total += (p.second + 255) / 256 * 256;
+  c->act_B = -1;
   if (c->arena) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipFree(c->arena));
@@ -338,6 +346,7 @@ int upload_xtab(smaml_ctx* c, hipStream_t s, const float* const* ptrs, int64_t n
 }
 
 void set_work(smaml_ctx* c, int Z, int B) {
+  c->act_B = -1;  // any new use of the workspace ends the validity of saved activations
   c->w.Z = Z;
   c->w.B = B;
   c->w.M = B * c->d.N;
@@ -358,8 +367,8 @@ void set_work(smaml_ctx* c, int Z, int B) {
     }                                                            \
   } while (0)
 
-// GCN x4 (no_grad, F2) + LSTM forward over all layers and time steps.
-int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev) {
+// GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc].
+int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
   const Dims& d = c->d;
   Work& w = c->w;
   const int rps = d.T * d.N;
@@ -375,6 +384,14 @@ int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride
                            rps, d.N));
     src = dst;
   }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+// LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront).
+int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
+  const Dims& d = c->d;
+  Work& w = c->w;
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     const double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
@@ -383,6 +400,13 @@ int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
+
+int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev) {
+  TRY(run_gcn(c, s, xtab_dev));
+  return run_lstm(c, s, theta, tstride);
+}
+
+int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, float* grad);
 
 // Backward from dpred (already written by k_head_loss) into grad [Z][P].
 int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, float* grad) {
@@ -396,6 +420,16 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
         launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, top + (int64_t)(d.T - 1) * w.M * d.H,
                      TM * d.H, d.H, nullptr, 0, 0, w.M, 0, grad, po.P, po.wo, -1, po.bo, -1));
+  return run_bptt(c, s, theta, tstride, grad);
+}
+
+// BPTT + LSTM weight gradients from the top layer's dh_T in w.dH [Z][M][H].
+int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, float* grad) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  const ParamOff& po = c->po;
+  const int64_t TM = (int64_t)d.T * w.M;
+  const int64_t lsz = (int64_t)w.Z * TM * d.H;
   // BPTT as reverse anti-diagonals; layer l's weight gradient as soon as its t = 0 step is done
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
@@ -495,7 +529,7 @@ extern "C" {
 
 const char* smaml_last_error(void) { return g_err.c_str(); }
 
-int32_t smaml_abi_version(void) { return 1; }
+int32_t smaml_abi_version(void) { return 2; }
 
 int smaml_param_layout(const smaml_dims* dims, int32_t which, int64_t* offsets, int64_t* sizes, int32_t cap,
                        int32_t* count, int64_t* total) {
@@ -581,6 +615,7 @@ int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out) {
 int smaml_destroy(smaml_ctx* c) {
   if (!c) return SMAML_OK;
   (void)hipSetDevice(c->device);
+  if (c->comm) (void)smaml_comm_destroy(c);
   (void)hipDeviceSynchronize();
   if (c->arena) (void)hipFree(c->arena);
   if (c->ell_c) (void)hipFree(c->ell_c);
@@ -665,6 +700,7 @@ int smaml_forward(smaml_ctx* c, void* stream, const float* theta, const float* c
   Work w = c->w;
   w.pred = pred;
   launch_head_loss(s, c->d, w, theta, 0, c->po, nullptr, 0.f, false);
+  c->act_B = nsamples;
   if (feats) {
     const Dims& d = c->d;
     const int64_t blk = (int64_t)d.N * d.Hc;
@@ -874,6 +910,239 @@ int smaml_adamw_step(smaml_ctx* c, void* stream, float* theta, const float* grad
                (float)(lr / bc1), (float)std::sqrt(bc2), max_norm, norm_out);
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
+}
+
+
+// ---- finer-grained entry points --------------------------------------
+
+int smaml_backward(smaml_ctx* c, void* stream, const float* theta, const float* dpred, float* grad) {
+  TRY(require_ready(c));
+  if (!theta || !dpred || !grad) return fail(SMAML_EINVAL, "bad backward arguments");
+  if (c->act_B < 1 || c->w.Z != 1) return fail(SMAML_ESTATE, "smaml_backward needs the activations of smaml_forward");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  const Dims& d = c->d;
+  // dpred [B][N*Hf][C] (rows n*Hf+h) == w.dpred [M = B*N][Hf*C]: same flat order
+  HIP_TRY(hipMemcpyAsync(c->w.dpred, dpred, (size_t)c->w.M * d.HfC * 4, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemsetAsync(grad, 0, (size_t)c->po.P * 4, s));
+  c->act_B = -1;  // the BPTT overwrites the saved gates with dG
+  TRY(run_backward(c, s, theta, 0, grad));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_gcn_forward(smaml_ctx* c, void* stream, const float* const* x_host, int32_t nsamples, float* feats) {
+  TRY(require_ready(c));
+  if (!x_host || nsamples <= 0 || !feats) return fail(SMAML_EINVAL, "bad gcn_forward arguments");
+  for (int i = 0; i < nsamples; ++i)
+    if (!x_host[i] || !aligned16(x_host[i])) return fail(SMAML_EINVAL, "sample x pointers must be 16-B aligned");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  TRY(reserve(c, 1, nsamples));
+  set_work(c, 1, nsamples);
+  TRY(upload_xtab(c, s, x_host, nsamples));
+  TRY(run_gcn(c, s, c->xtab));
+  const Dims& d = c->d;
+  const int64_t blk = (int64_t)d.N * d.Hc;
+  for (int si = 0; si < nsamples; ++si)  // F [T][M][Hc] -> feats [s][T*N][Hc]
+    HIP_TRY(hipMemcpy2DAsync(feats + (int64_t)si * d.T * blk, blk * 4, c->w.F + (int64_t)si * blk,
+                             (int64_t)nsamples * blk * 4, blk * 4, d.T, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_lstm_forward(smaml_ctx* c, void* stream, const float* theta, const float* feats, int32_t nsamples,
+                       float* hT) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!theta || !feats || nsamples <= 0 || !hT) return fail(SMAML_EINVAL, "bad lstm_forward arguments");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  TRY(reserve(c, 1, nsamples));
+  set_work(c, 1, nsamples);
+  const Dims& d = c->d;
+  const int64_t blk = (int64_t)d.N * d.Hc;
+  for (int si = 0; si < nsamples; ++si)  // feats [s][T*N][Hc] -> F [T][M][Hc]
+    HIP_TRY(hipMemcpy2DAsync(c->w.F + (int64_t)si * blk, (int64_t)nsamples * blk * 4, feats + (int64_t)si * d.T * blk,
+                             blk * 4, blk * 4, d.T, hipMemcpyDeviceToDevice, s));
+  TRY(run_lstm(c, s, theta, 0));
+  const int64_t lsz = (int64_t)d.T * c->w.M * d.H;
+  const float* top = c->w.Hs + (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * c->w.M * d.H;
+  HIP_TRY(hipMemcpyAsync(hT, top, (size_t)c->w.M * d.H * 4, hipMemcpyDeviceToDevice, s));
+  c->act_B = nsamples;
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_lstm_backward(smaml_ctx* c, void* stream, const float* theta, const float* dhT, float* grad) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!theta || !dhT || !grad) return fail(SMAML_EINVAL, "bad lstm_backward arguments");
+  if (c->act_B < 1 || c->w.Z != 1)
+    return fail(SMAML_ESTATE, "smaml_lstm_backward needs the activations of smaml_lstm_forward");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(c->w.dH, dhT, (size_t)c->w.M * c->d.H * 4, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemsetAsync(grad, 0, (size_t)c->po.P * 4, s));
+  c->act_B = -1;
+  TRY(run_bptt(c, s, theta, 0, grad));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_head_loss(smaml_ctx* c, void* stream, const float* theta, const float* hT, const float* const* y_host,
+                    int32_t nsamples, float* pred, float* loss, float* dpred) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!theta || !hT || nsamples <= 0 || !pred) return fail(SMAML_EINVAL, "bad head_loss arguments");
+  if (y_host && (!loss || !dpred)) return fail(SMAML_EINVAL, "loss and dpred are required with targets");
+  if (!aligned16(hT) || !aligned16(theta)) return fail(SMAML_EINVAL, "hT / theta must be 16-byte aligned");
+  TRY(ensure_device(c));
+  hipStream_t s = (hipStream_t)stream;
+  // the head only needs the small per-launch buffers; keep saved LSTM activations intact
+  if (nsamples > c->zb_cap) TRY(reserve(c, 1, nsamples));
+  const int act = c->act_B;
+  const Work saved = c->w;
+  set_work(c, 1, nsamples);
+  if (y_host) {
+    for (int i = 0; i < nsamples; ++i)
+      if (!y_host[i]) return fail(SMAML_EINVAL, "null target pointer");
+    TRY(upload_xtab(c, s, y_host, nsamples));
+  }
+  const Dims& d = c->d;
+  const float inv = 1.f / ((float)nsamples * d.N * d.HfC);  // mean over samples and elements (F9)
+  launch_head_loss_y(s, d, c->w, hT, theta, c->po, y_host ? c->xtab : nullptr, pred, dpred, 2.f * inv);
+  if (y_host) launch_loss_final(s, c->w, inv, loss);
+  c->w = saved;
+  c->act_B = act;
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_clip_sgd(smaml_ctx* c, void* stream, float* theta, const float* grad, int32_t ntasks, float lr,
+                   float max_norm, float* norms) {
+  if (!c || !theta || !grad || ntasks <= 0) return fail(SMAML_EINVAL, "bad clip_sgd arguments");
+  TRY(ensure_device(c));
+  if (ntasks > c->z_cap) TRY(reserve(c, ntasks, 1));
+  hipStream_t s = (hipStream_t)stream;
+  launch_sqsum(s, grad, c->po.P, ntasks, c->w.sqpart);
+  launch_clip_sgd(s, theta, grad, c->po.P, ntasks, c->w.sqpart, lr, max_norm, norms, nullptr);
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_inner_loop(smaml_ctx* c, void* stream, const float* theta, int32_t steps, int32_t batch,
+                     const int32_t* windows_host, float inner_lr, float max_norm, float* fast_out, float* losses,
+                     float* norms) {
+  if (!fast_out) return fail(SMAML_EINVAL, "fast_out is required");
+  return smaml_meta_step(c, stream, theta, 0, steps, batch, windows_host, inner_lr, max_norm, 1.f, nullptr, losses,
+                         norms, fast_out);
+}
+
+int smaml_alloc(smaml_ctx* c, int64_t bytes, void** out) {
+  if (!c || bytes <= 0 || !out) return fail(SMAML_EINVAL, "bad alloc arguments");
+  TRY(ensure_device(c));
+  if (hipMalloc(out, (size_t)bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return fail(SMAML_ENOMEM, "hipMalloc of " + std::to_string(bytes) + " B failed");
+  }
+  return SMAML_OK;
+}
+
+int smaml_free(smaml_ctx* c, void* p) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!p) return SMAML_OK;
+  TRY(ensure_device(c));
+  HIP_TRY(hipFree(p));
+  return SMAML_OK;
+}
+
+}  // extern "C"
+
+// ---- RCCL communicator (one process per GPU). librccl is resolved at first use with dlopen,
+// so the library has no link-time RCCL dependency (and shares the process's RCCL if torch
+// has already loaded one). Only the handful of symbols below are used.
+namespace {
+struct Rccl {
+  void* h = nullptr;
+  int (*get_unique_id)(void*) = nullptr;                                   // ncclGetUniqueId
+  int (*comm_init_rank)(void**, int, std::array<char, 128>, int) = nullptr;  // ncclCommInitRank
+  int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*comm_destroy)(void*) = nullptr;
+  const char* (*error_string)(int) = nullptr;
+};
+constexpr int NCCL_FLOAT32 = 7, NCCL_SUM = 0;  // ncclFloat32, ncclSum (nccl.h enums)
+
+int rccl(Rccl** out) {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+      r.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+      if (!r.h) r.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+      if (r.h) break;
+    }
+    if (r.h) {
+      r.get_unique_id = (int (*)(void*))dlsym(r.h, "ncclGetUniqueId");
+      r.comm_init_rank = (int (*)(void**, int, std::array<char, 128>, int))dlsym(r.h, "ncclCommInitRank");
+      r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(r.h, "ncclAllReduce");
+      r.comm_destroy = (int (*)(void*))dlsym(r.h, "ncclCommDestroy");
+      r.error_string = (const char* (*)(int))dlsym(r.h, "ncclGetErrorString");
+    }
+  }
+  if (!r.h || !r.get_unique_id || !r.comm_init_rank || !r.all_reduce || !r.comm_destroy)
+    return fail(SMAML_ESTATE, "librccl not found (dlopen librccl.so.1)");
+  *out = &r;
+  return SMAML_OK;
+}
+
+int nccl_fail(Rccl* r, int rc, const char* what) {
+  return fail(SMAML_EHIP, std::string(what) + ": " + (r->error_string ? r->error_string(rc) : std::to_string(rc)));
+}
+}  // namespace
+
+extern "C" {
+
+int smaml_comm_unique_id(uint8_t* id_out) {
+  if (!id_out) return fail(SMAML_EINVAL, "id_out is NULL");
+  Rccl* r = nullptr;
+  TRY(rccl(&r));
+  const int rc = r->get_unique_id(id_out);
+  return rc ? nccl_fail(r, rc, "ncclGetUniqueId") : SMAML_OK;
+}
+
+int smaml_comm_init(smaml_ctx* c, int32_t rank, int32_t world, const uint8_t* id) {
+  if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(SMAML_EINVAL, "bad comm_init arguments");
+  if (c->comm) return fail(SMAML_ESTATE, "communicator already initialised");
+  Rccl* r = nullptr;
+  TRY(rccl(&r));
+  TRY(ensure_device(c));
+  std::array<char, 128> uid;
+  std::memcpy(uid.data(), id, 128);
+  void* comm = nullptr;
+  const int rc = r->comm_init_rank(&comm, world, uid, rank);
+  if (rc) return nccl_fail(r, rc, "ncclCommInitRank");
+  c->comm = comm;
+  return SMAML_OK;
+}
+
+int smaml_comm_allreduce(smaml_ctx* c, void* stream, float* buf, int64_t n) {
+  if (!c || !buf || n < 0) return fail(SMAML_EINVAL, "bad allreduce arguments");
+  if (!c->comm) return fail(SMAML_ESTATE, "smaml_comm_init not called");
+  Rccl* r = nullptr;
+  TRY(rccl(&r));
+  TRY(ensure_device(c));
+  const int rc = r->all_reduce(buf, buf, (size_t)n, NCCL_FLOAT32, NCCL_SUM, c->comm, (hipStream_t)stream);
+  return rc ? nccl_fail(r, rc, "ncclAllReduce") : SMAML_OK;
+}
+
+int smaml_comm_destroy(smaml_ctx* c) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!c->comm) return SMAML_OK;
+  Rccl* r = nullptr;
+  TRY(rccl(&r));
+  const int rc = r->comm_destroy(c->comm);
+  c->comm = nullptr;
+  return rc ? nccl_fail(r, rc, "ncclCommDestroy") : SMAML_OK;
 }
 
 }  // extern "C"

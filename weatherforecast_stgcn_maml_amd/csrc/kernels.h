@@ -95,6 +95,8 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
                           int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                       const ParamOff& po, const float* const* xtab, float dscale, bool want_loss);
+void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float* hT, const float* theta,
+                        const ParamOff& po, const float* const* ytab, float* pred, float* dpred, float dscale);
 void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
 void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                     const ParamOff& po);

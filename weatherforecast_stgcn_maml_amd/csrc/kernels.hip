@@ -298,7 +298,7 @@ __global__ __launch_bounds__(NT) void k_head_loss(const float* __restrict__ hT_b
                                                   int64_t bo, const float* const* __restrict__ xtab,
                                                   float* __restrict__ pred, float* __restrict__ dpred,
                                                   float* __restrict__ lpart, int lblocks, int M, int H,
-                                                  int HfC, int N, int Hf, int C, int T, int cin0, int B,
+                                                  int HfC, int N, int Hf, int C, int yrow0, int yld, int B,
                                                   float dscale) {
   __shared__ float smem[CfgNT::SMEM_FLOATS];
   const int z = blockIdx.z;
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(NT) void k_head_loss(const float* __restrict__ hT_b
           const int rr = n * Hf + h;
           const int hp = rr / N, np = rr - hp * N;
           const float* xs = xtab[z * B + s];
-          const float y = xs[((int64_t)(T + 1 + hp) * N + np) * cin0 + c];
+          const float y = xs[((int64_t)(yrow0 + hp) * N + np) * yld + c];
           const float df = p - y;
           lsum = fmaf(df, df, lsum);
           if (dpred) dpred[o] = dscale * df;
@@ -349,10 +349,20 @@ void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* 
   const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
   const float* hT = top + (int64_t)(d.T - 1) * w.M * d.H;  // z stride T*M*H
   dim3 grid((w.M + CfgNT::BM - 1) / CfgNT::BM, 1, w.Z);
+  // targets from the feature stream: rows T+1 .. T+Hf after the window start, first C channels (F5)
   k_head_loss<<<grid, NT, 0, s>>>(hT, (int64_t)d.T * w.M * d.H, theta, tstride, po.wo, po.bo,
                                   want_loss ? xtab : nullptr, w.pred, want_loss ? w.dpred : nullptr,
                                   want_loss ? w.lpart : nullptr, w.lblocks, w.M, d.H, d.HfC, d.N, d.Hf,
-                                  d.C, d.T, d.Cin0, w.B, dscale);
+                                  d.C, d.T + 1, d.Cin0, w.B, dscale);
+}
+
+void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float* hT, const float* theta,
+                        const ParamOff& po, const float* const* ytab, float* pred, float* dpred, float dscale) {
+  // explicit targets: ytab[s] -> y [Hf*N][C] in the reference's layout (dataset.py:40-48)
+  dim3 grid((w.M + CfgNT::BM - 1) / CfgNT::BM, 1, 1);
+  k_head_loss<<<grid, NT, 0, s>>>(hT, 0, theta, 0, po.wo, po.bo, ytab, pred, ytab ? dpred : nullptr,
+                                  ytab ? w.lpart : nullptr, w.lblocks, w.M, d.H, d.HfC, d.N, d.Hf, d.C, 0, d.C,
+                                  w.B, dscale);
 }
 
 __global__ void k_loss_final(const float* __restrict__ lpart, int lblocks, float inv_count,

@@ -8,8 +8,15 @@ Constructor signature, attributes (``base_stgcn``, ``lstm``, ``output_layer``,
 GCN x4 (fp32 MFMA, F3 semantics), the 4-layer LSTM batched over nodes (the reference's
 per-node loop, F6, is one batched recurrence here), head. No CPU fallback.
 
-Training does not go through torch autograd: use ``weatherforecast_stgcn_maml_amd.maml``
-(meta-steps run entirely inside the library).
+With grad enabled, ``forward`` is a ``torch.autograd.Function`` (``_HybridFn``): its backward
+is ``smaml_backward`` (head, BPTT, weight gradients on the GPU), so unmodified callers --
+``loss.backward()``, ``clip_grad_norm_``, ``torch.optim.*`` as in ``inner_loop_v4``
+(train_hybrid_maml_v5.py:110-141) or ``adaptModel`` (adapt_hybrid_v5.py:168-203) -- drive
+the HIP path. Gradients reach the LSTM and head only (the reference computes the GCN under
+``no_grad``, F2). One forward/backward pair may be in flight per model shape: a second forward
+before the backward ends the first one's saved activations (the backward then raises).
+For whole meta-steps use ``weatherforecast_stgcn_maml_amd.maml`` (run entirely inside the
+library).
 """
 from __future__ import annotations
 
@@ -22,6 +29,24 @@ import torch.nn as nn
 from . import _capi, params
 from .config import ModelDims
 from .model import _context, _set_graph
+
+
+class _HybridFn(torch.autograd.Function):
+    """pred = HybridSTGCN_LSTM(x) with d pred / d (LSTM, head) from ``smaml_backward``."""
+
+    @staticmethod
+    def forward(fctx, x, lib_ctx, dims, theta, names, *tparams):
+        pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
+        lib_ctx.forward(_capi.stream_ptr(torch), theta, [x], pred)
+        fctx.lib_ctx, fctx.dims, fctx.theta, fctx.names = lib_ctx, dims, theta, names
+        return pred
+
+    @staticmethod
+    def backward(fctx, gpred):
+        grad = torch.empty_like(fctx.theta)
+        fctx.lib_ctx.backward(_capi.stream_ptr(torch), fctx.theta, gpred.contiguous().float(), grad)
+        g = params.unpack(grad, fctx.dims)
+        return (None, None, None, None, None, *[g[n] for n in fctx.names])
 
 
 class LSTMParams(nn.Module):
@@ -129,10 +154,18 @@ class HybridSTGCN_LSTM(nn.Module):
         ctx.forward(_capi.stream_ptr(torch), theta, [x], pred, feats)
         return feats
 
+    def _trainable_params(self):
+        named = [("lstm." + n, p) for n, p in self.lstm.named_parameters()]
+        named += [("output_layer.weight", self.output_layer.weight), ("output_layer.bias", self.output_layer.bias)]
+        return named
+
     def forward(self, x, edge_index):
         """hybrid_model.py:80-117 -> [N*forecast_horizon, out_channels] (rows n*Hf + h)."""
         ctx, dims, theta = self._prepare(x, edge_index)
         x = x.contiguous().float()
+        named = self._trainable_params()
+        if torch.is_grad_enabled() and any(p.requires_grad for _, p in named):
+            return _HybridFn.apply(x, ctx, dims, theta, [n for n, _ in named], *[p for _, p in named])
         pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
         ctx.forward(_capi.stream_ptr(torch), theta, [x], pred)
         return pred
