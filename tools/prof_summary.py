@@ -20,11 +20,14 @@ import sys
 # bench.py timing categories (api.cpp TIMED(...)) -> the kernels each category launches
 CATEGORIES = {
     "gcn_layer": r"k_gcn_layer",
-    "lstm_fwd_step": r"k_lstm_fwd_(step|dual)",
-    "lstm_bwd_step": r"k_lstm_bwd_(step|dual)",
-    "wgrad": r"k_wgrad",
-    "dx": r"k_gemm_nn",
-    "head": r"k_head_(loss|dual)",
+    "lstm_fwd_step": r"k_lstm_fwd_step",
+    "lstm_fwd_dual": r"k_lstm_fwd_dual",
+    "lstm_bwd_step": r"k_lstm_bwd_step",
+    "lstm_bwd_dual": r"k_lstm_bwd_dual",
+    "wgrad": r"k_wgrad$|k_wgrad\b(?!_)",
+    "wgrad_reduce": r"k_wgrad_reduce",
+    "head_dh": r"k_gemm_nn",
+    "head_loss": r"k_head_(loss|dual)",
 }
 
 

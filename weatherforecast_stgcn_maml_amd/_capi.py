@@ -26,8 +26,9 @@ EXPORTS = (
 )
 ABI_VERSION = 2
 
-TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "head_loss", "head_dh", "lstm_bwd_step",
-                     "wgrad", "dx", "misc")
+# api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
+TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",
+                     "lstm_bwd_dual", "wgrad", "wgrad_reduce", "misc")
 
 ERRORS = {1: "EINVAL", 2: "EHIP", 3: "ENOMEM", 4: "ESTATE", 5: "ENOTIMPL"}
 

@@ -123,7 +123,8 @@ int build_ell(const int64_t* ei, int64_t E, int N, std::vector<int32_t>& cols, s
   return SMAML_OK;
 }
 
-enum Cat { C_GCN = 0, C_FWD, C_HEAD, C_HEAD_DH, C_BWD, C_WGRAD, C_DX, C_MISC, NCAT };
+// one kernel per timing category (bench roofline = one kernel's launches)
+enum Cat { C_GCN = 0, C_FWD, C_FWD_DUAL, C_HEAD, C_HEAD_DH, C_BWD, C_BWD_DUAL, C_WGRAD, C_WGRAD_RED, C_MISC, NCAT };
 
 // Live per-category kernel timing with HIP events on the launch stream (bench roofline).
 struct Timer {
@@ -367,6 +368,18 @@ void set_work(smaml_ctx* c, int Z, int B) {
     }                                                            \
   } while (0)
 
+// Weight gradient = split-K GEMM (C_WGRAD) + fixed-order reduce (C_WGRAD_RED).
+void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t a_zstride, int Mrows,
+                 const float* B1, int64_t b1_zstride, int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K,
+                 int Mshift, float* grad, int64_t P, int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2,
+                 bool with_bias = true, bool accumulate = false) {
+  WgradPlan p;
+  plan_wgrad(c->w, A, a_zstride, Mrows, B1, b1_zstride, c1, B2, b2_zstride, c2, K, Mshift, grad, P, off_w1, off_w2,
+             off_b1, off_b2, with_bias, accumulate, p);
+  TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
+  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+}
+
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc].
 int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
   const Dims& d = c->d;
@@ -417,9 +430,8 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
   TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
   const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
-  TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
-        launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, top + (int64_t)(d.T - 1) * w.M * d.H,
-                     TM * d.H, d.H, nullptr, 0, 0, w.M, 0, grad, po.P, po.wo, -1, po.bo, -1));
+  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, top + (int64_t)(d.T - 1) * w.M * d.H,
+                     TM * d.H, d.H, nullptr, 0, 0, w.M, 0, grad, po.P, po.wo, -1, po.bo, -1);
   return run_bptt(c, s, theta, tstride, grad);
 }
 
@@ -439,10 +451,9 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
-    TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H),
-          launch_wgrad(s, d, w, w.Gs + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.Gs + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
                        w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
-                       lo.bhh));
+                       lo.bhh);
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -469,7 +480,7 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     const double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
-    TIMED(c, s, C_FWD, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
+    TIMED(c, s, C_FWD_DUAL, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -484,16 +495,14 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
   TIMED(c, s, C_HEAD_DH, 3.0 * 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh_dual(s, d, w, theta, U, tstride, po));
   const int64_t toff = (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
-  TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
-        launch_wgrad(s, d, w, w.Rdpred, (int64_t)w.M * d.HfC, d.HfC, w.Hs + toff, TM * d.H, d.H, nullptr, 0, 0,
-                     w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false));
-  TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
-        launch_wgrad(s, d, w, w.dpred, (int64_t)w.M * d.HfC, d.HfC, w.RHs + toff, TM * d.H, d.H, nullptr, 0, 0,
-                     w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true));
+  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.Rdpred, (int64_t)w.M * d.HfC, d.HfC, w.Hs + toff, TM * d.H, d.H, nullptr, 0, 0,
+                     w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false);
+  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, w.RHs + toff, TM * d.H, d.H, nullptr, 0, 0,
+                     w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true);
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
     const double fl = bwd_wave(d, w, po, e, 0, true, wv);
-    TIMED(c, s, C_BWD, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
+    TIMED(c, s, C_BWD_DUAL, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
     const int l = d.L - 1 - (e - (d.T - 1));
     if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
@@ -501,13 +510,11 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
     const float* dGl = w.Gs + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
-    TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H),
-          launch_wgrad(s, d, w, RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
-                       TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false));
-    TIMED(c, s, C_WGRAD, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H),
-          launch_wgrad(s, d, w, dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
+                       TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false);
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
                        w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh,
-                       false, true));
+                       false, true);
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;

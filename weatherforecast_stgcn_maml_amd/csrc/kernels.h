@@ -107,6 +107,30 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
                   int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                   int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias = true,
                   bool accumulate = false);
+// launch_wgrad split in its two launches (the GEMM into split-K partial slabs, then the
+// fixed-order reduce into the flat gradient), so each can be timed on its own.
+struct WgradPlan {
+  const float* A;
+  int64_t a_zstride;
+  int Mrows;
+  const float *B1, *B2;
+  int c1, c2;
+  int64_t K, Mshift;
+  int64_t b1_zstride, b2_zstride;
+  float* grad;
+  int64_t P, off_w1, off_w2, off_b1, off_b2;
+  bool with_bias, accumulate;
+  int Z;
+  float* part;
+  int ldp, ntm, ntn, nsplit;
+  int64_t kchunk;
+};
+void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
+                int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
+                int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,
+                WgradPlan& p);
+void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
+void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
 void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part);
 void launch_clip_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, const double* part,
                      float lr, float max_norm, float* norm_out, float* coef_out);

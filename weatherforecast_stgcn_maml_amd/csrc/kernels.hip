@@ -628,12 +628,10 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int M
   *dst = accumulate ? *dst + v : v;
 }
 
-void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
-                  int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
-                  int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
-                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias,
-                  bool accumulate) {
-  (void)d;
+void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
+                int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
+                int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,
+                WgradPlan& p) {
   const int ncols = c1 + c2;
   const int ldp = ncols + 1;
   const int ntm = (Mrows + CfgTN::BM - 1) / CfgTN::BM;
@@ -648,22 +646,67 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
   if (nsplit < 1) nsplit = 1;
   const int64_t kchunk = ((ktiles + nsplit - 1) / nsplit) * CfgTN::BK;
   nsplit = (K + kchunk - 1) / kchunk;
+  p.A = A;
+  p.a_zstride = a_zstride;
+  p.Mrows = Mrows;
+  p.B1 = B1;
+  p.B2 = B2;
+  p.c1 = c1;
+  p.c2 = c2;
+  p.K = K;
+  p.Mshift = Mshift;
+  p.b1_zstride = b1_zstride;
+  p.b2_zstride = b2_zstride;
+  p.grad = grad;
+  p.P = P;
+  p.off_w1 = off_w1;
+  p.off_w2 = off_w2;
+  p.off_b1 = off_b1;
+  p.off_b2 = off_b2;
+  p.with_bias = with_bias;
+  p.accumulate = accumulate;
+  p.Z = w.Z;
+  p.part = w.wpart;
+  p.ldp = ldp;
+  p.ntm = ntm;
+  p.ntn = ntn;
+  p.nsplit = (int)nsplit;
+  p.kchunk = kchunk;
+}
+
+void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
   WgB lb;
-  lb.B1 = B1;
-  lb.B2 = B2;
-  lb.c1 = c1;
-  lb.c2 = c2;
-  lb.K = K;
-  lb.Mshift = Mshift;
-  const int ntile = ntm * ntn;
-  const int ngroups = (int)nsplit * w.Z;
+  lb.B1 = p.B1;
+  lb.B2 = p.B2;
+  lb.c1 = p.c1;
+  lb.c2 = p.c2;
+  lb.K = p.K;
+  lb.Mshift = p.Mshift;
+  const int ntile = p.ntm * p.ntn;
+  const int ngroups = p.nsplit * p.Z;
   dim3 grid((unsigned)(((ngroups + 7) / 8) * 8 * ntile));
-  k_wgrad<<<grid, NT, 0, s>>>(A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, (int)nsplit,
-                              ngroups, w.wpart, ldp, with_bias ? 1 : 0);
-  const int64_t total = (int64_t)Mrows * ldp;
-  dim3 g2((unsigned)((total + 255) / 256), w.Z);
-  k_wgrad_reduce<<<g2, 256, 0, s>>>(w.wpart, (int)nsplit, Mrows, ldp, c1, c2, grad, P, off_w1, off_w2, off_b1,
-                                    off_b2, accumulate ? 1 : 0);
+  k_wgrad<<<grid, NT, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn, ntile,
+                              p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0);
+}
+
+void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p) {
+  const int64_t total = (int64_t)p.Mrows * p.ldp;
+  dim3 g2((unsigned)((total + 255) / 256), p.Z);
+  k_wgrad_reduce<<<g2, 256, 0, s>>>(p.part, p.nsplit, p.Mrows, p.ldp, p.c1, p.c2, p.grad, p.P, p.off_w1,
+                                    p.off_w2, p.off_b1, p.off_b2, p.accumulate ? 1 : 0);
+}
+
+void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
+                  int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
+                  int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
+                  int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias,
+                  bool accumulate) {
+  (void)d;
+  WgradPlan p;
+  plan_wgrad(w, A, a_zstride, Mrows, B1, b1_zstride, c1, B2, b2_zstride, c2, K, Mshift, grad, P, off_w1, off_w2,
+             off_b1, off_b2, with_bias, accumulate, p);
+  launch_wgrad_gemm(s, p);
+  launch_wgrad_reduce(s, p);
 }
 
 // ====================================================================================
