@@ -107,8 +107,7 @@ def main(d, title, traffic_out=None, profile_md=None):
             continue
         rd = 2 * sum(fr) / len(fr) * 1024
         wt = (sum(wr) / len(wr) * 1024) if wr else 0.0
-        # wgrad's timed launch is two dispatches (split-K GEMM + fixed-order reduce)
-        per = 2.0 if cat == "wgrad" else 1.0
+        per = 1.0  # one kernel per timing category
         traffic[cat] = {"read_bytes": rd * per, "write_bytes": wt * per, "bytes_per_launch": (rd + wt) * per}
         print(f"| {cat} | {len(fr)} | {rd * per / 1e6:.1f} | {wt * per / 1e6:.1f} | {(rd + wt) * per / 1e6:.1f} |")
     if traffic_out:

@@ -20,7 +20,7 @@
 namespace smaml {
 
 using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-contiguous)
-using CfgGate = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;  // LSTM forward: wave = 32 rows x 4 gates
+using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;  // LSTM forward: wave = 32 rows x 4 gates
 using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK>;  // C = A . B   (B n-contiguous)
 using CfgTN = GemmCfg<128, 128, 2, 2, false, false, SMAML_TN_BK>;  // C = A^T . B (split-K weight grads)
 
@@ -427,6 +427,8 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
 // and its GEMM reads other (l, t) slabs finished on the previous diagonal.
 // 64x64 tiles for small grids (few tasks per rank) so the launch fills the chip.
 using CfgNNs = GemmCfg<64, 64, 2, 2, true, false, SMAML_NN_BK>;
+// BPTT step tile (A/B-able at build time): rows x 128 units, waves WM x WN
+using CfgBwd = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_NN_BK>;
 
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv) {
@@ -451,7 +453,7 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 }
 
 template <int H, class CfgNN>
-__global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ GsAll, const float* __restrict__ CsAll,
+__global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(float* __restrict__ GsAll, const float* __restrict__ CsAll,
                                                       const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
                                                       BwdWave wv, int L, int T, int M) {
@@ -484,11 +486,13 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ GsAll,
   const bool head = first && l == L - 1;
   const float* dHz = dHhead + (int64_t)z * M * H;
   const bool full = m0 + CfgNN::BM <= M;
-  const int rb = m0 + acc_row<CfgNN>(0, 0);
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
+#pragma unroll
+  for (int i = 0; i < CfgNN::WTM; ++i)
 #pragma unroll
   for (int jj = 0; jj < CfgNN::WTN; ++jj) {
     const int j = n0 + acc_col<CfgNN>(jj);
+    const int rb = m0 + acc_row<CfgNN>(i, 0);
     if (j >= H) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(NT) void k_lstm_bwd_step(float* __restrict__ GsAll,
       const uint32_t oh = row * H + j;
       const uint32_t og = row * G4 + j;
       const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = acc.v[0][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
+      const float dh = acc.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
       const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
       const float c = ldb(Cz, 4u * (oh));
       const float tc = tanhf_(c);
@@ -518,12 +522,12 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
                           const ParamOff& po) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   BwdWave wv{};
-  const int ntm = (w.M + CfgNN::BM - 1) / CfgNN::BM, ntn = (d.H + CfgNN::BN - 1) / CfgNN::BN;
+  const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
   if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
     dim3 grid(wv.off[wv.n], ntn, w.Z);
-    SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNN><<<grid, CfgNN::NTH, 0, s>>>(
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgBwd><<<grid, CfgBwd::NTH, 0, s>>>(
                               w.Gs, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
   } else {
     const int ntms = (w.M + CfgNNs::BM - 1) / CfgNNs::BM, ntns = (d.H + CfgNNs::BN - 1) / CfgNNs::BN;

@@ -20,7 +20,7 @@ namespace smaml {
 #endif
 // The BPTT / dX / head duals stage four operand tiles per K-tile (gemm_dual_mainloop);
 // BK=16 keeps them at 54-80 KiB of LDS (two or more workgroups per CU).
-using CfgGateD = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;
+using CfgGateD = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;
 using CfgNTD = GemmCfg<128, 128, 2, 2, true, true, SMAML_DUAL_BK>;
 using CfgNND = GemmCfg<64, 128, 2, 2, true, false, SMAML_DUAL_BK>;
 
@@ -267,13 +267,14 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
 
 // ====================================================================================
 using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
+using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_DUAL_BK>;
 
 // Tangent BPTT step, one anti-diagonal per launch (kernels.hip k_lstm_bwd_step; BwdWave):
 //   dh  = A . B,   R(dh) = A2 . B + A . B2   with  A = [dG(l+1,t) | dG(l,t+1)],
 //   A2 = [R dG(l+1,t) | R dG(l,t+1)],  B = [W_ih(l+1) ; W_hh(l)],  B2 = [U_ih(l+1) ; U_hh(l)]
 // then the cell backward and its product-rule tangent; dG / R(dG) overwrite G / R(G) in place.
 template <int H, class CfgNND>
-__global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __restrict__ GsAll, float* __restrict__ RGsAll,
+__global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(float* __restrict__ GsAll, float* __restrict__ RGsAll,
                                                       const float* __restrict__ CsAll, const float* __restrict__ RCsAll,
                                                       const float* __restrict__ dHhead, const float* __restrict__ RdHhead,
                                                       float* __restrict__ dcAll, float* __restrict__ RdcAll,
@@ -317,11 +318,13 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __r
   const float* dHz = dHhead + (int64_t)z * M * H;
   const float* RdHz = RdHhead + (int64_t)z * M * H;
   const bool full = m0 + CfgNND::BM <= M;
-  const int rb = m0 + acc_row<CfgNND>(0, 0);
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
+#pragma unroll
+  for (int i = 0; i < CfgNND::WTM; ++i)
 #pragma unroll
   for (int jj = 0; jj < CfgNND::WTN; ++jj) {
     const int j = n0 + acc_col<CfgNND>(jj);
+    const int rb = m0 + acc_row<CfgNND>(i, 0);
     if (j >= H) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -331,8 +334,8 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(NT) void k_lstm_bwd_dual(float* __r
       const uint32_t oh = row * H + j;
       const uint32_t og = row * G4 + j;
       const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = ap.v[0][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
-      const float rdh = at.v[0][jj][r] + (head ? ldb(RdHz, 4u * oc) : 0.f);
+      const float dh = ap.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
+      const float rdh = at.v[i][jj][r] + (head ? ldb(RdHz, 4u * oc) : 0.f);
       const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
       const float ri = ldb(RGz, 4u * (og)), rf = ldb(RGz, 4u * (og + H)), rgg = ldb(RGz, 4u * (og + 2 * H)), ro = ldb(RGz, 4u * (og + 3 * H));
       const float c = ldb(Cz, 4u * (oh)), rc = ldb(RCz, 4u * (oh));
@@ -364,12 +367,12 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
                                const float* U, int64_t tstride, const ParamOff& po) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   BwdWave wv{};
-  const int ntm = (w.M + CfgNND::BM - 1) / CfgNND::BM, ntn = (d.H + CfgNND::BN - 1) / CfgNND::BN;
+  const int ntm = (w.M + CfgBwdD::BM - 1) / CfgBwdD::BM, ntn = (d.H + CfgBwdD::BN - 1) / CfgBwdD::BN;
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
   if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
     dim3 grid(wv.off[wv.n], ntn, w.Z);
-    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgNND><<<grid, CfgNND::NTH, 0, s>>>(
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgBwdD><<<grid, CfgBwdD::NTH, 0, s>>>(
                               w.Gs, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv, d.L,
                               d.T, w.M));
   } else {

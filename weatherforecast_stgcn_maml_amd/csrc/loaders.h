@@ -13,8 +13,20 @@
 #ifndef SMAML_GATE_WN
 #define SMAML_GATE_WN 1  // gate GEMM column waves: 1 -> 128x128 (4 waves), 2 -> 128x256 (8 waves)
 #endif
+#ifndef SMAML_GATE_WM
+#define SMAML_GATE_WM 4  // gate GEMM row waves (32 rows each): 4 -> 128-row tiles, 8 -> 256-row tiles
+#endif
 #ifndef SMAML_NN_BK
 #define SMAML_NN_BK 16
+#endif
+#ifndef SMAML_BWD_BM
+#define SMAML_BWD_BM 64  // BPTT step tile rows (x 128 units)
+#endif
+#ifndef SMAML_BWD_WM
+#define SMAML_BWD_WM 2
+#endif
+#ifndef SMAML_BWD_WN
+#define SMAML_BWD_WN 2
 #endif
 #ifndef SMAML_GCN_BK
 #define SMAML_GCN_BK 16
