@@ -453,7 +453,7 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 }
 
 template <int H, class CfgNN>
-__global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(float* __restrict__ GsAll, const float* __restrict__ CsAll,
+__global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(float* __restrict__ GsAll, const float* __restrict__ CsAll,
                                                       const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
                                                       BwdWave wv, int L, int T, int M) {

@@ -15,12 +15,15 @@
 
 namespace smaml {
 
+#ifndef SMAML_DUAL_RELOAD
+#define SMAML_DUAL_RELOAD 1  // 1: tangent gate kernel keeps one accumulator set live (re-reads gates)
+#endif
 #ifndef SMAML_DUAL_BK
 #define SMAML_DUAL_BK 16
 #endif
 // The BPTT / dX / head duals stage four operand tiles per K-tile (gemm_dual_mainloop);
 // BK=16 keeps them at 54-80 KiB of LDS (two or more workgroups per CU).
-using CfgGateD = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;
+using CfgGateD = GemmCfg<32 * SMAML_GATED_WM, 128 * SMAML_GATE_WN, SMAML_GATED_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;
 using CfgNTD = GemmCfg<128, 128, 2, 2, true, true, SMAML_DUAL_BK>;
 using CfgNND = GemmCfg<64, 128, 2, 2, true, false, SMAML_DUAL_BK>;
 
@@ -82,6 +85,86 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
 
+#if SMAML_DUAL_RELOAD
+  // Register diet: the primal epilogue runs between the two passes (its accumulators die
+  // there), and the tangent epilogue re-reads the gates / cell it needs from the lines this
+  // lane has just written (program order: a lane sees its own stores). One accumulator set
+  // is live at a time.
+  const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
+  const int rb = m0 + acc_row<CfgGateD>(0, 0);
+  const bool full = m0 + CfgGateD::BM <= M;
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
+  {
+    Acc<CfgGateD> ap;
+    ap.zero();
+    SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
+    SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
+    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh, ap, smem);
+    if (j < H) {
+      float bp[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bp[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = rb + racc(r);
+        if (!full && m >= M) continue;
+        const uint32_t row = tM + (uint32_t)m;
+        const uint32_t oh = row * H + j;
+        const uint32_t og = row * G4 + j;
+        const float gi = sigmoidf_(ap.v[0][0][r] + bp[0]);
+        const float gf = sigmoidf_(ap.v[0][1][r] + bp[1]);
+        const float gg = tanhf_(ap.v[0][2][r] + bp[2]);
+        const float go = sigmoidf_(ap.v[0][3][r] + bp[3]);
+        const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+        const float c = gf * cp + gi * gg;
+        stb(Gz, 4u * (og), gi);
+        stb(Gz, 4u * (og + H), gf);
+        stb(Gz, 4u * (og + 2 * H), gg);
+        stb(Gz, 4u * (og + 3 * H), go);
+        stb(Cz, 4u * (oh), c);
+        stb(Hz, 4u * (oh), go * tanhf_(c));
+      }
+    }
+  }
+  Acc<CfgGateD> at;
+  at.zero();
+  {
+    const int wrx = rxt ? cin : 0;
+    SegKC la{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M};
+    SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
+    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+  }
+  if (j >= H) return;
+  float bu[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bu[g] = u[lo.bih + g * H + j] + u[lo.bhh + g * H + j];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = rb + racc(r);
+    if (!full && m >= M) continue;
+    const uint32_t row = tM + (uint32_t)m;
+    const uint32_t oh = row * H + j;
+    const uint32_t og = row * G4 + j;
+    const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H));
+    const float gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
+    const float c = ldb(Cz, 4u * (oh));
+    const float ri = gi * (1.f - gi) * (at.v[0][0][r] + bu[0]);
+    const float rf = gf * (1.f - gf) * (at.v[0][1][r] + bu[1]);
+    const float rg = (1.f - gg * gg) * (at.v[0][2][r] + bu[2]);
+    const float ro = go * (1.f - go) * (at.v[0][3][r] + bu[3]);
+    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+    const float rcp = t > 0 ? ldb(RCz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+    const float rc = rf * cp + gf * rcp + ri * gg + gi * rg;
+    const float tc = tanhf_(c);
+    stb(RGz, 4u * (og), ri);
+    stb(RGz, 4u * (og + H), rf);
+    stb(RGz, 4u * (og + 2 * H), rg);
+    stb(RGz, 4u * (og + 3 * H), ro);
+    stb(RCz, 4u * (oh), rc);
+    stb(RHz, 4u * (oh), ro * tc + go * (1.f - tc * tc) * rc);
+  }
+}
+#else
   Acc<CfgGateD> ap, at;
   ap.zero();
   at.zero();
@@ -143,6 +226,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     stb(RHz, 4u * (oh), ro * tc + go * (1.f - tc * tc) * rc);
   }
 }
+#endif
 
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                                const float* U, int64_t tstride, const ParamOff& po, double* flops) {

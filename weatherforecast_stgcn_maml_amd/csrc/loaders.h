@@ -16,6 +16,9 @@
 #ifndef SMAML_GATE_WM
 #define SMAML_GATE_WM 4  // gate GEMM row waves (32 rows each): 4 -> 128-row tiles, 8 -> 256-row tiles
 #endif
+#ifndef SMAML_GATED_WM
+#define SMAML_GATED_WM 4  // same, for the tangent (dual) gate kernel
+#endif
 #ifndef SMAML_NN_BK
 #define SMAML_NN_BK 16
 #endif
@@ -41,10 +44,18 @@
 #define SMAML_GATE_WPE 4
 #endif
 #ifndef SMAML_GATED_WPE
-#define SMAML_GATED_WPE 0  // same, for the tangent (dual) gate kernel
+#define SMAML_GATED_WPE 4  // same, for the tangent (dual) gate kernel (127 VGPRs with SMAML_DUAL_RELOAD)
 #endif
 #ifndef SMAML_BWDD_WPE
 #define SMAML_BWDD_WPE 3  // same, for the tangent BPTT kernel (LDS caps it at 3 anyway)
+#endif
+#ifndef SMAML_BWD_WPE
+#define SMAML_BWD_WPE 6  // same, for the primal BPTT kernel (77 VGPRs, LDS allows 6)
+#endif
+#if SMAML_BWD_WPE > 0
+#define SMAML_BWD_ATTR __attribute__((amdgpu_waves_per_eu(SMAML_BWD_WPE)))
+#else
+#define SMAML_BWD_ATTR
 #endif
 #if SMAML_BWDD_WPE > 0
 #define SMAML_BWDD_ATTR __attribute__((amdgpu_waves_per_eu(SMAML_BWDD_WPE)))
