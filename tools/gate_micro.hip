@@ -55,6 +55,34 @@ __global__ __launch_bounds__(C::NTH) void k_gate(const float* __restrict__ A, co
   }
   const int wave = threadIdx.x >> 6;
   const int j = (ug * UPB + wave % UPB) * 32 + (threadIdx.x & 31);
+  if (EPI == 4) {  // loads of every row first (no store between them), then math + stores
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) {
+      const int rb = m0 + acc_row<C>(i, 0);
+      float cpv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = rb + racc(r);
+        cpv[r] = m < M ? ldb(CH, 4u * ((uint32_t)m * H + j)) : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = rb + racc(r);
+        if (m >= M) continue;
+        const uint32_t oh = (uint32_t)m * H + j, og = (uint32_t)m * 4 * H + j;
+        const float gi = sigmoidf_(acc.v[i][0][r]), gf = sigmoidf_(acc.v[i][1][r]);
+        const float gg = tanhf_(acc.v[i][2][r]), go = sigmoidf_(acc.v[i][3][r]);
+        const float c = gf * cpv[r] + gi * gg;
+        stb(G, 4u * og, gi);
+        stb(G, 4u * (og + H), gf);
+        stb(G, 4u * (og + 2 * H), gg);
+        stb(G, 4u * (og + 3 * H), go);
+        stb(CH, 4u * oh + 4u * M * H, c);
+        stb(CH, 4u * oh + 8u * M * H, go * tanhf_(c));
+      }
+    }
+    return;
+  }
   float keep = 0.f;
 #pragma unroll
   for (int i = 0; i < C::WTM; ++i) {
@@ -88,24 +116,108 @@ __global__ __launch_bounds__(C::NTH) void k_gate(const float* __restrict__ A, co
   if (EPI == 1) asm volatile("" ::"v"(keep));
 }
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gptr_t;
+
+// L2 prefetch of a wave's BPTT-epilogue operands by LDS-DMA into a scratch slot during the
+// last PF K-tiles of the mainloop (the data is dropped; the epilogue's own loads then hit L2).
+// Footprint per wave: 32 rows x 64 units x 7 arrays (4 gates, c_t, c_{t-1}, dc) = 224 segments
+// of 256 B = 56 wave-instructions of 1 KiB.
+template <class C>
+struct PrefetchHook {
+  const float *G, *Cs, *dc;
+  float* scratch;
+  int m0, n0, M, nkt, PF;
+  __device__ __forceinline__ void operator()(const float*, int kt) const {
+    const int first = nkt - PF;
+    if (kt < first) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+    const int per = (56 + PF - 1) / PF;
+    const int i0 = (kt - first) * per;
+    const int i1 = i0 + per < 56 ? i0 + per : 56;
+    for (int i = i0; i < i1; ++i) {
+      const int seg = 4 * i + (lane >> 4);
+      const int row = seg / 7, arr = seg - row * 7;
+      int m = m0 + wm * 32 + row;
+      m = m < M ? m : M - 1;
+      const int u = n0 + wn * 64 + (lane & 15) * 4;
+      const float* p;
+      if (arr < 4) p = G + (size_t)m * 4 * H + arr * H + u;
+      else if (arr == 4) p = Cs + (size_t)M * H + (size_t)m * H + u;
+      else if (arr == 5) p = Cs + (size_t)m * H + u;
+      else p = dc + (size_t)m * H + u;
+      __builtin_amdgcn_global_load_lds((gptr_t)p, (lds_ptr_t)(scratch + wave * 256), 16, 0, 0);
+    }
+  }
+};
+
 // BPTT step shape: dh = dGcat [M][K] . W [K][H] (W row-major [K][H]: "MC"), or W^T stored
 // [H][K] ("KC"), then the cell backward. EPI: 0 = plain store of dh; 1 = cell backward with
 // G [row][g*H + j]; 2 = cell backward with G interleaved [row][4j + g].
-template <class C, bool BKC, int EPI>
+template <class C, bool BKC, int EPI, int PF = 0>
 __global__ __launch_bounds__(C::NTH) void k_bptt(const float* __restrict__ A, const float* __restrict__ W,
                                                  float* __restrict__ G, const float* __restrict__ Cs,
                                                  float* __restrict__ dc, float* __restrict__ O, int M, int K) {
-  __shared__ float smem[C::SMEM_FLOATS];
+  __shared__ float smem[C::SMEM_FLOATS + (PF ? C::NTH / 64 * 256 : 0)];
   const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
   Acc<C> acc;
   acc.zero();
   RowMajorKC la{A, M, K};
-  if (BKC) {
+  if (PF) {
+    RowMajorMC lb{W, K, H};
+    PrefetchHook<C> hk{G, Cs, dc, smem + C::SMEM_FLOATS, m0, n0, M, (K + C::BK - 1) / C::BK, PF};
+    gemm_mainloop<C>(la, lb, m0, n0, 0, K, acc, smem, hk);
+  } else if (BKC) {
     RowMajorKC lb{W, H, K};
     gemm_mainloop<C>(la, lb, m0, n0, 0, K, acc, smem);
   } else {
     RowMajorMC lb{W, K, H};
     gemm_mainloop<C>(la, lb, m0, n0, 0, K, acc, smem);
+  }
+  if (EPI >= 3) {
+    constexpr int BATCH = EPI == 3 ? 4 : EPI == 4 ? 8 : 16;
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < C::WTN; ++jj) {
+        const int j = n0 + acc_col<C>(jj);
+        const int rb = m0 + acc_row<C>(i, 0);
+#pragma unroll
+        for (int b0 = 0; b0 < 16; b0 += BATCH) {
+          float v[BATCH][7];
+#pragma unroll
+          for (int q = 0; q < BATCH; ++q) {
+            int m = rb + racc(b0 + q);
+            m = m < M ? m : M - 1;
+            const uint32_t oh = (uint32_t)m * H + j, og = (uint32_t)m * 4 * H + j;
+            v[q][0] = ldb(G, 4u * og);
+            v[q][1] = ldb(G, 4u * (og + H));
+            v[q][2] = ldb(G, 4u * (og + 2 * H));
+            v[q][3] = ldb(G, 4u * (og + 3 * H));
+            v[q][4] = ldb(Cs, 4u * oh + 4u * M * H);
+            v[q][5] = ldb(Cs, 4u * oh);
+            v[q][6] = ldb(dc, 4u * oh);
+          }
+#pragma unroll
+          for (int q = 0; q < BATCH; ++q) {
+            const int m = rb + racc(b0 + q);
+            if (m >= M) continue;
+            const uint32_t oh = (uint32_t)m * H + j, og = (uint32_t)m * 4 * H + j;
+            const float dh = acc.v[i][jj][b0 + q];
+            const float gi = v[q][0], gf = v[q][1], gg = v[q][2], go = v[q][3];
+            const float c = v[q][4], cp = v[q][5], dcin = v[q][6];
+            const float tc = tanhf_(c);
+            const float dct = dcin + dh * go * (1.f - tc * tc);
+            stb(G, 4u * og, dct * gg * gi * (1.f - gi));
+            stb(G, 4u * (og + H), dct * cp * gf * (1.f - gf));
+            stb(G, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
+            stb(G, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
+            stb(dc, 4u * oh, dct * gf);
+          }
+        }
+      }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < C::WTM; ++i)
@@ -186,7 +298,7 @@ float run_gate(const Bufs& b, int K) {
   return ms / reps;
 }
 
-template <class C, bool BKC, int EPI>
+template <class C, bool BKC, int EPI, int PF = 0>
 float run_bptt(const Bufs& b, int K) {
   dim3 grid((b.M + C::BM - 1) / C::BM, (H + C::BN - 1) / C::BN);
   hipEvent_t e0, e1;
@@ -194,7 +306,7 @@ float run_bptt(const Bufs& b, int K) {
   (void)hipEventCreate(&e1);
   const int reps = 5;
   (void)hipEventRecord(e0);
-  for (int i = 0; i < reps; ++i) k_bptt<C, BKC, EPI><<<grid, C::NTH>>>(b.A, b.W, b.G, b.CH, b.dc, b.O, b.M, K);
+  for (int i = 0; i < reps; ++i) k_bptt<C, BKC, EPI, PF><<<grid, C::NTH>>>(b.A, b.W, b.G, b.CH, b.dc, b.O, b.M, K);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
   float ms = 0;
@@ -257,13 +369,10 @@ int main() {
   using G256w4 = GemmCfg<256, 128, 4, 1, true, true, 16>;   // 4 waves, wave 64 x 128
   std::vector<Variant> gv = {
       {"128x128 w4 BK16 (current)", run_gate<G128, 0>, 512},
-      {"128x128 w4 BK16 interleaved-G", run_gate<G128, 3>, 512},
+      {"128x128 w4 BK16 loads-first", run_gate<G128, 4>, 512},
       {"128x128 w4 BK16 no-store", run_gate<G128, 1>, 512},
       {"128x128 w4 BK16 no-epilogue", run_gate<G128, 2>, 512},
-      {"128x128 w4 BK32", run_gate<G128b32, 0>, 512},
       {"256x128 w8 BK16", run_gate<G256w8, 0>, 512},
-      {"256x128 w8 BK16 interleaved-G", run_gate<G256w8, 3>, 512},
-      {"256x128 w4(64x128) BK16", run_gate<G256w4, 0>, 512},
   };
   for (int K : {256, 384}) bench("gate", b, gv, K);
 
@@ -273,12 +382,10 @@ int main() {
   using N128w4 = GemmCfg<128, 128, 4, 1, true, false, 16>;
   std::vector<Variant> bv = {
       {"64x128 NN BK16 cell (current)", run_bptt<N64, false, 1>, 128},
-      {"64x128 NN BK16 cell interleaved-G", run_bptt<N64, false, 2>, 128},
+      {"64x128 NN BK16 cell batch-4", run_bptt<N64, false, 3>, 128},
+      {"64x128 NN BK16 cell batch-8", run_bptt<N64, false, 4>, 128},
+      {"64x128 NN BK16 cell batch-16", run_bptt<N64, false, 5>, 128},
       {"64x128 NN BK16 plain store", run_bptt<N64, false, 0>, 128},
-      {"64x128 NT BK16 cell", run_bptt<T64, true, 1>, 128},
-      {"128x128 NN w2x2 BK16 cell", run_bptt<N128, false, 1>, 128},
-      {"128x128 NN w2x2 BK16 cell interleaved", run_bptt<N128, false, 2>, 128},
-      {"128x128 NN w4x1 BK16 cell", run_bptt<N128w4, false, 1>, 128},
   };
   for (int K : {512, 1024}) bench("bptt", b, bv, K);
   return 0;

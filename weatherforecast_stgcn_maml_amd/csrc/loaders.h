@@ -50,7 +50,7 @@
 #define SMAML_BWDD_WPE 3  // same, for the tangent BPTT kernel (LDS caps it at 3 anyway)
 #endif
 #ifndef SMAML_BWD_WPE
-#define SMAML_BWD_WPE 6  // same, for the primal BPTT kernel (77 VGPRs, LDS allows 6)
+#define SMAML_BWD_WPE 5  // same, for the primal BPTT kernel (<= 96 VGPRs)
 #endif
 #if SMAML_BWD_WPE > 0
 #define SMAML_BWD_ATTR __attribute__((amdgpu_waves_per_eu(SMAML_BWD_WPE)))
