@@ -191,6 +191,7 @@ def main():
             "tasks": args.tasks, "batch": cfg.batch, "inner_steps": cfg.inner_steps,
             "maml_order": cfg.order, "parallelism": f"task-sharded x{world} + RCCL all-reduce",
             "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
+            "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
         },
         "meta_step_tflop": flops_meta / 1e12,
         "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,

@@ -84,6 +84,11 @@ int smaml_reserve(smaml_ctx* ctx, int32_t tasks, int32_t batch);
 /* Bytes of device workspace currently held. */
 int64_t smaml_workspace_bytes(const smaml_ctx* ctx);
 
+/* Inner steps whose primal activations the last second-order smaml_meta_step kept for its
+ * meta-backward sweep (tangent-only dual kernels there; the rest are recomputed). Sized to
+ * free HBM, capped by the SMAML_KEEP environment variable. New; no reference counterpart. */
+int32_t smaml_so_kept_steps(const smaml_ctx* ctx);
+
 /* ---- forward (module API) ----------------------------------------------------------- */
 
 /* GCNConv.forward(x, edge_index) (PyG semantics, F3): x [rows, cin] -> out [rows, cout].

@@ -281,10 +281,24 @@ def test_full_size_meta_step_properties():
 
 
 # ----------------------------------------------------------------------------- second order
+# SMAML_KEEP caps how many inner steps keep their primal activations for the second-order
+# sweep (tangent-only dual kernels there); unset = as many as fit (all of them at these sizes).
+KEEP_MODES = [None, "0", "1"]
+
+
+def set_keep(monkeypatch, keep):
+    if keep is None:
+        monkeypatch.delenv("SMAML_KEEP", raising=False)
+    else:
+        monkeypatch.setenv("SMAML_KEEP", keep)
+
+
+@pytest.mark.parametrize("keep", KEEP_MODES)
 @pytest.mark.parametrize("clip", [0, 1])
-def test_second_order_meta_grad_cfg1(golden_dir, clip):
+def test_second_order_meta_grad_cfg1(golden_dir, clip, keep, monkeypatch):
     """Second-order meta-gradient (through both inner SGD steps, the Hessian of each support
     loss and the clip_grad_norm_ coefficient) vs torch.func through the reference module."""
+    set_keep(monkeypatch, keep)
     d = CONFIG1
     z = load(golden_dir, "cfg1_maml.npz")
     steps, batch, support, qb = (int(z[k]) for k in ("steps", "batch", "support", "qbatch"))
@@ -309,9 +323,12 @@ def test_second_order_meta_grad_cfg1(golden_dir, clip):
         assert rel(mg[k].cpu().numpy(), total[k]) < 1e-4, k
 
 
+@pytest.mark.parametrize("keep", KEEP_MODES)
 @pytest.mark.parametrize("max_norm", [1.0, 0.02])
-def test_second_order_matches_oracle_cfg2(max_norm):
-    """Config-2 shapes (N=441, Hc=256, LSTM 4x128), K=2 inner steps, B=1, 2 tasks."""
+def test_second_order_matches_oracle_cfg2(max_norm, keep, monkeypatch):
+    """Config-2 shapes (N=441, Hc=256, LSTM 4x128), K=2 inner steps, B=1, 2 tasks; the sweep
+    recomputes every step's primal (keep 0), keeps the last step's (keep 1) or keeps all."""
+    set_keep(monkeypatch, keep)
     d = CONFIG2
     cfg = MamlConfig(inner_steps=2, batch=1, order=2, max_norm=max_norm)
     P = synth.init_params(8, d, gcn_bias_scale=0.1)

@@ -10,6 +10,7 @@
 #include <array>
 #include <cmath>
 #include <dlfcn.h>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -188,6 +189,15 @@ struct smaml_ctx {
   float* so_F = nullptr;  // [K][Z][T][M][Hc] GCN features of every inner step (null: recompute)
   int64_t so_F_cap = 0;
   float* F_main = nullptr;  // the workspace's own F buffer
+  float *Hs_main = nullptr, *Cs_main = nullptr, *Gs_main = nullptr;  // the workspace's own activations
+  // primal of the last inner steps kept for the second-order sweep (ensure_keep): slot 0 adds
+  // dG + dh to the workspace's Hs/Cs/Gs, slot i >= 1 holds Hs/Cs/Gs/dG/dh of its own
+  std::vector<float*> keep_mem;
+  int keep_n = 0;
+  int64_t keep_rows = 0;  // rows * L the slots were sized for
+  int keep_tried_K = -1;
+  int keep_last = 0;  // slots the last second-order meta-step used
+  int64_t keep_tried_rows = -1;
   // activations of the last smaml_forward / smaml_lstm_forward (single task, act_B samples);
   // -1 once anything else has used the workspace (the backward consumes them: dG in place)
   int act_B = -1;
@@ -199,6 +209,18 @@ namespace {
 
 int ensure_device(smaml_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
+  return SMAML_OK;
+}
+
+int free_keep(smaml_ctx* c) {
+  if (c->keep_mem.empty()) return SMAML_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  for (float* p : c->keep_mem) HIP_TRY(hipFree(p));
+  c->keep_mem.clear();
+  c->keep_n = 0;
+  c->keep_rows = 0;
+  c->keep_tried_K = -1;
+  c->keep_tried_rows = -1;
   return SMAML_OK;
 }
 
@@ -249,6 +271,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   int64_t total = 0;
   for (auto& p : parts) total += (p.second + 255) / 256 * 256;
   c->act_B = -1;
+  TRY(free_keep(c));
   if (c->arena) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipFree(c->arena));
@@ -277,6 +300,10 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   c->z_cap = zc;
   c->so_cap = so;
   c->F_main = w.F;
+  c->Hs_main = w.Hs;
+  c->Cs_main = w.Cs;
+  c->Gs_main = w.Gs;
+  c->w.dG = w.Gs;
   c->so_u = so_u;
   c->so_hu = so_hu;
   if (so_hu) HIP_TRY(hipMemset(so_hu, 0, (size_t)zc * c->po.P * 4));
@@ -323,6 +350,71 @@ int ensure_so_store(smaml_ctx* c, int K, int Z, int B) {
   return SMAML_OK;
 }
 
+// Primal activations of the last inner steps, kept for the second-order sweep so that its
+// dual kernels run tangent-only for those steps (no primal recompute of the forward or the
+// BPTT GEMMs). Slot 0 (step K-1) keeps the workspace's own Hs/Cs/Gs -- the query then runs in
+// the tangent buffers -- and adds dG + dh; slot i >= 1 (step K-1-i) holds its own
+// Hs/Cs/Gs/dG/dh. Best effort: as many slots as fit in free HBM with a margin, capped by the
+// SMAML_KEEP environment variable (0 disables). Needs the GCN feature cache (so_F).
+int ensure_keep(smaml_ctx* c, int K, int Z, int B) {
+  const Dims& d = c->d;
+  int want = c->so_F ? K : 0;
+  if (const char* e = std::getenv("SMAML_KEEP")) want = std::min(want, std::max(0, std::atoi(e)));
+  const int64_t rowsL = (int64_t)Z * B * d.T * d.N * d.L;
+  if (want <= c->keep_n && rowsL <= c->keep_rows) return SMAML_OK;
+  if (want == c->keep_tried_K && rowsL == c->keep_tried_rows) return SMAML_OK;  // already as many as fit
+  TRY(free_keep(c));
+  c->keep_tried_K = want;
+  c->keep_tried_rows = rowsL;
+  const int64_t margin = 8ll << 30;
+  for (int i = 0; i < want; ++i) {
+    const int64_t bytes = rowsL * (i == 0 ? 5 : 11) * d.H * 4;  // [dG | dh] or [Hs | Cs | Gs | dG | dh]
+    size_t freeb = 0, totb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totb));
+    float* p = nullptr;
+    if ((int64_t)freeb < bytes + margin || hipMalloc((void**)&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      break;
+    }
+    c->keep_mem.push_back(p);
+  }
+  c->keep_n = (int)c->keep_mem.size();
+  c->keep_rows = rowsL;
+  return SMAML_OK;
+}
+
+// Points the workspace's primal activation buffers at the workspace's own (slot < 0), at a
+// kept slot, or (query, when slot 0 holds the workspace's own) at the tangent buffers.
+enum { SET_MAIN = -1, SET_QUERY = -2 };
+void use_primal(smaml_ctx* c, int slot) {
+  Work& w = c->w;
+  const int64_t rowsL = (int64_t)w.Z * w.B * c->d.T * c->d.N * c->d.L;
+  const int64_t H = c->d.H;
+  w.dh = nullptr;
+  if (slot == SET_QUERY) {
+    w.Hs = w.RHs;
+    w.Cs = w.RCs;
+    w.Gs = w.dG = w.RGs;
+  } else if (slot < 0) {
+    w.Hs = c->Hs_main;
+    w.Cs = c->Cs_main;
+    w.Gs = w.dG = c->Gs_main;
+  } else if (slot == 0) {
+    w.Hs = c->Hs_main;
+    w.Cs = c->Cs_main;
+    w.Gs = c->Gs_main;
+    w.dG = c->keep_mem[0];
+    w.dh = c->keep_mem[0] + rowsL * 4 * H;
+  } else {
+    float* p = c->keep_mem[slot];
+    w.Hs = p;
+    w.Cs = p + rowsL * H;
+    w.Gs = p + rowsL * 2 * H;
+    w.dG = p + rowsL * 6 * H;
+    w.dh = p + rowsL * 10 * H;
+  }
+}
+
 int ensure_xtab(smaml_ctx* c, int64_t n) {
   if (n <= c->xtab_cap) return SMAML_OK;
   if (c->xtab) {
@@ -353,6 +445,8 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.M = B * c->d.N;
   c->w.lblocks = (c->w.M + 127) / 128;
   c->w.F = c->F_main;
+  c->w.primal_kept = 0;
+  if (c->Hs_main) use_primal(c, SET_MAIN);
 }
 
 #define TIMED(c, s, cat, fl, stmt)                              \
@@ -451,7 +545,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
-    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.Gs + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
                        w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
                        lo.bhh);
   }
@@ -479,7 +573,8 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   }
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
-    const double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
+    double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
+    if (w.primal_kept) fl -= fwd_wave(d, w, c->po, diag, 0, false, wv);  // tangent pass only
     TIMED(c, s, C_FWD_DUAL, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
   }
   HIP_TRY(hipGetLastError());
@@ -501,14 +596,14 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true);
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
-    const double fl = bwd_wave(d, w, po, e, 0, true, wv);
+    const double fl = bwd_wave(d, w, po, e, 0, true, wv) * (w.primal_kept ? 2.0 / 3.0 : 1.0);
     TIMED(c, s, C_BWD_DUAL, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
     const int l = d.L - 1 - (e - (d.T - 1));
     if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
-    const float* dGl = w.Gs + (int64_t)l * lsz * 4;
+    const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
                        TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false);
@@ -636,6 +731,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->so_norm) (void)hipFree(c->so_norm);
   if (c->so_coef) (void)hipFree(c->so_coef);
   if (c->so_F) (void)hipFree(c->so_F);
+  for (float* p : c->keep_mem) (void)hipFree(p);
   for (auto& r : c->tm.recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
@@ -675,6 +771,8 @@ int smaml_reserve(smaml_ctx* c, int32_t tasks, int32_t batch) {
 }
 
 int64_t smaml_workspace_bytes(const smaml_ctx* c) { return c ? c->arena_bytes : 0; }
+
+int32_t smaml_so_kept_steps(const smaml_ctx* c) { return c ? c->keep_last : 0; }
 
 int smaml_gcn_conv(smaml_ctx* c, void* stream, const float* x, int32_t rows, int32_t cin, const float* weight,
                    const float* bias, int32_t cout, float* out) {
@@ -747,7 +845,10 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const int B = batch;
   TRY(reserve(c, Z, B, order == 2));
   if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z, B));
+  if (order == 2) TRY(ensure_keep(c, steps, Z, B));
   set_work(c, Z, B);
+  const int nkeep = order == 2 ? std::min(c->keep_n, steps) : 0;
+  c->keep_last = nkeep;
   // sample window table for every step (support steps then the query batch)
   const int64_t nptr = (int64_t)(steps + 1) * Z * B;
   std::vector<const float*> ptrs(nptr);
@@ -782,6 +883,8 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       HIP_TRY(hipMemcpyAsync(c->so_theta + (int64_t)k * Z * P, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
       c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
     }
+    const int slot = steps - 1 - k;
+    use_primal(c, slot < nkeep ? slot : SET_MAIN);
     TRY(run_forward(c, s, c->fast, P, xt));
     TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
     TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
@@ -802,6 +905,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   }
   const float* const* xq = c->xtab + (int64_t)steps * Z * B;
   c->w.F = c->F_main;
+  use_primal(c, nkeep > 0 ? SET_QUERY : SET_MAIN);  // slot 0 holds the workspace's own Hs/Cs/Gs
   TRY(run_forward(c, s, c->fast, P, xq));
   TIMED(c, s, C_HEAD, head_fl,
         launch_head_loss(s, d, c->w, c->fast, P, c->po, xq, 2.f * inv * query_scale, true));
@@ -815,6 +919,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     if (fast_out) HIP_TRY(hipMemcpyAsync(fast_out, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
     fast_out = nullptr;
     TRY(run_backward(c, s, c->fast, P, c->grad));
+    use_primal(c, SET_MAIN);
     float* V = c->grad;
     for (int k = steps - 1; k >= 0; --k) {
       const float* th = c->so_theta + (int64_t)k * Z * P;
@@ -824,11 +929,16 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
             launch_so_dir(s, V, gk, P, Z, c->w.sqpart, c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z,
                           max_norm, c->so_u));
       c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
+      const int slot = steps - 1 - k;
+      use_primal(c, slot < nkeep ? slot : SET_MAIN);
+      c->w.primal_kept = slot < nkeep ? 1 : 0;
       TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
       TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
+      c->w.primal_kept = 0;
     }
+    use_primal(c, SET_MAIN);
     TIMED(c, s, C_MISC, 0, launch_sum_tasks(s, V, P, Z, meta_grad));
     c->w.F = c->F_main;
   }

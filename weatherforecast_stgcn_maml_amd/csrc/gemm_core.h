@@ -219,7 +219,7 @@ struct DualStage {
   static constexpr int FLOATS = 2 * (2 * C::A_STAGE + 2 * C::B_STAGE);
 };
 
-template <class C, bool A2>
+template <class C, bool A2, bool PRIMAL = true>
 __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, int h, Acc<C>& accp, Acc<C>& acct) {
   constexpr int BKc = C::BK;
   constexpr int SA = C::A_STAGE, SB = C::B_STAGE;
@@ -242,7 +242,8 @@ __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, in
       for (int i = 0; i < C::WTM; ++i)
 #pragma unroll
         for (int j = 0; j < C::WTN; ++j) {
-          accp.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b[j], e), accp.v[i][j], 0, 0, 0);
+          if (PRIMAL)
+            accp.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b[j], e), accp.v[i][j], 0, 0, 0);
           acct.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b2[j], e), acct.v[i][j], 0, 0, 0);
           if (A2)
             acct.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a2[i], e), f4get(b[j], e), acct.v[i][j], 0, 0, 0);
@@ -250,7 +251,9 @@ __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, in
   }
 }
 
-template <class C, class LA, class LA2, class LB, class LB2>
+// PRIMAL = false: tangent only (acc_t += A2 . B + A . B2), acc_p untouched -- the primal
+// product is already stored (second-order sweep with the inner step's activations kept).
+template <class C, bool PRIMAL = true, class LA, class LA2, class LB, class LB2>
 __device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2, const LB& lb, const LB2& lb2,
                                                    int m0, int n0, int K, int a2_kbeg, Acc<C>& accp, Acc<C>& acct,
                                                    float* smem) {
@@ -287,9 +290,9 @@ __device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2,
     if (more) fetch(k0 + BKc);
     const float* st = smem + cur * STAGE;
     if (k0 >= a2_kbeg)
-      dual_mma<C, true>(st, arow, brow, h, accp, acct);
+      dual_mma<C, true, PRIMAL>(st, arow, brow, h, accp, acct);
     else
-      dual_mma<C, false>(st, arow, brow, h, accp, acct);
+      dual_mma<C, false, PRIMAL>(st, arow, brow, h, accp, acct);
     if (more) store(smem + (cur ^ 1) * STAGE, k0 + BKc);
     __syncthreads();
   }

@@ -45,6 +45,10 @@ struct Work {
   float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
   float* F;                // [Z][T][M][Hc] LSTM layer-0 input
   float *Hs, *Cs, *Gs;     // [L][Z][T][M][H] / [L][Z][T][M][H] / [L][Z][T][M][4H]
+  float* dG;               // BPTT output [L][Z][T][M][4H]: == Gs (in place) unless the step's
+                           // primal is kept for the second-order sweep (then its own slab)
+  float* dh;               // optional: the BPTT's dh [L][Z][T][M][H] (kept for the SO sweep)
+  int primal_kept;         // SO sweep: Hs/Cs/Gs/dG/dh hold this step's primal (tangent-only kernels)
   float *dH, *dc;          // head's dh_T [Z][M][H]; cell-state carry per layer [L][Z][M][H]
                            // (the BPTT writes dG in place over Gs: [L][Z][T][M][4H])
   float *pred, *dpred;     // [Z][M][HfC]

@@ -452,8 +452,11 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
   return fl;
 }
 
+// GsAll: gates in; dGAll: dG out (== GsAll: in place) and the neighbours' dG read by the GEMM;
+// dhAll (optional): the step's dh kept for the second-order sweep ([L][Z][T][M][H]).
 template <int H, class CfgNN>
-__global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(float* __restrict__ GsAll, const float* __restrict__ CsAll,
+__global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(const float* GsAll, float* dGAll,
+                                                      float* __restrict__ dhAll, const float* __restrict__ CsAll,
                                                       const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
                                                       BwdWave wv, int L, int T, int M) {
@@ -467,7 +470,9 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(flo
   const int m0 = ((int)blockIdx.x - b0) * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
-  float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in, dG out
+  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in
+  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;        // dG out
+  float* dhz = dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr;
   const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
   float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
   Acc<CfgNN> acc;
@@ -475,8 +480,8 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(flo
   {
     // segments [above | next], compacted with selects (static indices keep the loaders in registers)
     const bool up = l + 1 < L, nx = t + 1 < T;
-    const float* pa = GsAll + (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
-    const float* pn = Gz + (int64_t)(t + 1) * M * G4;
+    const float* pa = dGAll + (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
+    const float* pn = dGz + (int64_t)(t + 1) * M * G4;
     const int ns = (up ? 1 : 0) + (nx ? 1 : 0);
     SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
     SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
@@ -509,11 +514,12 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(flo
       const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
       const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
       const float dct = dcin + dh * go * (1.f - tc * tc);
-      stb(Gz, 4u * (og), dct * gg * gi * (1.f - gi));
-      stb(Gz, 4u * (og + H), dct * cp * gf * (1.f - gf));
-      stb(Gz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
-      stb(Gz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
+      stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
+      stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
+      stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
+      stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
       stb(dcz, 4u * (oc), dct * gf);
+      if (dhz) stb(dhz, 4u * (oh), dh);
     }
   }
 }
@@ -528,13 +534,13 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
   if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
     dim3 grid(wv.off[wv.n], ntn, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgBwd><<<grid, CfgBwd::NTH, 0, s>>>(
-                              w.Gs, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
   } else {
     const int ntms = (w.M + CfgNNs::BM - 1) / CfgNNs::BM, ntns = (d.H + CfgNNs::BN - 1) / CfgNNs::BN;
     bwd_wave(d, w, po, e, ntms, false, wv);
     dim3 grid(wv.off[wv.n], ntns, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
-                              w.Gs, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
   }
 }
 

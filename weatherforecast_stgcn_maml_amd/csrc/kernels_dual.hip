@@ -15,9 +15,6 @@
 
 namespace smaml {
 
-#ifndef SMAML_DUAL_RELOAD
-#define SMAML_DUAL_RELOAD 1  // 1: tangent gate kernel keeps one accumulator set live (re-reads gates)
-#endif
 #ifndef SMAML_DUAL_BK
 #define SMAML_DUAL_BK 16
 #endif
@@ -41,7 +38,9 @@ __device__ __forceinline__ float block_sum_f(float v, float* red) {
 }
 
 // ====================================================================================
-template <int H>
+// KEPT: the primal of this step (gates, c, h) is already in Hs / Cs / Gs (kept from the inner
+// step for the second-order sweep): only the tangent pass runs.
+template <int H, bool KEPT>
 __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
                                                       float* __restrict__ HsAll, float* __restrict__ CsAll,
                                                       float* __restrict__ GsAll, float* __restrict__ RHsAll,
@@ -85,7 +84,6 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
 
-#if SMAML_DUAL_RELOAD
   // Register diet: the primal epilogue runs between the two passes (its accumulators die
   // there), and the tangent epilogue re-reads the gates / cell it needs from the lines this
   // lane has just written (program order: a lane sees its own stores). One accumulator set
@@ -94,7 +92,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   const int rb = m0 + acc_row<CfgGateD>(0, 0);
   const bool full = m0 + CfgGateD::BM <= M;
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
-  {
+  if (!KEPT) {
     Acc<CfgGateD> ap;
     ap.zero();
     SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
@@ -164,69 +162,6 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     stb(RHz, 4u * (oh), ro * tc + go * (1.f - tc * tc) * rc);
   }
 }
-#else
-  Acc<CfgGateD> ap, at;
-  ap.zero();
-  at.zero();
-  // two passes (the fused 4-operand loop does not fit the 4-gate tile's registers):
-  //   ap = [x|h].[W_ih|W_hh]^T ;  at = [x|h|Rx|Rh].[U_ih|U_hh|W_ih|W_hh]^T
-  {
-    SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
-    SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
-    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh, ap, smem);
-  }
-  {
-    const int wrx = rxt ? cin : 0;
-    SegKC la{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M};
-    SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
-    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
-  }
-  const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
-  if (j >= H) return;
-  float bp[4], bu[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    bp[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
-    bu[g] = u[lo.bih + g * H + j] + u[lo.bhh + g * H + j];
-  }
-  const int rb = m0 + acc_row<CfgGateD>(0, 0);
-  const bool full = m0 + CfgGateD::BM <= M;
-  const uint32_t tM = (uint32_t)t * (uint32_t)M;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = rb + racc(r);
-    if (!full && m >= M) continue;
-    const uint32_t row = tM + (uint32_t)m;
-    const uint32_t oh = row * H + j;
-    const uint32_t og = row * G4 + j;
-    const float gi = sigmoidf_(ap.v[0][0][r] + bp[0]);
-    const float gf = sigmoidf_(ap.v[0][1][r] + bp[1]);
-    const float gg = tanhf_(ap.v[0][2][r] + bp[2]);
-    const float go = sigmoidf_(ap.v[0][3][r] + bp[3]);
-    const float ri = gi * (1.f - gi) * (at.v[0][0][r] + bu[0]);
-    const float rf = gf * (1.f - gf) * (at.v[0][1][r] + bu[1]);
-    const float rg = (1.f - gg * gg) * (at.v[0][2][r] + bu[2]);
-    const float ro = go * (1.f - go) * (at.v[0][3][r] + bu[3]);
-    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-    const float rcp = t > 0 ? ldb(RCz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-    const float c = gf * cp + gi * gg;
-    const float rc = rf * cp + gf * rcp + ri * gg + gi * rg;
-    const float tc = tanhf_(c);
-    stb(Gz, 4u * (og), gi);
-    stb(Gz, 4u * (og + H), gf);
-    stb(Gz, 4u * (og + 2 * H), gg);
-    stb(Gz, 4u * (og + 3 * H), go);
-    stb(RGz, 4u * (og), ri);
-    stb(RGz, 4u * (og + H), rf);
-    stb(RGz, 4u * (og + 2 * H), rg);
-    stb(RGz, 4u * (og + 3 * H), ro);
-    stb(Cz, 4u * (oh), c);
-    stb(Hz, 4u * (oh), go * tc);
-    stb(RCz, 4u * (oh), rc);
-    stb(RHz, 4u * (oh), ro * tc + go * (1.f - tc * tc) * rc);
-  }
-}
-#endif
 
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                                const float* U, int64_t tstride, const ParamOff& po, double* flops) {
@@ -238,8 +173,13 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   if (flops) *flops = fl;
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT><<<grid, CfgGateD::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs,
-                                                                            lsz, theta, U, tstride, wv, d.T, w.M));
+  if (w.primal_kept) {
+    SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, true><<<grid, CfgGateD::NTH, 0, s>>>(
+                              w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, d.T, w.M));
+  } else {
+    SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, false><<<grid, CfgGateD::NTH, 0, s>>>(
+                              w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, d.T, w.M));
+  }
 }
 
 // ====================================================================================
@@ -357,8 +297,14 @@ using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, fal
 //   dh  = A . B,   R(dh) = A2 . B + A . B2   with  A = [dG(l+1,t) | dG(l,t+1)],
 //   A2 = [R dG(l+1,t) | R dG(l,t+1)],  B = [W_ih(l+1) ; W_hh(l)],  B2 = [U_ih(l+1) ; U_hh(l)]
 // then the cell backward and its product-rule tangent; dG / R(dG) overwrite G / R(G) in place.
-template <int H, class CfgNND>
-__global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(float* __restrict__ GsAll, float* __restrict__ RGsAll,
+//
+// KEPT: the step's primal BPTT is kept from the inner step (gates in GsAll, dG in dGAll, dh in
+// dhAll): the GEMM forms only the tangent (R(dh) = A2 . B + A . B2), the primal cell backward is
+// re-derived elementwise from the kept dh, and only R(dG) and the carries are written.
+// Otherwise dGAll == GsAll (dG written in place over the gates) and dhAll is unused.
+template <int H, class CfgNND, bool KEPT>
+__global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(const float* GsAll, float* dGAll,
+                                                      const float* __restrict__ dhAll, float* __restrict__ RGsAll,
                                                       const float* __restrict__ CsAll, const float* __restrict__ RCsAll,
                                                       const float* __restrict__ dHhead, const float* __restrict__ RdHhead,
                                                       float* __restrict__ dcAll, float* __restrict__ RdcAll,
@@ -376,8 +322,10 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(f
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
-  float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;    // gates in, dG out
-  float* RGz = RGsAll + (int64_t)l * lsz * 4 + slab * G4;  // R(gates) in, R(dG) out
+  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in
+  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;        // dG out (in place unless KEPT)
+  float* RGz = RGsAll + (int64_t)l * lsz * 4 + slab * G4;       // R(gates) in, R(dG) out
+  const float* dhz = dhAll + (int64_t)l * lsz + slab * H;
   const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
   const float* RCz = RCsAll + (int64_t)l * lsz + slab * H;
   float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
@@ -391,11 +339,11 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(f
     const int64_t on = (int64_t)(t + 1) * M * G4;
     const int ns = (up ? 1 : 0) + (nx ? 1 : 0);
     const int w0 = ns >= 1 ? G4 : 0, w1 = ns >= 2 ? G4 : 0;
-    SegKC la{{up ? GsAll + oa : Gz + on, up ? Gz + on : nullptr, nullptr, nullptr}, {w0, w1, 0, 0}, M};
+    SegKC la{{up ? dGAll + oa : dGz + on, up ? dGz + on : nullptr, nullptr, nullptr}, {w0, w1, 0, 0}, M};
     SegKC la2{{up ? RGsAll + oa : RGz + on, up ? RGz + on : nullptr, nullptr, nullptr}, {w0, w1, 0, 0}, M};
     SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {w0, w1}, H};
     SegMC lb2{{up ? u + wih_up : u + lo.whh, u + lo.whh}, {w0, w1}, H};
-    if (ns) gemm_dual_mainloop<CfgNND>(la, la2, lb, lb2, m0, n0, ns * G4, 0, ap, at, smem);
+    if (ns) gemm_dual_mainloop<CfgNND, !KEPT>(la, la2, lb, lb2, m0, n0, ns * G4, 0, ap, at, smem);
   }
   const bool first = (t == T - 1);
   const bool head = first && l == L - 1;
@@ -418,7 +366,7 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(f
       const uint32_t oh = row * H + j;
       const uint32_t og = row * G4 + j;
       const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = ap.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
+      const float dh = KEPT ? ldb(dhz, 4u * oh) : ap.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
       const float rdh = at.v[i][jj][r] + (head ? ldb(RdHz, 4u * oc) : 0.f);
       const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
       const float ri = ldb(RGz, 4u * (og)), rf = ldb(RGz, 4u * (og + H)), rgg = ldb(RGz, 4u * (og + 2 * H)), ro = ldb(RGz, 4u * (og + 3 * H));
@@ -433,10 +381,12 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(f
       const float dct = dcin + dh * go * s2;
       const float rdct = rdcin + rdh * go * s2 + dh * ro * s2 - 2.f * dh * go * tc * rtc;
       const float si = gi * (1.f - gi), sf = gf * (1.f - gf), so = go * (1.f - go), sg = 1.f - gg * gg;
-      stb(Gz, 4u * (og), dct * gg * si);
-      stb(Gz, 4u * (og + H), dct * cp * sf);
-      stb(Gz, 4u * (og + 2 * H), dct * gi * sg);
-      stb(Gz, 4u * (og + 3 * H), dh * tc * so);
+      if (!KEPT) {
+        stb(dGz, 4u * (og), dct * gg * si);
+        stb(dGz, 4u * (og + H), dct * cp * sf);
+        stb(dGz, 4u * (og + 2 * H), dct * gi * sg);
+        stb(dGz, 4u * (og + 3 * H), dh * tc * so);
+      }
       stb(RGz, 4u * (og), rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri);
       stb(RGz, 4u * (og + H), rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf);
       stb(RGz, 4u * (og + 2 * H), rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg);
@@ -447,25 +397,36 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(f
   }
 }
 
+template <class Cfg, bool KEPT>
+static void bwd_dual_grid(hipStream_t s, const Dims& d, const Work& w, const BwdWave& wv, int ntn, const float* theta,
+                          const float* U, int64_t tstride) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  dim3 grid(wv.off[wv.n], ntn, w.Z);
+  const float* dh = KEPT ? w.dh : w.Gs;  // unread unless KEPT
+  SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, Cfg, KEPT><<<grid, Cfg::NTH, 0, s>>>(
+                            w.Gs, w.dG, dh, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv,
+                            d.L, d.T, w.M));
+}
+
 void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
                                const float* U, int64_t tstride, const ParamOff& po) {
-  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   BwdWave wv{};
   const int ntm = (w.M + CfgBwdD::BM - 1) / CfgBwdD::BM, ntn = (d.H + CfgBwdD::BN - 1) / CfgBwdD::BN;
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
+  const bool kept = w.primal_kept != 0;
   if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
-    dim3 grid(wv.off[wv.n], ntn, w.Z);
-    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgBwdD><<<grid, CfgBwdD::NTH, 0, s>>>(
-                              w.Gs, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv, d.L,
-                              d.T, w.M));
+    if (kept)
+      bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
+    else
+      bwd_dual_grid<CfgBwdD, false>(s, d, w, wv, ntn, theta, U, tstride);
   } else {
     const int ntms = (w.M + CfgNNDs::BM - 1) / CfgNNDs::BM, ntns = (d.H + CfgNNDs::BN - 1) / CfgNNDs::BN;
     bwd_wave(d, w, po, e, ntms, true, wv);
-    dim3 grid(wv.off[wv.n], ntns, w.Z);
-    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, CfgNNDs><<<grid, CfgNNDs::NTH, 0, s>>>(
-                              w.Gs, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv, d.L,
-                              d.T, w.M));
+    if (kept)
+      bwd_dual_grid<CfgNNDs, true>(s, d, w, wv, ntns, theta, U, tstride);
+    else
+      bwd_dual_grid<CfgNNDs, false>(s, d, w, wv, ntns, theta, U, tstride);
   }
 }
 
