@@ -42,7 +42,20 @@ def parse():
     p.add_argument("--cpu-sample-steps", type=int, default=6,
                    help="reference-port CPU sample-steps to time (0 = skip)")
     p.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
-    return p.parse_args()
+    p.add_argument("--config", type=int, default=2, choices=(2, 5),
+                   help="5 = BASELINE stress config: 64 tasks, N=1024 (32x32), Hc=512, LSTM 4x128, K=10, "
+                        "second order (flags given explicitly still win, e.g. --tasks 8 = one rank's share at 8 GPUs)")
+    p.add_argument("--hidden-channels", type=int, default=None)
+    p.add_argument("--task-group", type=int, default=None,
+                   help="tasks per pass of the C driver (default: all of this rank's tasks)")
+    args = p.parse_args()
+    if args.config == 5:
+        given = {a.split("=")[0] for a in sys.argv[1:] if a.startswith("--")}
+        for flag, key, val in (("--tasks", "tasks", 64), ("--nodes", "nodes", 1024), ("--inner-steps", "inner_steps", 10),
+                               ("--hidden-channels", "hidden_channels", 512), ("--cpu-sample-steps", "cpu_sample_steps", 0)):
+            if flag not in given:
+                setattr(args, key, val)
+    return args
 
 
 def algorithmic_flops(d, tasks, K, B, order):
@@ -126,7 +139,7 @@ def main():
     init_from_env(os.environ.get("SMAML_DIST_BACKEND", "nccl"), torch.device("cuda", dev_idx))
     local = dev_idx
 
-    d = ModelDims(num_nodes=args.nodes)
+    d = ModelDims(num_nodes=args.nodes, hidden_channels=args.hidden_channels or 256)
     cfg = MamlConfig(inner_steps=args.inner_steps, batch=args.batch, order=args.order)
     side = int(round(d.num_nodes ** 0.5))
     lats, lons = synth.region_grid(n_lat=side, n_lon=side)
@@ -137,7 +150,7 @@ def main():
     T_total = stream_len_for(cfg, d)
     feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T_total) for j in mine]
     ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
-                     ei, device=f"cuda:{local}")
+                     ei, device=f"cuda:{local}", task_group=args.task_group)
     ml.set_tasks(feats)
     torch.cuda.synchronize()
 
@@ -172,7 +185,8 @@ def main():
     value = args.steps / elapsed
     flops_meta = algorithmic_flops(d, args.tasks, cfg.inner_steps, cfg.batch, cfg.order)
     out = {
-        "metric": "MAML meta-steps/sec (15-task batch, N=441, T=24)",
+        "metric": "MAML meta-steps/sec (15-task batch, N=441, T=24)" if args.config == 2 else
+                  "MAML meta-steps/sec (BASELINE config 5 stress: 64 tasks, N=1024, Hc=512, K=10)",
         "value": value,
         "unit": "meta-steps/s",
         "n_gpus": world,
@@ -185,13 +199,14 @@ def main():
         "dtype": "f32",
         "data": "synthetic ERA5-shaped feature streams (numpy PCG64 seeds 1000+j), random-init weights",
         "config": {
-            "workload": f"BASELINE config 2: {args.tasks} tasks x B={cfg.batch} x T={d.window_size} x "
+            "workload": f"BASELINE config {args.config}: {args.tasks} tasks x B={cfg.batch} x T={d.window_size} x "
                         f"N={d.num_nodes} x C={d.input_channels}, Hc={d.hidden_channels}, "
                         f"LSTM {d.lstm_num_layers}x{d.lstm_hidden_size}, K={cfg.inner_steps} inner steps",
             "tasks": args.tasks, "batch": cfg.batch, "inner_steps": cfg.inner_steps,
             "maml_order": cfg.order, "parallelism": f"task-sharded x{world} + RCCL all-reduce",
             "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
             "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
+            "task_group": args.task_group or len(mine),
         },
         "meta_step_tflop": flops_meta / 1e12,
         "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,

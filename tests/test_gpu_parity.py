@@ -13,7 +13,7 @@ import torch
 
 from oracle import refcpu
 from weatherforecast_stgcn_maml_amd import _capi, params, synth
-from weatherforecast_stgcn_maml_amd.config import CONFIG1, CONFIG2, MamlConfig, ModelDims
+from weatherforecast_stgcn_maml_amd.config import CONFIG1, CONFIG2, CONFIG5, MamlConfig, ModelDims
 from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
 from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for, window_table
 
@@ -351,3 +351,49 @@ def test_second_order_matches_oracle_cfg2(max_norm, keep, monkeypatch):
     mg = params.unpack(ml.meta_grad, d, 0)
     for k in names:
         assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
+
+
+# ----------------------------------------------------------------------------- config 5 shapes
+def test_second_order_matches_oracle_cfg5():
+    """BASELINE config-5 shapes (N=1024 32x32 grid, Hc=512, LSTM 4x128), K=2, B=1, 1 task:
+    second-order meta-gradient and query MSE against the oracle."""
+    d = CONFIG5
+    cfg = MamlConfig(inner_steps=2, batch=1, order=2)
+    P = synth.init_params(9, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1300, d.num_nodes, stream_len_for(cfg, d))]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml.set_tasks(feats)
+    res = ml.meta_step()
+    PT = refcpu.to_torch(P)
+    S = cfg.inner_steps * cfg.batch
+    ref = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
+                           [refcpu.TaskData(feats[0], ei, d)], list(range(S, S + cfg.batch)),
+                           cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, 2)
+    q = float(res.losses[-1, 0].item())
+    assert abs(q - ref["query_losses"][0]) < 1e-4 * ref["query_losses"][0]
+    mg = params.unpack(ml.meta_grad, d, 0)
+    for k in names:
+        assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
+
+
+@pytest.mark.parametrize("order", [1, 2])
+def test_task_groups_match_one_pass(order):
+    """A rank running its tasks in groups (task_group) gives the one-pass losses and the same
+    meta-gradient (summed over groups before the outer step; rounding-level difference)."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=2, order=order)
+    P = synth.init_params(10, d)
+    theta, gcn, _ = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1400 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(3)]
+    out = []
+    for g in (None, 2):
+        ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=g)
+        ml.set_tasks(feats)
+        res = ml.meta_step()
+        out.append((res.losses.cpu().numpy(), ml.meta_grad.cpu().numpy(), ml.theta.cpu().numpy()))
+    assert rel(out[1][0], out[0][0]) < 1e-6
+    assert rel(out[1][1], out[0][1]) < 1e-6
+    assert rel(out[1][2], out[0][2]) < 1e-6

@@ -56,9 +56,13 @@ class MetaLearner:
     """Holds theta (flat trainable vector), AdamW state and the tasks of this rank."""
 
     def __init__(self, dims: ModelDims, cfg: MamlConfig, gcn_params: dict, theta: dict,
-                 edge_index: np.ndarray, device=None, process_group=None):
+                 edge_index: np.ndarray, device=None, process_group=None, task_group: Optional[int] = None):
+        """``task_group``: tasks batched into one pass of the C driver (all of this rank's by
+        default). A rank whose tasks do not fit in HBM at once runs them in groups of this
+        size; the meta-gradient is summed over groups before the all-reduce and outer step."""
         self.dims = dims
         self.cfg = cfg
+        self.task_group = task_group
         self.device = torch.device(device or "cuda")
         self.ctx = _capi.Context(dims, self.device.index or 0)
         self.ctx.set_graph(edge_index)
@@ -80,8 +84,11 @@ class MetaLearner:
             t = f if torch.is_tensor(f) else torch.from_numpy(np.ascontiguousarray(f))
             feats.append(t.to(self.device, torch.float32).contiguous())
         self.tasks = feats
-        self.ctx.set_tasks(feats)
-        self.ctx.reserve(len(feats), self.cfg.batch)
+        G = min(self.task_group or len(feats), len(feats))
+        self._groups = [(z0, feats[z0:z0 + G]) for z0 in range(0, len(feats), G)]
+        self.ctx.set_tasks(self._groups[0][1])
+        self.ctx.reserve(G, self.cfg.batch)
+        self._mg_part = torch.zeros_like(self.meta_grad) if len(self._groups) > 1 else None
 
     def meta_step(self, windows: Optional[np.ndarray] = None, fast_out=None, sync=True,
                   lr: Optional[float] = None) -> StepResult:
@@ -90,13 +97,31 @@ class MetaLearner:
         if windows is None:
             windows = window_table(cfg, Z)
         K = cfg.inner_steps
-        losses = torch.empty(K + 1, Z, device=self.device)
-        norms = torch.empty(max(K, 1), Z, device=self.device)
         stream = _capi.stream_ptr(torch)
-        self.ctx.meta_step(stream, self.theta, cfg.order, K, cfg.batch, windows, cfg.inner_lr,
-                           cfg.max_norm, cfg.query_loss_scale,
-                           meta_grad=self.meta_grad if cfg.order >= 1 else None,
-                           losses=losses, norms=norms, fast_out=fast_out)
+        if len(self._groups) == 1:
+            losses = torch.empty(K + 1, Z, device=self.device)
+            norms = torch.empty(max(K, 1), Z, device=self.device)
+            self.ctx.meta_step(stream, self.theta, cfg.order, K, cfg.batch, windows, cfg.inner_lr,
+                               cfg.max_norm, cfg.query_loss_scale,
+                               meta_grad=self.meta_grad if cfg.order >= 1 else None,
+                               losses=losses, norms=norms, fast_out=fast_out)
+        else:
+            lparts, nparts = [], []
+            for gi, (z0, grp) in enumerate(self._groups):
+                n = len(grp)
+                lg = torch.empty(K + 1, n, device=self.device)
+                ng = torch.empty(max(K, 1), n, device=self.device)
+                self.ctx.set_tasks(grp)
+                mg = (self.meta_grad if gi == 0 else self._mg_part) if cfg.order >= 1 else None
+                self.ctx.meta_step(stream, self.theta, cfg.order, K, cfg.batch, windows[:, z0:z0 + n],
+                                   cfg.inner_lr, cfg.max_norm, cfg.query_loss_scale, meta_grad=mg,
+                                   losses=lg, norms=ng, fast_out=fast_out[z0:z0 + n] if fast_out is not None else None)
+                if gi > 0 and mg is not None:
+                    self.meta_grad.add_(mg)
+                lparts.append(lg)
+                nparts.append(ng)
+            losses = torch.cat(lparts, 1)
+            norms = torch.cat(nparts, 1)
         qsum = (losses[K].sum() * cfg.query_loss_scale).reshape(1)
         reduce_meta(self.meta_grad if cfg.order >= 1 else None, qsum, self.pg)
         if cfg.order >= 1:
