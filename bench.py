@@ -46,9 +46,12 @@ def parse():
                    help="5 = BASELINE stress config: 64 tasks, N=1024 (32x32), Hc=512, LSTM 4x128, K=10, "
                         "second order (flags given explicitly still win, e.g. --tasks 8 = one rank's share at 8 GPUs)")
     p.add_argument("--hidden-channels", type=int, default=None)
-    p.add_argument("--task-group", type=int, default=None,
-                   help="tasks per pass of the C driver (default: all of this rank's tasks)")
+    p.add_argument("--task-group", default="auto",
+                   help="tasks per pass of the C driver: an int, 'all', or 'auto' (default: groups small "
+                        "enough that every inner step's primal stays resident for the second-order sweep)")
     args = p.parse_args()
+    args.task_group = None if args.task_group == "all" else args.task_group if args.task_group == "auto" \
+        else int(args.task_group)
     if args.config == 5:
         given = {a.split("=")[0] for a in sys.argv[1:] if a.startswith("--")}
         for flag, key, val in (("--tasks", "tasks", 64), ("--nodes", "nodes", 1024), ("--inner-steps", "inner_steps", 10),
@@ -206,7 +209,7 @@ def main():
             "maml_order": cfg.order, "parallelism": f"task-sharded x{world} + RCCL all-reduce",
             "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
             "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
-            "task_group": args.task_group or len(mine),
+            "task_group": len(ml._groups[0][1]),
         },
         "meta_step_tflop": flops_meta / 1e12,
         "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,

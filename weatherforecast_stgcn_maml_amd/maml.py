@@ -44,6 +44,36 @@ def stream_len_for(cfg: MamlConfig, dims: ModelDims, support: Optional[int] = No
     return synth.t_total_for(S + cfg.batch, dims.window_size, dims.forecast_horizon)
 
 
+KEEP_MARGIN = 8 << 30   # matches api.cpp ensure_keep's free-HBM margin
+
+
+def task_bytes(dims: ModelDims, cfg: MamlConfig, kept: int) -> int:
+    """Device bytes one task holds in a second-order meta-step (api.cpp reserve /
+    ensure_so_store / ensure_keep): workspace [F, gcn ping-pong: 3 Hc; Hs, Cs, Gs and their
+    tangents: 12 L H per row], the per-step GCN feature cache, and ``kept`` inner steps'
+    primal (the last one 5 L H per row: dG + dh; the others 11 L H: Hs, Cs, Gs, dG, dh)."""
+    rows = cfg.batch * dims.window_size * dims.num_nodes
+    Hc, H, L, K = dims.hidden_channels, dims.lstm_hidden_size, dims.lstm_num_layers, cfg.inner_steps
+    f = rows * (3 * Hc + 12 * L * H) + K * rows * Hc
+    if kept > 0:
+        f += rows * L * H * (5 + 11 * (kept - 1))
+    return 4 * f
+
+
+def plan_task_group(dims: ModelDims, cfg: MamlConfig, n_tasks: int, free_bytes: int) -> int:
+    """Tasks per pass of the C driver for a second-order meta-step: the largest group whose
+    workspace fits with EVERY inner step's primal kept (tangent-only sweep), balanced over the
+    groups it implies; all tasks at once when that already fits (or when nothing would)."""
+    if cfg.order != 2 or n_tasks <= 1:
+        return n_tasks
+    per = task_bytes(dims, cfg, cfg.inner_steps)
+    g = max(1, int((free_bytes - KEEP_MARGIN) // per))
+    if g >= n_tasks:
+        return n_tasks
+    ngroups = -(-n_tasks // g)
+    return -(-n_tasks // ngroups)
+
+
 @dataclass
 class StepResult:
     losses: torch.Tensor        # [(K+1), tasks] (device); last row = query MSE
@@ -56,10 +86,11 @@ class MetaLearner:
     """Holds theta (flat trainable vector), AdamW state and the tasks of this rank."""
 
     def __init__(self, dims: ModelDims, cfg: MamlConfig, gcn_params: dict, theta: dict,
-                 edge_index: np.ndarray, device=None, process_group=None, task_group: Optional[int] = None):
-        """``task_group``: tasks batched into one pass of the C driver (all of this rank's by
-        default). A rank whose tasks do not fit in HBM at once runs them in groups of this
-        size; the meta-gradient is summed over groups before the all-reduce and outer step."""
+                 edge_index: np.ndarray, device=None, process_group=None, task_group="auto"):
+        """``task_group``: tasks batched into one pass of the C driver. ``None`` = all of this
+        rank's tasks at once; ``"auto"`` (default) = plan_task_group: second-order meta-steps run
+        in groups small enough that every inner step's primal stays resident for the sweep.
+        The meta-gradient is summed over groups before the all-reduce and outer step."""
         self.dims = dims
         self.cfg = cfg
         self.task_group = task_group
@@ -84,7 +115,11 @@ class MetaLearner:
             t = f if torch.is_tensor(f) else torch.from_numpy(np.ascontiguousarray(f))
             feats.append(t.to(self.device, torch.float32).contiguous())
         self.tasks = feats
-        G = min(self.task_group or len(feats), len(feats))
+        tg = self.task_group
+        if tg == "auto":
+            free, _ = torch.cuda.mem_get_info(self.device)
+            tg = plan_task_group(self.dims, self.cfg, len(feats), free)
+        G = min(tg or len(feats), len(feats))
         self._groups = [(z0, feats[z0:z0 + G]) for z0 in range(0, len(feats), G)]
         self.ctx.set_tasks(self._groups[0][1])
         self.ctx.reserve(G, self.cfg.batch)
