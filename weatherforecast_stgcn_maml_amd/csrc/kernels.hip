@@ -22,7 +22,7 @@ namespace smaml {
 using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-contiguous)
 using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;  // LSTM forward: wave = 32 rows x 4 gates
 using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK>;  // C = A . B   (B n-contiguous)
-using CfgTN = GemmCfg<128, 128, 2, 2, false, false, SMAML_TN_BK>;  // C = A^T . B (split-K weight grads)
+using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK>;  // C = A^T . B (split-K weight grads)
 
 // ------------------------------------------------------------------------------------
 // Block-wide deterministic sum (fixed shuffle tree + fixed wave order).
@@ -562,7 +562,7 @@ struct ColSumHook {
   }
 };
 
-__global__ __launch_bounds__(NT) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
+__global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
                                               int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
                                               int ldp, int with_bias) {
@@ -647,8 +647,9 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   const int ntm = (Mrows + CfgTN::BM - 1) / CfgTN::BM;
   const int ntn = (ncols + CfgTN::BN - 1) / CfgTN::BN;
   const int64_t ktiles = (K + CfgTN::BK - 1) / CfgTN::BK;
-  // aim for ~2048 workgroups, at least 8 K-tiles per split, bounded by the slab buffer
-  int64_t nsplit = 2048 / ((int64_t)ntm * ntn * w.Z);
+  // aim for ~2048 4-wave workgroups' worth of waves, at least 8 K-tiles per split, bounded by
+  // the slab buffer
+  int64_t nsplit = (SMAML_WGRAD_THREADS / CfgTN::NTH) / ((int64_t)ntm * ntn * w.Z);
   if (nsplit < 1) nsplit = 1;
   if (nsplit > ktiles / 8) nsplit = ktiles / 8 > 0 ? ktiles / 8 : 1;
   const int64_t per_split = (int64_t)w.Z * Mrows * ldp;
@@ -695,7 +696,7 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
   const int ntile = p.ntm * p.ntn;
   const int ngroups = p.nsplit * p.Z;
   dim3 grid((unsigned)(((ngroups + 7) / 8) * 8 * ntile));
-  k_wgrad<<<grid, NT, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn, ntile,
+  k_wgrad<<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn, ntile,
                               p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0);
 }
 

@@ -34,8 +34,26 @@
 #ifndef SMAML_GCN_BK
 #define SMAML_GCN_BK 16
 #endif
+// weight-gradient tile (BM x BN), waves WM x WN: all 4H = 512 gate rows of a layer in one
+// tile (8 waves of 64 x 128), so the split-K slices read each [x | h] row once
+// (profiles/r01_ab_wgrad_tiles.log: 874 -> 798 ms/meta-step against 128 x 128, BK 32)
+#ifndef SMAML_WGRAD_THREADS
+#define SMAML_WGRAD_THREADS (2048 * 256)  // split-K target: total threads of one weight-gradient launch
+#endif
 #ifndef SMAML_TN_BK
-#define SMAML_TN_BK 32
+#define SMAML_TN_BK 16
+#endif
+#ifndef SMAML_TN_BM
+#define SMAML_TN_BM 512
+#endif
+#ifndef SMAML_TN_BN
+#define SMAML_TN_BN 128
+#endif
+#ifndef SMAML_TN_WM
+#define SMAML_TN_WM 8
+#endif
+#ifndef SMAML_TN_WN
+#define SMAML_TN_WN 1
 #endif
 
 // Minimum resident waves per SIMD requested from the register allocator for the LSTM gate
