@@ -236,7 +236,7 @@ __global__ __launch_bounds__(C::NTH) void k_bptt(const float* __restrict__ A, co
         }
         const uint32_t oh = (uint32_t)m * H + j;
         float gi, gf, gg, go;
-        if (EPI == 1) {
+        if (EPI == 1 || EPI >= 6) {
           const uint32_t og = (uint32_t)m * 4 * H + j;
           gi = ldb(G, 4u * og);
           gf = ldb(G, 4u * (og + H));
@@ -250,13 +250,14 @@ __global__ __launch_bounds__(C::NTH) void k_bptt(const float* __restrict__ A, co
           go = g4.w;
         }
         const float c = ldb(Cs, 4u * oh + 4u * M * H);
-        const float cp = ldb(Cs, 4u * oh);
-        const float dcin = ldb(dc, 4u * oh);
+        // EPI 6: cell-state carry in registers (no dc load/store); 7: also c_{t-1} in registers
+        const float cp = EPI == 7 ? c * 0.9f : ldb(Cs, 4u * oh);
+        const float dcin = EPI >= 6 ? c * 0.5f : ldb(dc, 4u * oh);
         const float tc = tanhf_(c);
         const float dct = dcin + dh * go * (1.f - tc * tc);
         const float a0 = dct * gg * gi * (1.f - gi), a1 = dct * cp * gf * (1.f - gf);
         const float a2 = dct * gi * (1.f - gg * gg), a3 = dh * tc * go * (1.f - go);
-        if (EPI == 1) {
+        if (EPI == 1 || EPI >= 6) {
           const uint32_t og = (uint32_t)m * 4 * H + j;
           stb(G, 4u * og, a0);
           stb(G, 4u * (og + H), a1);
@@ -265,7 +266,8 @@ __global__ __launch_bounds__(C::NTH) void k_bptt(const float* __restrict__ A, co
         } else {
           *reinterpret_cast<float4*>(G + (size_t)m * 4 * H + 4 * j) = make_float4(a0, a1, a2, a3);
         }
-        stb(dc, 4u * oh, dct * gf);
+        if (EPI < 6) stb(dc, 4u * oh, dct * gf);
+        else acc.v[i][jj][r] = dct * gf;  // keep the carry live
       }
     }
 }
@@ -386,6 +388,9 @@ int main() {
       {"64x128 NN BK16 cell batch-8", run_bptt<N64, false, 4>, 128},
       {"64x128 NN BK16 cell batch-16", run_bptt<N64, false, 5>, 128},
       {"64x128 NN BK16 plain store", run_bptt<N64, false, 0>, 128},
+      {"64x128 NN BK16 cell, gates [4j+g] float4", run_bptt<N64, false, 2>, 128},
+      {"64x128 NN BK16 cell, dc carry in regs", run_bptt<N64, false, 6>, 128},
+      {"64x128 NN BK16 cell, dc + c_{t-1} in regs", run_bptt<N64, false, 7>, 128},
   };
   for (int K : {512, 1024}) bench("bptt", b, bv, K);
   return 0;
