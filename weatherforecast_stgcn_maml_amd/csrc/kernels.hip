@@ -83,6 +83,21 @@ struct GcnA {
   }
 };
 
+// Rows with no neighbours (t >= 1, F3): layer 1 reads the sample's window, layers 2-4 the
+// previous layer's [g][rps][cin] buffer, which is simply row-major [R][cin].
+struct GcnPlain {
+  const float* const* tab;
+  const float* buf;
+  FastDiv rps_div;
+  int rps, cin, R;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    if (r >= R || k >= cin) return f4zero();
+    if (buf) return ld4(buf + (int64_t)r * cin + k);
+    const int g = (int)rps_div.div((uint32_t)r);
+    return ld4(tab[g] + (int64_t)(r - g * rps) * cin + k);
+  }
+};
+
 // 8 waves, 128 rows x 256 cols: one workgroup covers a row block's whole Hc=256 output,
 // so each input row is read once.
 using CfgGcn = GemmCfg<128, 256, 2, 4, true, true, SMAML_GCN_BK>;
@@ -94,7 +109,14 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
   const int m0 = blockIdx.x * CfgGcn::BM, n0 = blockIdx.y * CfgGcn::BN;
   Acc<CfgGcn> acc;
   acc.zero();
-  gemm_mainloop<CfgGcn>(la, lb, m0, n0, 0, la.cin, acc, smem);
+  // only tiles that reach a sample's t = 0 block (its first N rows) need the ELL gather
+  const int q0 = m0 - (int)la.rps_div.div((uint32_t)m0) * la.rps;
+  if (q0 < la.ell_rows || q0 + CfgGcn::BM > la.rps) {
+    gemm_mainloop<CfgGcn>(la, lb, m0, n0, 0, la.cin, acc, smem);
+  } else {
+    const GcnPlain lp{la.tab, la.buf, la.rps_div, la.rps, la.cin, la.R};
+    gemm_mainloop<CfgGcn>(lp, lb, m0, n0, 0, la.cin, acc, smem);
+  }
   const int64_t M = (int64_t)B * N;
   float bc[CfgGcn::WTN];
 #pragma unroll
