@@ -553,7 +553,7 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
   const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
-  if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
+  if ((int64_t)wv.n * ntm * ntn * w.Z >= SMAML_BWD_BIG_MIN) {
     dim3 grid(wv.off[wv.n], ntn, w.Z);
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgBwd><<<grid, CfgBwd::NTH, 0, s>>>(
                               w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));

@@ -415,7 +415,7 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
   const bool kept = w.primal_kept != 0;
-  if ((int64_t)wv.n * ntm * ntn * w.Z >= 3 * 256) {
+  if ((int64_t)wv.n * ntm * ntn * w.Z >= SMAML_BWDD_BIG_MIN) {
     if (kept)
       bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
     else
