@@ -154,7 +154,7 @@ def main():
     feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T_total) for j in mine]
     ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
                      ei, device=f"cuda:{local}", task_group=args.task_group)
-    ml.set_tasks(feats)
+    ml.set_tasks(feats, task_ids=mine)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):

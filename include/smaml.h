@@ -89,6 +89,18 @@ int64_t smaml_workspace_bytes(const smaml_ctx* ctx);
  * free HBM, capped by the SMAML_KEEP environment variable. New; no reference counterpart. */
 int32_t smaml_so_kept_steps(const smaml_ctx* ctx);
 
+/* Train-mode dropout of smaml_meta_step / smaml_adapt_steps (replaces the nn.Dropout calls at
+ * hybrid_model.py:67,70,73 (p_gcn = STGCN dropout_rate), the nn.LSTM inter-layer dropout
+ * hybrid_model.py:42-49 and the head input dropout :108 (p_lstm = lstm_dropout)). Masks are
+ * counter-based (seed, global task id, inner step, site, element), identical in the
+ * forward, the backward and the second-order sweep; p = 0 (the default) disables them.
+ * The reference draws masks from torch's RNG, so runs agree with it only at p = 0. */
+int smaml_set_dropout(smaml_ctx* ctx, float p_gcn, float p_lstm, uint32_t seed);
+
+/* Global task id of each task of the next smaml_set_tasks batch (the dropout masks' task
+ * index, so a task's masks do not depend on how tasks are grouped or sharded). */
+int smaml_set_task_ids(smaml_ctx* ctx, const int32_t* ids_host, int32_t n);
+
 /* ---- forward (module API) ----------------------------------------------------------- */
 
 /* GCNConv.forward(x, edge_index) (PyG semantics, F3): x [rows, cin] -> out [rows, cout].

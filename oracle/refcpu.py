@@ -21,6 +21,10 @@ What each function follows:
   * ``inner_loop``          train_hybrid_maml_v5.py:110-141 (SGD lr 0.01, batch of B samples)
   * ``meta_step``           train_hybrid_maml_v5.py:144-184 (+ FO / second-order meta-grad)
   * ``ReferencePort``       op-for-op mirror (per-node nn.LSTM loop, batch 1) for CPU timing
+  * ``Dropout``             train-mode dropout (hybrid_model.py:67,70,73,108; nn.LSTM dropout :47)
+                            with the HIP path's counter-based masks (kernels.h drop_keep),
+                            restated here so masks agree bit for bit; the reference draws its
+                            masks from torch's RNG, so only p = 0 is pinned to the reference
 """
 from __future__ import annotations
 
@@ -30,6 +34,64 @@ from typing import Dict, List, Sequence
 import numpy as np
 import torch
 import torch.nn.functional as F
+
+
+# ----------------------------------------------------------------------------- dropout masks
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _mix32(x):
+    """lowbias32 on uint64 arrays holding 32-bit values (kernels.h mix32)."""
+    x = x & _M32
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & _M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & _M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def drop_site(seed: int, kind: int, step: int, layer: int) -> np.uint64:
+    k = np.uint64(((kind << 24) ^ (step << 8) ^ layer) & 0xFFFFFFFF)
+    return _mix32(np.uint64(seed & 0xFFFFFFFF) ^ _mix32(k))
+
+
+def drop_keep(site, idx: np.ndarray, p: float) -> np.ndarray:
+    """bool mask: element idx (uint64) of a site is kept iff (hash >> 8) >= round(p * 2^24)."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    thr = np.uint64(min(int(round(p * 16777216.0)), 16777216))
+    h = _mix32((idx >> np.uint64(32)) + np.uint64(0x9E3779B9))
+    h = _mix32((idx & _M32) ^ h)
+    h = _mix32(np.uint64(site) ^ h)
+    return (h >> np.uint64(8)) >= thr
+
+
+class Dropout:
+    """Masks of one forward pass (meta-step seed, inner step) for one task (global id)."""
+
+    def __init__(self, seed: int, p_gcn: float, p_lstm: float, task: int, step: int):
+        self.seed, self.p_gcn, self.p_lstm, self.task, self.step = seed, p_gcn, p_lstm, task, step
+
+    def _apply(self, x: torch.Tensor, kind: int, layer: int, base: int, p: float) -> torch.Tensor:
+        if p <= 0.0:
+            return x
+        idx = np.uint64(base) + np.arange(x.numel(), dtype=np.uint64)
+        keep = torch.from_numpy(drop_keep(drop_site(self.seed, kind, self.step, layer), idx, p))
+        return x * keep.view(x.shape).to(x.dtype) * (1.0 / (1.0 - p))
+
+    def gcn(self, h: torch.Tensor, layer: int, b: int, B: int) -> torch.Tensor:
+        """h [T*N, Hc] of sample b of the batch after conv layer+1 (layer 0..2)."""
+        return self._apply(h, 1, layer, (self.task * B + b) * h.numel(), self.p_gcn)
+
+    def lstm(self, out: torch.Tensor, layer: int) -> torch.Tensor:
+        """out [M, T, H] (sequences m = b*N + n) of LSTM layer `layer` fed to layer+1; the
+        element order of the masks is [t][m][unit]."""
+        M, T, H = out.shape
+        tm = out.permute(1, 0, 2).contiguous()
+        return self._apply(tm, 2, layer, self.task * T * M * H, self.p_lstm).permute(1, 0, 2)
+
+    def head(self, hT: torch.Tensor) -> torch.Tensor:
+        return self._apply(hT, 3, 0, self.task * hT.numel(), self.p_lstm)
 
 
 # ----------------------------------------------------------------------------- GCN
@@ -53,17 +115,20 @@ def gcn_conv(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor,
     return out + bias
 
 
-def stgcn_features(x: torch.Tensor, edge_index: torch.Tensor, P: Dict[str, torch.Tensor]):
+def stgcn_features(x: torch.Tensor, edge_index: torch.Tensor, P: Dict[str, torch.Tensor],
+                   drop: "Dropout" = None, b: int = 0, B: int = 1):
     h = x
     for k in range(1, 5):
         h = F.relu(gcn_conv(h, edge_index, P[f"base_stgcn.conv{k}.lin.weight"],
                             P[f"base_stgcn.conv{k}.bias"]))
+        if drop is not None and k < 4:
+            h = drop.gcn(h, k - 1, b, B)
     return h
 
 
 # ----------------------------------------------------------------------------- LSTM
-def lstm_stack(seq: torch.Tensor, P: Dict[str, torch.Tensor], layers: int):
-    """seq [B, T, C] -> top-layer h_T [B, H]; h0 = c0 = 0."""
+def lstm_stack(seq: torch.Tensor, P: Dict[str, torch.Tensor], layers: int, drop: "Dropout" = None):
+    """seq [B, T, C] -> top-layer h_T [B, H]; h0 = c0 = 0 (drop: masks between layers)."""
     Bn, T, _ = seq.shape
     inp = seq
     for l in range(layers):
@@ -82,6 +147,8 @@ def lstm_stack(seq: torch.Tensor, P: Dict[str, torch.Tensor], layers: int):
             h = o * torch.tanh(c)
             outs.append(h)
         inp = torch.stack(outs, dim=1)
+        if drop is not None and l < layers - 1:
+            inp = drop.lstm(inp, l)
     return inp[:, -1]
 
 
@@ -98,11 +165,13 @@ def hybrid_forward(P: Dict[str, torch.Tensor], x: torch.Tensor, edge_index: torc
     return pred.view(N, dims.forecast_horizon, dims.output_channels).reshape(-1, dims.output_channels)
 
 
-def batched_forward(P, feats_list: Sequence[torch.Tensor], dims) -> List[torch.Tensor]:
+def batched_forward(P, feats_list: Sequence[torch.Tensor], dims, drop: "Dropout" = None) -> List[torch.Tensor]:
     """Same as ``hybrid_forward`` for several samples at once (sequences stacked)."""
     T, N = dims.window_size, dims.num_nodes
     seq = torch.cat([f.view(T, N, -1).permute(1, 0, 2) for f in feats_list], dim=0)
-    hT = lstm_stack(seq, P, dims.lstm_num_layers)
+    hT = lstm_stack(seq, P, dims.lstm_num_layers, drop)
+    if drop is not None:
+        hT = drop.head(hT)
     pred = hT @ P["output_layer.weight"].t() + P["output_layer.bias"]
     pred = pred.view(len(feats_list), N * dims.forecast_horizon, dims.output_channels)
     return list(pred)
@@ -156,12 +225,16 @@ class TaskData:
 
 
 def batch_loss(Pt: Dict[str, torch.Tensor], Pg: Dict[str, torch.Tensor], task: TaskData,
-               idx: Sequence[int]):
+               idx: Sequence[int], drop: "Dropout" = None):
     """Mean over the B samples of the per-sample MSE (SURVEY F9 definition)."""
     P = dict(Pg)
     P.update(Pt)
-    feats = [task.gcn(i, Pg) for i in idx]
-    preds = batched_forward(P, feats, task.dims)
+    if drop is None:
+        feats = [task.gcn(i, Pg) for i in idx]
+    else:
+        with torch.no_grad():
+            feats = [stgcn_features(task.xy(i)[0], task.edge_index, Pg, drop, b, len(idx)) for b, i in enumerate(idx)]
+    preds = batched_forward(P, feats, task.dims, drop)
     losses = torch.stack([mse(p, task.xy(i)[1]) for p, i in zip(preds, idx)])
     return losses.mean(), preds
 
@@ -173,13 +246,15 @@ def support_schedule(step: int, batch: int, support: int) -> List[int]:
 
 
 def inner_loop(Pt, Pg, task: TaskData, steps: int, batch: int, support: int, lr: float,
-               max_norm: float, create_graph: bool = False, record=None):
+               max_norm: float, create_graph: bool = False, record=None, dropout=None):
+    """dropout = (seed, p_gcn, p_lstm, global task id) or None."""
     names = list(Pt.keys())
     params = [Pt[k] for k in names]
     for k in range(steps):
         idx = support_schedule(k, batch, support)
         cur = dict(zip(names, params))
-        loss, _ = batch_loss(cur, Pg, task, idx)
+        drop = Dropout(dropout[0], dropout[1], dropout[2], dropout[3], k) if dropout else None
+        loss, _ = batch_loss(cur, Pg, task, idx, drop)
         grads = torch.autograd.grad(loss, params, create_graph=create_graph)
         coef, total = clip_coef(grads, max_norm)
         if record is not None:
@@ -192,18 +267,22 @@ def inner_loop(Pt, Pg, task: TaskData, steps: int, batch: int, support: int, lr:
 
 def meta_step(Pt0: Dict[str, torch.Tensor], Pg, tasks: Sequence[TaskData], query_idx,
               steps: int, batch: int, support: int, lr: float, max_norm: float,
-              order: int, query_scale: float = 0.5):
+              order: int, query_scale: float = 0.5, dropout=None, task_ids=None):
     """Returns dict(meta_loss, query_losses, meta_grad (per name, summed over tasks),
-    step_records, adapted (per task))."""
+    step_records, adapted (per task)). dropout = (seed, p_gcn, p_lstm): masks of inner step k
+    keyed (seed, task_ids[j], k), the query batch's (seed, task_ids[j], steps)."""
     names = list(Pt0.keys())
     meta_grad = {k: torch.zeros_like(v) for k, v in Pt0.items()}
     qlosses, records, adapted_all = [], [], []
-    for task in tasks:
+    for j, task in enumerate(tasks):
         theta0 = [Pt0[k].detach().clone().requires_grad_(True) for k in names]
         rec = []
+        tid = task_ids[j] if task_ids is not None else j
+        dk = (dropout[0], dropout[1], dropout[2], tid) if dropout else None
         adapted = inner_loop(dict(zip(names, theta0)), Pg, task, steps, batch, support, lr,
-                             max_norm, create_graph=(order == 2), record=rec)
-        qloss, _ = batch_loss(adapted, Pg, task, query_idx)
+                             max_norm, create_graph=(order == 2), record=rec, dropout=dk)
+        qdrop = Dropout(dropout[0], dropout[1], dropout[2], tid, steps) if dropout else None
+        qloss, _ = batch_loss(adapted, Pg, task, query_idx, qdrop)
         scaled = qloss * query_scale
         if order == 2:
             g = torch.autograd.grad(scaled, theta0)

@@ -397,3 +397,58 @@ def test_task_groups_match_one_pass(order):
     assert rel(out[1][0], out[0][0]) < 1e-6
     assert rel(out[1][1], out[0][1]) < 1e-6
     assert rel(out[1][2], out[0][2]) < 1e-6
+
+
+# ----------------------------------------------------------------------------- dropout
+@pytest.mark.parametrize("order", [1, 2])
+def test_dropout_matches_oracle(order):
+    """Train-mode dropout at the reference's training rates (STGCN dropout_rate 0.2 after
+    conv1-3, lstm_dropout 0.2 between LSTM layers and on the head input), with the HIP path's
+    counter-based masks restated in the oracle: per-step losses, query MSE, meta-gradient
+    (first and second order: the sweep must reuse each step's masks)."""
+    d = CONFIG1
+    cfg = MamlConfig(inner_steps=2, batch=2, order=order)
+    P = synth.init_params(11, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1500 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2)]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, dropout=(0.2, 0.2), dropout_seed=5)
+    ml.set_tasks(feats, task_ids=[3, 7])
+    res = ml.meta_step()
+    seed = (5 * 1000003 + 1) & 0xFFFFFFFF  # MetaLearner's seed of its first meta-step
+    PT = refcpu.to_torch(P)
+    S = cfg.inner_steps * cfg.batch
+    ref = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
+                           [refcpu.TaskData(f, ei, d) for f in feats], list(range(S, S + cfg.batch)),
+                           cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, order,
+                           dropout=(seed, 0.2, 0.2), task_ids=[3, 7])
+    losses = res.losses.cpu().numpy()
+    for j in range(2):
+        steps = [r[0] for r in ref["step_records"][j]]
+        assert rel(losses[:cfg.inner_steps, j], steps) < 1e-5
+        assert abs(losses[-1, j] - ref["query_losses"][j]) < 1e-5 * ref["query_losses"][j]
+    mg = params.unpack(ml.meta_grad, d, 0)
+    for k in names:
+        assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
+    # the masks matter: without dropout the losses differ
+    ml0 = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml0.set_tasks(feats)
+    assert not np.allclose(ml0.meta_step().losses.cpu().numpy(), losses, rtol=1e-3)
+
+
+def test_dropout_masks_follow_task_ids_not_groups():
+    """A task's masks are keyed by its global id: running the tasks in groups of one gives the
+    one-pass losses under dropout."""
+    d = CONFIG1
+    cfg = MamlConfig(inner_steps=2, batch=2, order=2)
+    P = synth.init_params(12, d)
+    theta, gcn, _ = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1600 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(3)]
+    out = []
+    for g in (None, 1):
+        ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=g, dropout=(0.3, 0.2), dropout_seed=9)
+        ml.set_tasks(feats, task_ids=[10, 11, 12])
+        out.append((ml.meta_step().losses.cpu().numpy(), ml.meta_grad.cpu().numpy()))
+    assert rel(out[1][0], out[0][0]) < 1e-6
+    assert rel(out[1][1], out[0][1]) < 1e-5

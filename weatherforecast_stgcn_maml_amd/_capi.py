@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SMAML_LIB") or os.path.join(HERE, "libsmaml.so")
 EXPORTS = (
     "smaml_last_error", "smaml_abi_version", "smaml_param_layout", "smaml_graph_ell",
     "smaml_create", "smaml_destroy", "smaml_set_graph", "smaml_set_gcn_params", "smaml_reserve",
-    "smaml_workspace_bytes", "smaml_so_kept_steps", "smaml_gcn_conv", "smaml_forward", "smaml_set_tasks",
+    "smaml_workspace_bytes", "smaml_so_kept_steps", "smaml_set_dropout", "smaml_set_task_ids", "smaml_gcn_conv", "smaml_forward", "smaml_set_tasks",
     "smaml_meta_step", "smaml_adamw_step", "smaml_adapt_steps", "smaml_timing", "smaml_timing_collect",
     "smaml_backward", "smaml_gcn_forward", "smaml_lstm_forward", "smaml_lstm_backward", "smaml_head_loss",
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
@@ -74,6 +74,8 @@ _SIGS = {
     "smaml_reserve": ([P, I32, I32], I32),
     "smaml_workspace_bytes": ([P], I64),
     "smaml_so_kept_steps": ([P], I32),
+    "smaml_set_dropout": ([P, ctypes.c_float, ctypes.c_float, ctypes.c_uint32], I32),
+    "smaml_set_task_ids": ([P, PI32, I32], I32),
     "smaml_gcn_conv": ([P, P, P, I32, I32, P, P, I32, P], I32),
     "smaml_forward": ([P, P, P, ctypes.POINTER(P), I32, P, P], I32),
     "smaml_set_tasks": ([P, I32, ctypes.POINTER(P), PI32], I32),
@@ -209,6 +211,13 @@ class Context:
 
     def so_kept_steps(self):
         return int(self._L.smaml_so_kept_steps(self._h))
+
+    def set_dropout(self, p_gcn, p_lstm, seed):
+        check(self._L.smaml_set_dropout(self._h, float(p_gcn), float(p_lstm), int(seed) & 0xFFFFFFFF))
+
+    def set_task_ids(self, ids):
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        check(self._L.smaml_set_task_ids(self._h, a.ctypes.data_as(PI32), a.size))
 
     # --- compute
     def gcn_conv(self, stream, x, weight, bias, out):

@@ -197,6 +197,11 @@ struct smaml_ctx {
   int64_t keep_rows = 0;  // rows * L the slots were sized for
   int keep_tried_K = -1;
   int keep_last = 0;  // slots the last second-order meta-step used
+  // train-mode dropout (smaml_set_dropout / smaml_set_task_ids); p = 0: off
+  float p_gcn = 0.f, p_lstm = 0.f;
+  uint32_t drop_seed = 0;
+  std::vector<int32_t> task_ids;  // global id of each task of smaml_set_tasks (default: its index)
+  int* task_id_dev = nullptr;     // [z_cap] (arena)
   int64_t keep_tried_rows = -1;
   // activations of the last smaml_forward / smaml_lstm_forward (single task, act_B samples);
   // -1 once anything else has used the workspace (the backward consumes them: dG in place)
@@ -254,6 +259,9 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   parts.push_back({(void**)&w.wpart, wpart * 4});
   parts.push_back({(void**)&w.lpart, lblk * 4});
   parts.push_back({(void**)&w.sqpart, (int64_t)(zc + 1) * SQB * 8});
+  parts.push_back({(void**)&w.hTd, seq * d.H * 4});
+  int* task_id_dev = nullptr;
+  parts.push_back({(void**)&task_id_dev, (int64_t)zc * 4});
   float *fast = nullptr, *grad = nullptr;
   parts.push_back({(void**)&fast, (int64_t)zc * c->po.P * 4});
   parts.push_back({(void**)&grad, (int64_t)zc * c->po.P * 4});
@@ -265,6 +273,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
     parts.push_back({(void**)&w.RdH, seq * d.H * 4});
     parts.push_back({(void**)&w.Rdc, seq * d.L * d.H * 4});
     parts.push_back({(void**)&w.Rdpred, seq * d.HfC * 4});
+    parts.push_back({(void**)&w.RhTd, seq * d.H * 4});
     parts.push_back({(void**)&so_u, (int64_t)zc * c->po.P * 4});
     parts.push_back({(void**)&so_hu, (int64_t)zc * c->po.P * 4});
   }
@@ -294,6 +303,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   c->arena = arena;
   c->arena_bytes = total;
   c->w = w;
+  c->task_id_dev = task_id_dev;
   c->fast = fast;
   c->grad = grad;
   c->zb_cap = zbc;
@@ -415,6 +425,28 @@ void use_primal(smaml_ctx* c, int slot) {
   }
 }
 
+// Dropout masks of one forward pass (inner step / query `step`) for the Z tasks of the workspace.
+int upload_task_ids(smaml_ctx* c, hipStream_t s, int Z) {
+  std::vector<int32_t> ids(Z);
+  for (int z = 0; z < Z; ++z) ids[z] = z < (int)c->task_ids.size() ? c->task_ids[z] : z;
+  HIP_TRY(hipMemcpyAsync(c->task_id_dev, ids.data(), (size_t)Z * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));  // ids is a stack buffer
+  return SMAML_OK;
+}
+
+void set_step_drop(smaml_ctx* c, int step) {
+  Drop dr{};
+  auto thr = [](float p) { return (uint32_t)std::min<double>(std::llround((double)p * 16777216.0), 16777216.0); };
+  dr.seed = c->drop_seed;
+  dr.step = step;
+  dr.thr_gcn = thr(c->p_gcn);
+  dr.thr_lstm = thr(c->p_lstm);
+  dr.sc_gcn = 1.f / (1.f - c->p_gcn);
+  dr.sc_lstm = 1.f / (1.f - c->p_lstm);
+  dr.task_id = c->task_id_dev;
+  c->w.drop = dr;
+}
+
 int ensure_xtab(smaml_ctx* c, int64_t n) {
   if (n <= c->xtab_cap) return SMAML_OK;
   if (c->xtab) {
@@ -446,6 +478,7 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.lblocks = (c->w.M + 127) / 128;
   c->w.F = c->F_main;
   c->w.primal_kept = 0;
+  c->w.drop = Drop{};  // dropout only inside smaml_meta_step / smaml_adapt_steps (set_step_drop)
   if (c->Hs_main) use_primal(c, SET_MAIN);
 }
 
@@ -466,10 +499,12 @@ void set_work(smaml_ctx* c, int Z, int B) {
 void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t a_zstride, int Mrows,
                  const float* B1, int64_t b1_zstride, int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K,
                  int Mshift, float* grad, int64_t P, int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2,
-                 bool with_bias = true, bool accumulate = false) {
+                 bool with_bias = true, bool accumulate = false, int drop_layer = -1) {
   WgradPlan p;
   plan_wgrad(c->w, A, a_zstride, Mrows, B1, b1_zstride, c1, B2, b2_zstride, c2, K, Mshift, grad, P, off_w1, off_w2,
              off_b1, off_b2, with_bias, accumulate, p);
+  p.drop = c->w.drop;  // B1 = drop(h_{drop_layer}) under LSTM dropout (input weights of layer >= 1)
+  p.drop_layer = drop_layer;
   TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
 }
@@ -488,7 +523,7 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
     TIMED(c, s, C_GCN, 2.0 * zb * rps * c->go.cin[k] * d.Hc,
           launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
                            c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
-                           rps, d.N));
+                           rps, d.N, &w.drop));
     src = dst;
   }
   HIP_TRY(hipGetLastError());
@@ -523,9 +558,10 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
   TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
-  const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
-  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, top + (int64_t)(d.T - 1) * w.M * d.H,
-                     TM * d.H, d.H, nullptr, 0, 0, w.M, 0, grad, po.P, po.wo, -1, po.bo, -1);
+  int64_t hz = 0;
+  const float* hT = head_input(d, w, false, &hz);  // h_T, or drop(h_T) under dropout
+  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, hT, hz, d.H, nullptr, 0, 0,
+                     w.M, 0, grad, po.P, po.wo, -1, po.bo, -1);
   return run_bptt(c, s, theta, tstride, grad);
 }
 
@@ -547,7 +583,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
                        w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
-                       lo.bhh);
+                       lo.bhh, true, false, l - 1);
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -568,7 +604,7 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
     TIMED(c, s, C_GCN, 2.0 * zb * rps * c->go.cin[k] * d.Hc,
           launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
                            c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
-                           rps, d.N));
+                           rps, d.N, &w.drop));
     src = dst;
   }
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
@@ -589,10 +625,12 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
   TIMED(c, s, C_HEAD_DH, 3.0 * 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh_dual(s, d, w, theta, U, tstride, po));
-  const int64_t toff = (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
-  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.Rdpred, (int64_t)w.M * d.HfC, d.HfC, w.Hs + toff, TM * d.H, d.H, nullptr, 0, 0,
+  int64_t hz = 0;
+  const float* hT = head_input(d, w, false, &hz);
+  const float* RhT = head_input(d, w, true, &hz);
+  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.Rdpred, (int64_t)w.M * d.HfC, d.HfC, hT, hz, d.H, nullptr, 0, 0,
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false);
-  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, w.RHs + toff, TM * d.H, d.H, nullptr, 0, 0,
+  timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, RhT, hz, d.H, nullptr, 0, 0,
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true);
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
@@ -606,10 +644,10 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
-                       TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false);
+                       TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false, l - 1);
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
                        w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh,
-                       false, true);
+                       false, true, l - 1);
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -774,6 +812,22 @@ int64_t smaml_workspace_bytes(const smaml_ctx* c) { return c ? c->arena_bytes : 
 
 int32_t smaml_so_kept_steps(const smaml_ctx* c) { return c ? c->keep_last : 0; }
 
+int smaml_set_dropout(smaml_ctx* c, float p_gcn, float p_lstm, uint32_t seed) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  if (!(p_gcn >= 0.f && p_gcn < 1.f) || !(p_lstm >= 0.f && p_lstm < 1.f))
+    return fail(SMAML_EINVAL, "dropout probabilities must lie in [0, 1)");
+  c->p_gcn = p_gcn;
+  c->p_lstm = p_lstm;
+  c->drop_seed = seed;
+  return SMAML_OK;
+}
+
+int smaml_set_task_ids(smaml_ctx* c, const int32_t* ids_host, int32_t n) {
+  if (!c || n < 0 || (n > 0 && !ids_host)) return fail(SMAML_EINVAL, "bad set_task_ids arguments");
+  c->task_ids.assign(ids_host, ids_host + n);
+  return SMAML_OK;
+}
+
 int smaml_gcn_conv(smaml_ctx* c, void* stream, const float* x, int32_t rows, int32_t cin, const float* weight,
                    const float* bias, int32_t cout, float* out) {
   if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
@@ -874,11 +928,14 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   }
   const int64_t P = c->po.P;
   const float inv = 1.f / ((float)d.N * d.HfC * B);
+  const bool dropout = c->p_gcn > 0.f || c->p_lstm > 0.f;
+  if (dropout) TRY(upload_task_ids(c, s, Z));
   launch_broadcast(s, theta, P, Z, c->fast);
   const double head_fl = 2.0 * Z * c->w.M * d.HfC * d.H;
   const bool so = order == 2;
   for (int k = 0; k < steps; ++k) {
     const float* const* xt = c->xtab + (int64_t)k * Z * B;
+    if (dropout) set_step_drop(c, k);
     if (so) {
       HIP_TRY(hipMemcpyAsync(c->so_theta + (int64_t)k * Z * P, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
       c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
@@ -906,6 +963,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const float* const* xq = c->xtab + (int64_t)steps * Z * B;
   c->w.F = c->F_main;
   use_primal(c, nkeep > 0 ? SET_QUERY : SET_MAIN);  // slot 0 holds the workspace's own Hs/Cs/Gs
+  if (dropout) set_step_drop(c, steps);
   TRY(run_forward(c, s, c->fast, P, xq));
   TIMED(c, s, C_HEAD, head_fl,
         launch_head_loss(s, d, c->w, c->fast, P, c->po, xq, 2.f * inv * query_scale, true));
@@ -932,6 +990,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       const int slot = steps - 1 - k;
       use_primal(c, slot < nkeep ? slot : SET_MAIN);
       c->w.primal_kept = slot < nkeep ? 1 : 0;
+      if (dropout) set_step_drop(c, k);  // the masks of inner step k's forward
       TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
@@ -943,6 +1002,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     c->w.F = c->F_main;
   }
   if (fast_out) HIP_TRY(hipMemcpyAsync(fast_out, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
+  c->w.drop = Drop{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -970,8 +1030,11 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
   TRY(upload_xtab(c, s, ptrs.data(), nptr));
   const int64_t P = c->po.P;
   const float inv = 1.f / ((float)d.N * d.HfC * B);
+  const bool dropout = c->p_gcn > 0.f || c->p_lstm > 0.f;
+  if (dropout) TRY(upload_task_ids(c, s, 1));
   for (int k = 0; k < nsteps; ++k) {
     const float* const* xt = c->xtab + (int64_t)k * B;
+    if (dropout) set_step_drop(c, step0 + k);
     TRY(run_forward(c, s, theta, 0, xt));
     launch_head_loss(s, d, c->w, theta, 0, c->po, xt, 2.f * inv, true);
     launch_loss_final(s, c->w, inv, losses + k);
@@ -979,6 +1042,7 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
                    weight_decay, max_norm);
   }
+  c->w.drop = Drop{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }

@@ -39,6 +39,38 @@ struct GcnOff {
   int64_t total;
 };
 
+// Train-mode dropout (hybrid_model.py:67,70,73 GCN outputs; nn.LSTM's inter-layer dropout :47;
+// the head input :108) from counter-based masks: element idx of site (kind, step, layer) is
+// kept iff (mix32(site ^ mix32(lo(idx) ^ mix32(hi(idx) + golden))) >> 8) >= thr, and scaled by
+// 1 / (1 - p). oracle/refcpu.py (drop_keep) restates the same function, so the masks agree
+// bit for bit. Element indices (task = global task id):
+//   kind 1, layer k (GCN conv k+1 output): ((task * B + s) * T*N + row) * Hc + channel
+//   kind 2, layer l (LSTM layer l output fed to layer l+1): ((task * T + t) * M + m) * H + unit
+//   kind 3 (head input h_T): (task * M + m) * H + unit
+__host__ __device__ inline uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ inline uint32_t drop_site(uint32_t seed, int kind, int step, int layer) {
+  return mix32(seed ^ mix32(((uint32_t)kind << 24) ^ ((uint32_t)step << 8) ^ (uint32_t)layer));
+}
+__host__ __device__ inline bool drop_keep(uint32_t site, uint64_t idx, uint32_t thr) {
+  return (mix32(site ^ mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) + 0x9E3779B9U))) >> 8) >= thr;
+}
+struct Drop {
+  uint32_t seed;
+  int step;                  // inner step (K = the query batch) whose forward the masks belong to
+  uint32_t thr_gcn, thr_lstm;  // round(p * 2^24); 0 = off
+  float sc_gcn, sc_lstm;     // 1 / (1 - p)
+  const int* task_id;        // [Z] global task id of each workspace task (device)
+  __host__ __device__ bool gcn() const { return thr_gcn != 0; }
+  __host__ __device__ bool lstm() const { return thr_lstm != 0; }
+};
+
 // Activations of one forward pass for Z tasks x B samples (M = B*N sequences per task).
 struct Work {
   int Z, B, M;
@@ -61,6 +93,9 @@ struct Work {
   float *RHs, *RCs, *RGs;  // like Hs, Cs, Gs
   float *RdH, *Rdc;        // like dH, dc (R(dG) is written in place over RGs)
   float* Rdpred;           // like dpred
+  // dropout (zero thresholds: off) and the masked head inputs drop(h_T), drop(R h_T) [Z][M][H]
+  Drop drop;
+  float *hTd, *RhTd;
 };
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
@@ -94,7 +129,7 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
                       const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
                       const float* b, int cin, int cout, const int* ell_c, const float* ell_v, int rows_per_sample,
-                      int ell_rows);
+                      int ell_rows, const Drop* drop = nullptr);
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
@@ -102,6 +137,10 @@ void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* 
 void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float* hT, const float* theta,
                         const ParamOff& po, const float* const* ytab, float* pred, float* dpred, float dscale);
 void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
+// dst[z] = drop(src[z]) with the head-input mask ([M][H] rows per task; src == dst allowed)
+void launch_drop_rows(hipStream_t s, const Work& w, int H, const float* src, int64_t src_zstride, float* dst);
+// rows the head reads: h_T (or R h_T) of the top layer, or their dropout-masked copies
+const float* head_input(const Dims& d, const Work& w, bool tangent, int64_t* zstride);
 void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                     const ParamOff& po);
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
@@ -128,6 +167,8 @@ struct WgradPlan {
   float* part;
   int ldp, ntm, ntn, nsplit;
   int64_t kchunk;
+  Drop drop;       // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
+  int drop_layer;
 };
 void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
                 int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,

@@ -104,7 +104,8 @@ using CfgGcn = GemmCfg<128, 256, 2, 4, true, true, SMAML_GCN_BK>;
 
 __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
                                                            float* __restrict__ out, int cout, int remap, int relu,
-                                                           int T, int N, int B, FastDiv ndiv, FastDiv bdiv) {
+                                                           int T, int N, int B, FastDiv ndiv, FastDiv bdiv, Drop dr,
+                                                           uint32_t dsite) {
   __shared__ float smem[CfgGcn::SMEM_FLOATS];
   const int m0 = blockIdx.x * CfgGcn::BM, n0 = blockIdx.y * CfgGcn::BN;
   Acc<CfgGcn> acc;
@@ -130,6 +131,12 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
     for (int r = 0; r < 16; ++r) {
       const int row = m0 + acc_row<CfgGcn>(i, r);
       if (row >= la.R) continue;
+      uint64_t didx = 0;  // dropout element index of (row, column 0)
+      if (dr.gcn()) {
+        const int g = (int)la.rps_div.div((uint32_t)row), q = row - g * la.rps;
+        const int z = (int)bdiv.div((uint32_t)g), s = g - z * B;
+        didx = (((uint64_t)dr.task_id[z] * B + s) * la.rps + q) * cout;
+      }
       int64_t orow = row;
       if (remap) {  // [g][t*N+n] -> [z][t][s*N+n]
         const int g = (int)la.rps_div.div((uint32_t)row), q = row - g * la.rps;
@@ -144,6 +151,7 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
         if (c >= cout) continue;
         float v = acc.v[i][j][r] + bc[j];
         if (relu) v = fmaxf(v, 0.f);
+        if (dr.gcn()) v = drop_keep(dsite, didx + c, dr.thr_gcn) ? v * dr.sc_gcn : 0.f;
         o[c] = v;
       }
     }
@@ -152,8 +160,14 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
                       const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
                       const float* b, int cin, int cout, const int* ell_c, const float* ell_v,
-                      int rows_per_sample, int ell_rows) {
-  (void)layer;
+                      int rows_per_sample, int ell_rows, const Drop* drop) {
+  // train-mode dropout after the ReLU of conv1..conv3 (hybrid_model.py:67,70,73)
+  Drop dr{};
+  uint32_t dsite = 0;
+  if (drop && drop->gcn() && layer < 3) {
+    dr = *drop;
+    dsite = drop_site(dr.seed, 1, dr.step, layer);
+  }
   GcnA la;
   la.tab = xtab;
   la.buf = src;
@@ -168,7 +182,7 @@ void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, co
   RowMajorKC lb{W, cout, cin};
   dim3 grid((la.R + CfgGcn::BM - 1) / CfgGcn::BM, (cout + CfgGcn::BN - 1) / CfgGcn::BN);
   k_gcn_layer<<<grid, CfgGcn::NTH, 0, s>>>(la, lb, b, dst, cout, remap_lstm ? 1 : 0, relu ? 1 : 0, d.T, d.N, B,
-                                           FastDiv((uint32_t)d.N), FastDiv((uint32_t)B));
+                                           FastDiv((uint32_t)d.N), FastDiv((uint32_t)B), dr, dsite);
 }
 
 // ====================================================================================
@@ -176,14 +190,15 @@ void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, co
 //   pre[m, g*H+j] = [x_t | h_{t-1}][m] . [W_ih | W_hh][g*H+j] + b_ih + b_hh
 // Column tile = 32 hidden units x 4 gates, so each lane holds i,f,g,o of the same
 // (row, unit) in the same accumulator register and the cell update is in-register.
-template <int H>
+template <int H, bool DROP = false>
 struct LstmFwdA {
   const float* X;   // layer input at time t: [M][cin]
   const float* Hp;  // h_{t-1}: [M][H] (nullptr at t = 0)
   int M, cin;
+  XDrop d;          // DROP: x = drop(h_{l-1})
   __device__ __forceinline__ float4 operator()(int m, int k) const {
     if (m >= M) return f4zero();
-    if (k < cin) return ld4(X + (int64_t)m * cin + k);
+    if (k < cin) return DROP ? d.apply(ld4(X + (int64_t)m * cin + k), m, k) : ld4(X + (int64_t)m * cin + k);
     k -= cin;
     if (!Hp || k >= H) return f4zero();
     return ld4(Hp + (int64_t)m * H + k);
@@ -207,11 +222,11 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 };
 
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
-template <int H>
+template <int H, bool DROP>
 __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                                       float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      FwdWave wv, int T, int M) {
+                                                      FwdWave wv, int T, int M, Drop dr) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
   int l, t, b0;
   LayerOff lo;
@@ -227,11 +242,7 @@ __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(
   float* Gz = Gs + slab * (4 * H);
   float* Cz = Cs + slab * H;
   float* Hz = Hs + slab * H;
-  LstmFwdA<H> la;
-  la.X = X + (slab + (int64_t)t * M) * cin;
-  la.Hp = t > 0 ? Hz + (int64_t)(t - 1) * M * H : nullptr;
-  la.M = M;
-  la.cin = cin;
+  const float* Hp = t > 0 ? Hz + (int64_t)(t - 1) * M * H : nullptr;
   LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
   int tm, ug;
   constexpr int UPB = CfgGate::WAVES_N;  // 32-unit groups per workgroup
@@ -240,7 +251,16 @@ __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(
   const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
   acc.zero();
-  gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+  if (DROP && l > 0) {
+    // nn.LSTM inter-layer dropout: layer l reads drop(h_{l-1, t})
+    const XDrop xd{drop_site(dr.seed, 2, dr.step, l - 1), dr.thr_lstm, dr.sc_lstm,
+                   ((uint64_t)dr.task_id[z] * T + t) * M * H, H};
+    LstmFwdA<H, true> la{X + (slab + (int64_t)t * M) * cin, Hp, M, cin, xd};
+    gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+  } else {
+    LstmFwdA<H> la{X + (slab + (int64_t)t * M) * cin, Hp, M, cin, XDrop{}};
+    gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+  }
 
   const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
   if (j >= H) return;
@@ -307,8 +327,13 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   if (flops) *flops = fl;
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
-                                                                           wv, d.T, w.M));
+  if (w.drop.lstm()) {
+    SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT, true><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
+                                                                                   tstride, wv, d.T, w.M, w.drop));
+    return;
+  }
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT, false><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
+                                                                           wv, d.T, w.M, w.drop));
 }
 
 // ====================================================================================
@@ -365,14 +390,47 @@ __global__ __launch_bounds__(NT) void k_head_loss(const float* __restrict__ hT_b
   }
 }
 
+// dst[z][m][j] = drop(src[z][m][j]) with the head-input mask (kind 3; hybrid_model.py:108):
+// h_T -> drop(h_T), R h_T -> drop(R h_T), and in place on dh_T / R dh_T.
+__global__ void k_drop_rows(const float* src, int64_t src_zstride, float* dst, int M, int H, Drop dr) {
+  const int z = blockIdx.y;
+  const uint32_t site = drop_site(dr.seed, 3, dr.step, 0);
+  const int64_t n = (int64_t)M * H;
+  const uint64_t base = (uint64_t)dr.task_id[z] * (uint64_t)n;
+  const float* sz = src + (int64_t)z * src_zstride;
+  float* dz = dst + (int64_t)z * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dz[i] = drop_keep(site, base + i, dr.thr_lstm) ? sz[i] * dr.sc_lstm : 0.f;
+}
+
+void launch_drop_rows(hipStream_t s, const Work& w, int H, const float* src, int64_t src_zstride, float* dst) {
+  const int64_t n = (int64_t)w.M * H;
+  int nb = (int)((n + NT - 1) / NT);
+  if (nb > 1024) nb = 1024;
+  k_drop_rows<<<dim3(nb, w.Z), NT, 0, s>>>(src, src_zstride, dst, w.M, H, w.drop);
+}
+
+// The head's input rows: h_T of the top layer (z stride T*M*H), or drop(h_T) under dropout.
+const float* head_input(const Dims& d, const Work& w, bool tangent, int64_t* zstride) {
+  if (w.drop.lstm()) {
+    *zstride = (int64_t)w.M * d.H;
+    return tangent ? w.RhTd : w.hTd;
+  }
+  *zstride = (int64_t)d.T * w.M * d.H;
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  return (tangent ? w.RHs : w.Hs) + (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
+}
+
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                       const ParamOff& po, const float* const* xtab, float dscale, bool want_loss) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   const float* top = w.Hs + (int64_t)(d.L - 1) * lsz;
-  const float* hT = top + (int64_t)(d.T - 1) * w.M * d.H;  // z stride T*M*H
+  if (w.drop.lstm()) launch_drop_rows(s, w, d.H, top + (int64_t)(d.T - 1) * w.M * d.H, (int64_t)d.T * w.M * d.H, w.hTd);
+  int64_t hz = 0;
+  const float* hT = head_input(d, w, false, &hz);
   dim3 grid((w.M + CfgNT::BM - 1) / CfgNT::BM, 1, w.Z);
   // targets from the feature stream: rows T+1 .. T+Hf after the window start, first C channels (F5)
-  k_head_loss<<<grid, NT, 0, s>>>(hT, (int64_t)d.T * w.M * d.H, theta, tstride, po.wo, po.bo,
+  k_head_loss<<<grid, NT, 0, s>>>(hT, hz, theta, tstride, po.wo, po.bo,
                                   want_loss ? xtab : nullptr, w.pred, want_loss ? w.dpred : nullptr,
                                   want_loss ? w.lpart : nullptr, w.lblocks, w.M, d.H, d.HfC, d.N, d.Hf,
                                   d.C, d.T + 1, d.Cin0, w.B, dscale);
@@ -436,6 +494,7 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
   dim3 grid((w.M + CfgNN::BM - 1) / CfgNN::BM, (d.H + CfgNN::BN - 1) / CfgNN::BN, w.Z);
   k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(w.dpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, tstride, po.wo, d.H,
                                 w.dH, (int64_t)w.M * d.H);
+  if (w.drop.lstm()) launch_drop_rows(s, w, d.H, w.dH, (int64_t)w.M * d.H, w.dH);  // d drop(h_T) -> d h_T
 }
 
 // ====================================================================================
@@ -476,12 +535,14 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 
 // GsAll: gates in; dGAll: dG out (== GsAll: in place) and the neighbours' dG read by the GEMM;
 // dhAll (optional): the step's dh kept for the second-order sweep ([L][Z][T][M][H]).
-template <int H, class CfgNN>
+// DROP: the layer-above segment carries dX of layer l+1's input drop(h_l): its contribution
+// is masked before the recurrent segment accumulates (two mainloops instead of one).
+template <int H, class CfgNN, bool DROP>
 __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(const float* GsAll, float* dGAll,
                                                       float* __restrict__ dhAll, const float* __restrict__ CsAll,
                                                       const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      BwdWave wv, int L, int T, int M) {
+                                                      BwdWave wv, int L, int T, int M, Drop dr) {
   __shared__ float smem[CfgNN::SMEM_FLOATS];
   constexpr int G4 = 4 * H;
   const int p = wave_index(wv, (int)blockIdx.x);
@@ -505,9 +566,20 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
     const float* pa = dGAll + (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
     const float* pn = dGz + (int64_t)(t + 1) * M * G4;
     const int ns = (up ? 1 : 0) + (nx ? 1 : 0);
-    SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
-    SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
-    if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
+    if (DROP && up) {
+      const XDrop xd{drop_site(dr.seed, 2, dr.step, l), dr.thr_lstm, dr.sc_lstm,
+                     ((uint64_t)dr.task_id[z] * T + t) * M * H, H};
+      gemm_mainloop<CfgNN>(SegKC{{pa, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
+                           SegMC{{th + wih_up, nullptr}, {G4, 0}, H}, m0, n0, 0, G4, acc, smem);
+      drop_acc<CfgNN>(acc, xd, m0, n0);
+      if (nx)
+        gemm_mainloop<CfgNN>(SegKC{{pn, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
+                             SegMC{{th + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, 0, G4, acc, smem);
+    } else {
+      SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
+      SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
+      if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
+    }
   }
   const bool first = (t == T - 1);
   const bool head = first && l == L - 1;
@@ -553,17 +625,27 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
   const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
+#define SMAML_BWD_STEP(CFG, D_)                                                                               \
+  SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
+                            w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
   if ((int64_t)wv.n * ntm * ntn * w.Z >= SMAML_BWD_BIG_MIN) {
     dim3 grid(wv.off[wv.n], ntn, w.Z);
-    SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgBwd><<<grid, CfgBwd::NTH, 0, s>>>(
-                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
+    if (w.drop.lstm()) {
+      SMAML_BWD_STEP(CfgBwd, true);
+    } else {
+      SMAML_BWD_STEP(CfgBwd, false);
+    }
   } else {
     const int ntms = (w.M + CfgNNs::BM - 1) / CfgNNs::BM, ntns = (d.H + CfgNNs::BN - 1) / CfgNNs::BN;
     bwd_wave(d, w, po, e, ntms, false, wv);
     dim3 grid(wv.off[wv.n], ntns, w.Z);
-    SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
-                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M));
+    if (w.drop.lstm()) {
+      SMAML_BWD_STEP(CfgNNs, true);
+    } else {
+      SMAML_BWD_STEP(CfgNNs, false);
+    }
   }
+#undef SMAML_BWD_STEP
 }
 
 // ====================================================================================
@@ -584,10 +666,23 @@ struct ColSumHook {
   }
 };
 
+// B1 = drop(h_{l-1}) for the input weights of LSTM layer l >= 1 under dropout: row k of the
+// task's [T*M][H] slab is element (task * T*M + k) * H + unit of kind 2, layer l-1.
+struct WgBDrop {
+  WgB b;
+  XDrop d;
+  __device__ __forceinline__ float4 operator()(int64_t k, int j) const {
+    if (k >= b.K) return f4zero();
+    if (j < b.c1) return b.B1 ? d.apply(ld4(b.B1 + k * b.c1 + j), (int)k, j) : f4zero();
+    return b(k, j);
+  }
+};
+
+template <bool DROP>
 __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
                                               int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
-                                              int ldp, int with_bias) {
+                                              int ldp, int with_bias, Drop dr, int drop_layer) {
   __shared__ float smem[CfgTN::SMEM_FLOATS];
   // XCD-aware: the ntile output tiles of one (split, task) group stream the same K rows of
   // A and B, so they are placed on one XCD (blocks 8 apart) to share its L2. Speed only.
@@ -608,7 +703,16 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
   float bsum = 0.f;
   // k indices exceed int range only in the loaders (int64 there); the mainloop
   // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
-  if (tn == 0 && with_bias) {
+  if (DROP) {
+    const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
+                              (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
+    if (tn == 0 && with_bias) {
+      ColSumHook hook{&bsum};
+      gemm_mainloop<CfgTN>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    } else {
+      gemm_mainloop<CfgTN>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    }
+  } else if (tn == 0 && with_bias) {
     ColSumHook hook{&bsum};
     gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
@@ -718,8 +822,14 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
   const int ntile = p.ntm * p.ntn;
   const int ngroups = p.nsplit * p.Z;
   dim3 grid((unsigned)(((ngroups + 7) / 8) * 8 * ntile));
-  k_wgrad<<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn, ntile,
-                              p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0);
+  if (p.drop_layer >= 0 && p.drop.lstm())
+    k_wgrad<true><<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk,
+                                              p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
+                                              p.drop, p.drop_layer);
+  else
+    k_wgrad<false><<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk,
+                                               p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
+                                               p.drop, -1);
 }
 
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p) {

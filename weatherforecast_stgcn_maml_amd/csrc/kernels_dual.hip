@@ -40,14 +40,15 @@ __device__ __forceinline__ float block_sum_f(float v, float* red) {
 // ====================================================================================
 // KEPT: the primal of this step (gates, c, h) is already in Hs / Cs / Gs (kept from the inner
 // step for the second-order sweep): only the tangent pass runs.
-template <int H, bool KEPT>
+// DROP: layers >= 1 read x = drop(h_{l-1}) and R x = drop(R h_{l-1}) (the same mask).
+template <int H, bool KEPT, bool DROP>
 __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
                                                       float* __restrict__ HsAll, float* __restrict__ CsAll,
                                                       float* __restrict__ GsAll, float* __restrict__ RHsAll,
                                                       float* __restrict__ RCsAll, float* __restrict__ RGsAll,
                                                       int64_t lsz, const float* __restrict__ theta,
                                                       const float* __restrict__ U, int64_t tstride, FwdWave wv,
-                                                      int T, int M) {
+                                                      int T, int M, Drop dr) {
   __shared__ float smem[CfgGateD::SMEM_FLOATS];
   constexpr int G4 = 4 * H;
   int l, t, b0;
@@ -83,6 +84,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
                  ug))
     return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
+  XDrop xd{};
+  if (DROP && l > 0)
+    xd = XDrop{drop_site(dr.seed, 2, dr.step, l - 1), dr.thr_lstm, dr.sc_lstm,
+               ((uint64_t)dr.task_id[z] * T + t) * M * H, H};
 
   // Register diet: the primal epilogue runs between the two passes (its accumulators die
   // there), and the tangent epilogue re-reads the gates / cell it needs from the lines this
@@ -97,7 +102,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     ap.zero();
     SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
-    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh, ap, smem);
+    if (DROP && l > 0)
+      gemm_mainloop<CfgGateD>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
+    else
+      gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh, ap, smem);
     if (j < H) {
       float bp[4];
 #pragma unroll
@@ -130,7 +138,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     const int wrx = rxt ? cin : 0;
     SegKC la{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M};
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
-    gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+    if (DROP && l > 0)
+      gemm_mainloop<CfgGateD>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+    else
+      gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
   }
   if (j >= H) return;
   float bu[4];
@@ -173,13 +184,21 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   if (flops) *flops = fl;
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
-  if (w.primal_kept) {
-    SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, true><<<grid, CfgGateD::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, d.T, w.M));
+  const bool kept = w.primal_kept != 0, drop = w.drop.lstm();
+#define SMAML_FWD_DUAL(K_, D_)                                                                  \
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, K_, D_><<<grid, CfgGateD::NTH, 0, s>>>(              \
+                            w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
+                            d.T, w.M, w.drop))
+  if (kept && drop) {
+    SMAML_FWD_DUAL(true, true);
+  } else if (kept) {
+    SMAML_FWD_DUAL(true, false);
+  } else if (drop) {
+    SMAML_FWD_DUAL(false, true);
   } else {
-    SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, false><<<grid, CfgGateD::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, d.T, w.M));
+    SMAML_FWD_DUAL(false, false);
   }
+#undef SMAML_FWD_DUAL
 }
 
 // ====================================================================================
@@ -236,8 +255,15 @@ void launch_head_dual(hipStream_t s, const Dims& d, const Work& w, const float* 
                       int64_t tstride, const ParamOff& po, const float* const* xtab, float dscale) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   const int64_t off = (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
+  if (w.drop.lstm()) {  // drop(h_T), R drop(h_T) = drop(R h_T)
+    launch_drop_rows(s, w, d.H, w.Hs + off, (int64_t)d.T * w.M * d.H, w.hTd);
+    launch_drop_rows(s, w, d.H, w.RHs + off, (int64_t)d.T * w.M * d.H, w.RhTd);
+  }
+  int64_t hz = 0;
+  const float* hT = head_input(d, w, false, &hz);
+  const float* RhT = head_input(d, w, true, &hz);
   dim3 grid((w.M + CfgNTD::BM - 1) / CfgNTD::BM, 1, w.Z);
-  k_head_dual<<<grid, NT, 0, s>>>(w.Hs + off, w.RHs + off, (int64_t)d.T * w.M * d.H, theta, U, tstride, po.wo,
+  k_head_dual<<<grid, NT, 0, s>>>(hT, RhT, hz, theta, U, tstride, po.wo,
                                   po.bo, xtab, w.dpred, w.Rdpred, w.M, d.H, d.HfC, d.N, d.Hf, d.C, d.T, d.Cin0, w.B,
                                   dscale);
 }
@@ -287,6 +313,10 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
   dim3 grid((w.M + CfgNND::BM - 1) / CfgNND::BM, (d.H + CfgNND::BN - 1) / CfgNND::BN, w.Z);
   k_gemm_nn_dual<<<grid, CfgNND::NTH, 0, s>>>(w.dpred, w.Rdpred, (int64_t)w.M * d.HfC, w.M, d.HfC, theta, U, tstride, po.wo,
                                      d.H, w.dH, w.RdH, (int64_t)w.M * d.H);
+  if (w.drop.lstm()) {  // back through drop(h_T): the same mask on dh_T and R dh_T
+    launch_drop_rows(s, w, d.H, w.dH, (int64_t)w.M * d.H, w.dH);
+    launch_drop_rows(s, w, d.H, w.RdH, (int64_t)w.M * d.H, w.RdH);
+  }
 }
 
 // ====================================================================================
@@ -302,7 +332,8 @@ using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, fal
 // dhAll): the GEMM forms only the tangent (R(dh) = A2 . B + A . B2), the primal cell backward is
 // re-derived elementwise from the kept dh, and only R(dG) and the carries are written.
 // Otherwise dGAll == GsAll (dG written in place over the gates) and dhAll is unused.
-template <int H, class CfgNND, bool KEPT>
+// DROP: as k_lstm_bwd_step (the layer-above segment masked by drop(h_l) before the recurrent one).
+template <int H, class CfgNND, bool KEPT, bool DROP>
 __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(const float* GsAll, float* dGAll,
                                                       const float* __restrict__ dhAll, float* __restrict__ RGsAll,
                                                       const float* __restrict__ CsAll, const float* __restrict__ RCsAll,
@@ -310,7 +341,7 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                                       float* __restrict__ dcAll, float* __restrict__ RdcAll,
                                                       int64_t lsz, const float* __restrict__ theta,
                                                       const float* __restrict__ U, int64_t tstride, BwdWave wv, int L,
-                                                      int T, int M) {
+                                                      int T, int M, Drop dr) {
   __shared__ float smem[DualStage<CfgNND>::FLOATS];
   constexpr int G4 = 4 * H;
   const int p = wave_index(wv, (int)blockIdx.x);
@@ -343,7 +374,24 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
     SegKC la2{{up ? RGsAll + oa : RGz + on, up ? RGz + on : nullptr, nullptr, nullptr}, {w0, w1, 0, 0}, M};
     SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {w0, w1}, H};
     SegMC lb2{{up ? u + wih_up : u + lo.whh, u + lo.whh}, {w0, w1}, H};
-    if (ns) gemm_dual_mainloop<CfgNND, !KEPT>(la, la2, lb, lb2, m0, n0, ns * G4, 0, ap, at, smem);
+    if (DROP && up) {
+      // layer-above segment masked by drop(h_l) (primal and tangent alike), then the recurrent one
+      const XDrop xd{drop_site(dr.seed, 2, dr.step, l), dr.thr_lstm, dr.sc_lstm,
+                     ((uint64_t)dr.task_id[z] * T + t) * M * H, H};
+      gemm_dual_mainloop<CfgNND, !KEPT>(SegKC{{dGAll + oa, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
+                                        SegKC{{RGsAll + oa, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
+                                        SegMC{{th + wih_up, nullptr}, {G4, 0}, H},
+                                        SegMC{{u + wih_up, nullptr}, {G4, 0}, H}, m0, n0, G4, 0, ap, at, smem);
+      if (!KEPT) drop_acc<CfgNND>(ap, xd, m0, n0);
+      drop_acc<CfgNND>(at, xd, m0, n0);
+      if (nx)
+        gemm_dual_mainloop<CfgNND, !KEPT>(SegKC{{dGz + on, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
+                                          SegKC{{RGz + on, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
+                                          SegMC{{th + lo.whh, nullptr}, {G4, 0}, H},
+                                          SegMC{{u + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, G4, 0, ap, at, smem);
+    } else if (ns) {
+      gemm_dual_mainloop<CfgNND, !KEPT>(la, la2, lb, lb2, m0, n0, ns * G4, 0, ap, at, smem);
+    }
   }
   const bool first = (t == T - 1);
   const bool head = first && l == L - 1;
@@ -403,9 +451,15 @@ static void bwd_dual_grid(hipStream_t s, const Dims& d, const Work& w, const Bwd
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   dim3 grid(wv.off[wv.n], ntn, w.Z);
   const float* dh = KEPT ? w.dh : w.Gs;  // unread unless KEPT
-  SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, Cfg, KEPT><<<grid, Cfg::NTH, 0, s>>>(
-                            w.Gs, w.dG, dh, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride, wv,
-                            d.L, d.T, w.M));
+  if (w.drop.lstm()) {
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, Cfg, KEPT, true><<<grid, Cfg::NTH, 0, s>>>(
+                              w.Gs, w.dG, dh, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride,
+                              wv, d.L, d.T, w.M, w.drop));
+  } else {
+    SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, Cfg, KEPT, false><<<grid, Cfg::NTH, 0, s>>>(
+                              w.Gs, w.dG, dh, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride,
+                              wv, d.L, d.T, w.M, w.drop));
+  }
 }
 
 void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,

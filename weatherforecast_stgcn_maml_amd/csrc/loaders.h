@@ -186,6 +186,60 @@ struct WgB {
   }
 };
 
+// Dropout mask on the x segment of an LSTM layer's input: x = drop(h_{l-1}) of one
+// (task, t) slab; element (m, k) has index base + m*H + k (kernels.h Drop, kind 2).
+struct XDrop {
+  uint32_t site, thr;
+  float sc;
+  uint64_t base;
+  int H;
+  __device__ __forceinline__ float4 apply(float4 v, int m, int k) const {
+    const uint64_t i0 = base + (uint64_t)m * H + k;
+    v.x = drop_keep(site, i0, thr) ? v.x * sc : 0.f;
+    v.y = drop_keep(site, i0 + 1, thr) ? v.y * sc : 0.f;
+    v.z = drop_keep(site, i0 + 2, thr) ? v.z * sc : 0.f;
+    v.w = drop_keep(site, i0 + 3, thr) ? v.w * sc : 0.f;
+    return v;
+  }
+};
+
+// acc(m, j) *= mask of element base + m*H + j (the BPTT's layer-above segment, whose dX
+// reaches h_l through drop(h_l)).
+template <class C>
+__device__ __forceinline__ void drop_acc(Acc<C>& acc, const XDrop& d, int m0, int n0) {
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < C::WTN; ++jj) {
+      const int j = n0 + acc_col<C>(jj);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint64_t idx = d.base + (uint64_t)(m0 + acc_row<C>(i, r)) * d.H + j;
+        acc.v[i][jj][r] = drop_keep(d.site, idx, d.thr) ? acc.v[i][jj][r] * d.sc : 0.f;
+      }
+    }
+}
+
+// SegKC whose segments 0 (x) and 2 (R x) are dropout-masked (tangent gate GEMM, layers >= 1).
+struct SegKCDrop {
+  SegKC s;
+  XDrop d;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    if (r >= s.rows) return f4zero();
+    int kk = k;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (kk < s.w[q]) {
+        if (!s.p[q]) return f4zero();
+        const float4 v = ld4(s.p[q] + (int64_t)r * s.w[q] + kk);
+        return (q == 0 || q == 2) ? d.apply(v, r, kk) : v;
+      }
+      kk -= s.w[q];
+    }
+    return f4zero();
+  }
+};
+
 // Gate nonlinearities. SMAML_FAST_GATES (default) uses the hardware transcendentals:
 // v_exp_f32 on x*log2(e) and v_rcp_f32 (1 ulp), and for tanh 1 - 2/(1+e^{2|x|}) with an odd
 // Taylor polynomial below |x| < 0.125 (no cancellation near 0). Relative error <~1e-6 per

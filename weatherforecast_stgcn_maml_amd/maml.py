@@ -86,14 +86,23 @@ class MetaLearner:
     """Holds theta (flat trainable vector), AdamW state and the tasks of this rank."""
 
     def __init__(self, dims: ModelDims, cfg: MamlConfig, gcn_params: dict, theta: dict,
-                 edge_index: np.ndarray, device=None, process_group=None, task_group="auto"):
+                 edge_index: np.ndarray, device=None, process_group=None, task_group="auto",
+                 dropout=(0.0, 0.0), dropout_seed: int = 0):
         """``task_group``: tasks batched into one pass of the C driver. ``None`` = all of this
         rank's tasks at once; ``"auto"`` (default) = plan_task_group: second-order meta-steps run
         in groups small enough that every inner step's primal stays resident for the sweep.
-        The meta-gradient is summed over groups before the all-reduce and outer step."""
+        The meta-gradient is summed over groups before the all-reduce and outer step.
+
+        ``dropout = (p_gcn, p_lstm)``: train-mode dropout as the reference applies it in its
+        inner loop (STGCN ``dropout_rate`` after conv1-3, ``lstm_dropout`` between LSTM layers
+        and on the head input), with counter-based masks keyed by
+        (``dropout_seed``, meta-step, global task id, inner step, element). (0, 0) = off: the
+        reference parity setting."""
         self.dims = dims
         self.cfg = cfg
         self.task_group = task_group
+        self.dropout = (float(dropout[0]), float(dropout[1]))
+        self.dropout_seed = int(dropout_seed)
         self.device = torch.device(device or "cuda")
         self.ctx = _capi.Context(dims, self.device.index or 0)
         self.ctx.set_graph(edge_index)
@@ -109,12 +118,14 @@ class MetaLearner:
         self.tasks: List[torch.Tensor] = []
 
     # tasks are [t_total, N, 24] float32 feature streams resident in HBM
-    def set_tasks(self, features: Sequence):
+    def set_tasks(self, features: Sequence, task_ids: Optional[Sequence[int]] = None):
+        """``task_ids``: global ids of these tasks (dropout mask keys; default 0..n-1)."""
         feats = []
         for f in features:
             t = f if torch.is_tensor(f) else torch.from_numpy(np.ascontiguousarray(f))
             feats.append(t.to(self.device, torch.float32).contiguous())
         self.tasks = feats
+        self.task_ids = np.asarray(task_ids if task_ids is not None else np.arange(len(feats)), np.int32)
         tg = self.task_group
         if tg == "auto":
             free, _ = torch.cuda.mem_get_info(self.device)
@@ -133,7 +144,13 @@ class MetaLearner:
             windows = window_table(cfg, Z)
         K = cfg.inner_steps
         stream = _capi.stream_ptr(torch)
+        if self.dropout != (0.0, 0.0):  # fresh masks every meta-step
+            self.ctx.set_dropout(self.dropout[0], self.dropout[1],
+                                 (self.dropout_seed * 1000003 + self.step * 7919 + 1) & 0xFFFFFFFF)
+        else:
+            self.ctx.set_dropout(0.0, 0.0, 0)
         if len(self._groups) == 1:
+            self.ctx.set_task_ids(self.task_ids)
             losses = torch.empty(K + 1, Z, device=self.device)
             norms = torch.empty(max(K, 1), Z, device=self.device)
             self.ctx.meta_step(stream, self.theta, cfg.order, K, cfg.batch, windows, cfg.inner_lr,
@@ -147,6 +164,7 @@ class MetaLearner:
                 lg = torch.empty(K + 1, n, device=self.device)
                 ng = torch.empty(max(K, 1), n, device=self.device)
                 self.ctx.set_tasks(grp)
+                self.ctx.set_task_ids(self.task_ids[z0:z0 + n])
                 mg = (self.meta_grad if gi == 0 else self._mg_part) if cfg.order >= 1 else None
                 self.ctx.meta_step(stream, self.theta, cfg.order, K, cfg.batch, windows[:, z0:z0 + n],
                                    cfg.inner_lr, cfg.max_norm, cfg.query_loss_scale, meta_grad=mg,

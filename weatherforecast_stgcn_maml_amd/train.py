@@ -48,12 +48,14 @@ class OuterLR:
 def meta_train(dims: ModelDims, features: Sequence, edge_index, gcn_full: dict, theta: dict, cfg: MamlConfig,
                epochs: int = NUM_EPOCHS, batch_tasks: int = BATCH_SIZE, koppen_state: Optional[dict] = None,
                log_csv: Optional[str] = None, ckpt_dir: Optional[str] = None, seed: int = SEED,
-               device: str = "cuda", verbose: bool = True):
+               device: str = "cuda", verbose: bool = True, dropout=(0.0, 0.0)):
     """Returns (learner, history). ``gcn_full`` holds every non-trainable hybrid tensor
-    (conv params + the unused ``base_stgcn.output_layer``) for the checkpoint."""
+    (conv params + the unused ``base_stgcn.output_layer``) for the checkpoint. ``dropout`` =
+    (STGCN dropout_rate, lstm_dropout): the reference trains with (0.2, 0.2); the default (0, 0)
+    is the parity setting."""
     rng = np.random.RandomState(seed)
     gcn = {k: v for k, v in gcn_full.items() if k.startswith("base_stgcn.conv")}
-    ml = MetaLearner(dims, cfg, gcn, theta, edge_index, device=device)
+    ml = MetaLearner(dims, cfg, gcn, theta, edge_index, device=device, dropout=dropout, dropout_seed=seed)
     feats = [f if torch.is_tensor(f) else torch.from_numpy(np.ascontiguousarray(f)) for f in features]
     feats = [f.to(ml.device, torch.float32).contiguous() for f in feats]
     sched = OuterLR(cfg.outer_lr)
@@ -76,7 +78,7 @@ def meta_train(dims: ModelDims, features: Sequence, edge_index, gcn_full: dict, 
             idx = rng.choice(n, batch_tasks, replace=False)
         else:
             idx = np.arange(n)
-        ml.set_tasks([feats[i] for i in idx])
+        ml.set_tasks([feats[i] for i in idx], task_ids=idx)
         res = ml.meta_step(lr=sched.lr)
         loss = res.meta_loss
         if len(task_losses) < n:
