@@ -46,6 +46,8 @@ def parse():
                    help="5 = BASELINE stress config: 64 tasks, N=1024 (32x32), Hc=512, LSTM 4x128, K=10, "
                         "second order (flags given explicitly still win, e.g. --tasks 8 = one rank's share at 8 GPUs)")
     p.add_argument("--hidden-channels", type=int, default=None)
+    p.add_argument("--dropout", type=float, nargs=2, default=(0.0, 0.0), metavar=("P_GCN", "P_LSTM"),
+                   help="train-mode dropout (the reference trains at 0.2 0.2; 0 0 = the parity setting)")
     p.add_argument("--task-group", default="auto",
                    help="tasks per pass of the C driver: an int, 'all', or 'auto' (default: groups small "
                         "enough that every inner step's primal stays resident for the second-order sweep)")
@@ -153,7 +155,8 @@ def main():
     T_total = stream_len_for(cfg, d)
     feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T_total) for j in mine]
     ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
-                     ei, device=f"cuda:{local}", task_group=args.task_group)
+                     ei, device=f"cuda:{local}", task_group=args.task_group, dropout=tuple(args.dropout),
+                     dropout_seed=SEED)
     ml.set_tasks(feats, task_ids=mine)
     torch.cuda.synchronize()
 
@@ -210,6 +213,7 @@ def main():
             "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
             "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
             "task_group": len(ml._groups[0][1]),
+            "dropout": list(args.dropout),
         },
         "meta_step_tflop": flops_meta / 1e12,
         "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,

@@ -88,7 +88,10 @@ class AdaptResult:
 
 def adapt(dims: ModelDims, features, edge_index, gcn: dict, theta: dict, region_name: str, epochs: int = 15,
           max_samples: int = 1200, train_frac: float = 0.8, base_lr: float = 0.0006, device="cuda",
-          val_batch: int = 32, ctx: Optional[_capi.Context] = None) -> AdaptResult:
+          val_batch: int = 32, ctx: Optional[_capi.Context] = None, dropout=(0.0, 0.0),
+          dropout_seed: int = 0) -> AdaptResult:
+    """``dropout`` = (STGCN dropout_rate, lstm_dropout) of the train-mode steps (the reference
+    adapts in train mode: (0.2, 0.2)); validation runs without dropout (eval mode)."""
     dev = torch.device(device)
     ctx = ctx or _capi.Context(dims, dev.index or 0)
     ei = edge_index.detach().cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
@@ -111,7 +114,9 @@ def adapt(dims: ModelDims, features, edge_index, gcn: dict, theta: dict, region_
     lr = lr0
     step = 0
     losses = torch.empty(max(n_train, 1), device=dev)
+    ctx.set_task_ids([0])
     for _ in range(epochs):
+        ctx.set_dropout(dropout[0], dropout[1], dropout_seed)  # masks keyed by the global step index
         order = random_sampler_order(n_train).numpy().astype(np.int32)
         lr_dev = torch.full((n_train,), lr, device=dev, dtype=torch.float32)
         ctx.adapt_steps(stream, th, m, v, step, order.reshape(n_train, 1), lr_dev, (0.9, 0.999), 1e-8, wd,
@@ -121,12 +126,14 @@ def adapt(dims: ModelDims, features, edge_index, gcn: dict, theta: dict, region_
         res.epoch_losses.append(avg)
         res.lrs.append(lr)
         lr = sched.step(avg)
+    ctx.set_dropout(0.0, 0.0, 0)
     res.val_loss = evaluate(ctx, th, list(range(n_train, n_max)), val_batch)
     return res
 
 
 def evaluate(ctx: _capi.Context, theta: torch.Tensor, sample_ids, batch: int = 32) -> float:
-    """Mean per-sample MSE over the given windows of task 0 (no gradients)."""
+    """Mean per-sample MSE over the given windows of task 0 (no gradients, no dropout)."""
+    ctx.set_dropout(0.0, 0.0, 0)
     total, n = 0.0, 0
     stream = _capi.stream_ptr(torch)
     for i in range(0, len(sample_ids), batch):

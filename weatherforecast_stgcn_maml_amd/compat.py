@@ -27,7 +27,11 @@ def _learner(hybrid_model, edge_index, device, steps, num_nodes):
     cfg = MamlConfig(inner_steps=steps, batch=1, order=0, inner_lr=INNER_LR, max_norm=MAX_GRAD_NORM,
                      query_loss_scale=1.0 / GRAD_ACCUMULATION_STEPS)
     ei = edge_index.detach().cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
-    return MetaLearner(dims, cfg, hybrid_model.named_gcn(), hybrid_model.named_trainable(), ei, device=device), dims
+    # the reference adapts a train()-mode copy (train_hybrid_maml_v5.py:113,159): its dropout
+    # rates apply; masks are keyed off torch's seed for reproducibility
+    drop = (float(hybrid_model.base_stgcn.dropout_rate), float(hybrid_model.dropout.p))
+    return MetaLearner(dims, cfg, hybrid_model.named_gcn(), hybrid_model.named_trainable(), ei, device=device,
+                       dropout=drop, dropout_seed=torch.initial_seed() & 0xFFFFFFFF), dims
 
 
 def _run(hybrid_model, task_specs, device):

@@ -131,8 +131,9 @@ class HybridSTGCN_LSTM(nn.Module):
         if x.device.type != "cuda":
             raise _capi.SmamlError(-1, "HybridSTGCN_LSTM.forward runs on a HIP device only")
         if self.training and (self.dropout.p > 0 or self.base_stgcn.dropout_rate > 0):
-            warnings.warn("the HIP path applies no dropout; build the model with dropout 0 "
-                          "for train-mode parity (SURVEY F7)", stacklevel=3)
+            warnings.warn("the module-level forward/backward applies no dropout (the training drivers "
+                          "MetaLearner / meta_train / adapt and the inner_loop_v4 / meta_update_v4 wrappers "
+                          "do); build the model with dropout 0 for train-mode parity (SURVEY F7)", stacklevel=3)
         T = self.base_stgcn.window_size
         if x.shape[0] % T:
             raise ValueError(f"x has {x.shape[0]} rows, not a multiple of window_size={T}")
