@@ -383,11 +383,12 @@ def climate_lr(region_name, epoch_idx, base_lr, epoch_loss):
 
 
 def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_samples: int = 1200,
-                    base_lr: float = 0.0006):
+                    base_lr: float = 0.0006, dropout=None):
     """adapt_hybrid_v5.adaptModel's fine-tuning loop (adapt_hybrid_v5.py:152-231): batch-1
     samples in DataLoader(shuffle=True) order, MSE, backward, clip_grad_norm_(1.0),
     torch.optim.Adam(lr, weight_decay) from create_climate_optimizer, scheduler per epoch,
-    then the validation MSE. Returns (params, epoch_losses, lrs, val_loss)."""
+    then the validation MSE. Returns (params, epoch_losses, lrs, val_loss). dropout = (seed,
+    p_gcn, p_lstm): train-step masks keyed by the global step index (task id 0)."""
     n_all = task.features.shape[0] - task.dims.window_size - task.dims.forecast_horizon
     n_max = min(max_samples, n_all)
     n_train = int(0.8 * n_max)
@@ -399,6 +400,7 @@ def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_s
     leaves = [Pt[k].detach().clone().requires_grad_(True) for k in names]
     opt = torch.optim.Adam(leaves, lr=lr0, weight_decay=wd)
     epoch_losses, lrs = [], []
+    gstep = 0
     for ep in range(epochs):
         seed = int(torch.empty((), dtype=torch.int64).random_().item())
         g = torch.Generator()
@@ -408,7 +410,9 @@ def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_s
         lrs.append(opt.param_groups[0]["lr"])
         for i in order:
             opt.zero_grad()
-            loss, _ = batch_loss(dict(zip(names, leaves)), Pg, task, [i])
+            drop = Dropout(dropout[0], dropout[1], dropout[2], 0, gstep) if dropout else None
+            gstep += 1
+            loss, _ = batch_loss(dict(zip(names, leaves)), Pg, task, [i], drop)
             loss.backward()
             torch.nn.utils.clip_grad_norm_(leaves, max_norm=1.0)
             opt.step()

@@ -18,8 +18,9 @@ def rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-@pytest.mark.parametrize("region", ["Thailand", "Delhi"])
-def test_adaptation_matches_oracle(region, tmp_path):
+@pytest.mark.parametrize("region,drop", [("Thailand", None), ("Delhi", None), ("Delhi", (0.2, 0.2))])
+def test_adaptation_matches_oracle(region, drop, tmp_path):
+    """drop: train-mode dropout at the reference's rates with the oracle's restated masks."""
     d = CONFIG1
     P = synth.init_params(21, d, gcn_bias_scale=0.1)
     tr = {k: v for k, v in P.items() if k.startswith(("lstm.", "output_layer."))}
@@ -30,12 +31,12 @@ def test_adaptation_matches_oracle(region, tmp_path):
     epochs = 5
     torch.manual_seed(123)
     res = adapt(d, feats, ei, {k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, tr, region,
-                epochs=epochs, device="cuda:0")
+                epochs=epochs, device="cuda:0", dropout=drop or (0.0, 0.0), dropout_seed=77)
     torch.manual_seed(123)
     PT = refcpu.to_torch(P)
     ref_p, ref_losses, ref_lrs, ref_val = refcpu.adapt_reference(
         {k: PT[k] for k in tr}, {k: v for k, v in PT.items() if k not in tr}, refcpu.TaskData(feats, ei, d),
-        region, epochs)
+        region, epochs, dropout=(77, drop[0], drop[1]) if drop else None)
     assert res.n_train == 16 and res.n_val == 4
     np.testing.assert_allclose(res.lrs, ref_lrs, rtol=1e-12)
     assert rel(res.epoch_losses, ref_losses) < 1e-5
