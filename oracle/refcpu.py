@@ -57,12 +57,12 @@ def drop_site(seed: int, kind: int, step: int, layer: int) -> np.uint64:
 
 
 def drop_keep(site, idx: np.ndarray, p: float) -> np.ndarray:
-    """bool mask: element idx (uint64) of a site is kept iff (hash >> 8) >= round(p * 2^24)."""
+    """bool mask: element idx (uint64) of a site is kept iff
+    (mix32(site ^ lo(idx) ^ hi(idx) * 0x9E3779B9) >> 8) >= round(p * 2^24)."""
     idx = np.asarray(idx, dtype=np.uint64)
     thr = np.uint64(min(int(round(p * 16777216.0)), 16777216))
-    h = _mix32((idx >> np.uint64(32)) + np.uint64(0x9E3779B9))
-    h = _mix32((idx & _M32) ^ h)
-    h = _mix32(np.uint64(site) ^ h)
+    hi = ((idx >> np.uint64(32)) * np.uint64(0x9E3779B9)) & _M32
+    h = _mix32(np.uint64(site) ^ (idx & _M32) ^ hi)
     return (h >> np.uint64(8)) >= thr
 
 

@@ -430,10 +430,11 @@ def test_dropout_matches_oracle(order):
     mg = params.unpack(ml.meta_grad, d, 0)
     for k in names:
         assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
-    # the masks matter: without dropout the losses differ
+    # the masks matter: without dropout the meta-gradient is a different one
     ml0 = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
     ml0.set_tasks(feats)
-    assert not np.allclose(ml0.meta_step().losses.cpu().numpy(), losses, rtol=1e-3)
+    ml0.meta_step()
+    assert rel(ml.meta_grad.cpu().numpy(), ml0.meta_grad.cpu().numpy()) > 0.05
 
 
 def test_dropout_masks_follow_task_ids_not_groups():

@@ -41,9 +41,10 @@ struct GcnOff {
 
 // Train-mode dropout (hybrid_model.py:67,70,73 GCN outputs; nn.LSTM's inter-layer dropout :47;
 // the head input :108) from counter-based masks: element idx of site (kind, step, layer) is
-// kept iff (mix32(site ^ mix32(lo(idx) ^ mix32(hi(idx) + golden))) >> 8) >= thr, and scaled by
-// 1 / (1 - p). oracle/refcpu.py (drop_keep) restates the same function, so the masks agree
-// bit for bit. Element indices (task = global task id):
+// kept iff (mix32(site ^ lo(idx) ^ hi(idx) * golden) >> 8) >= thr (one mixing round per
+// element: the site seed is already mixed), and scaled by 1 / (1 - p). oracle/refcpu.py
+// (drop_keep) restates the same function, so the masks agree bit for bit. Element indices
+// (task = global task id):
 //   kind 1, layer k (GCN conv k+1 output): ((task * B + s) * T*N + row) * Hc + channel
 //   kind 2, layer l (LSTM layer l output fed to layer l+1): ((task * T + t) * M + m) * H + unit
 //   kind 3 (head input h_T): (task * M + m) * H + unit
@@ -59,7 +60,7 @@ __host__ __device__ inline uint32_t drop_site(uint32_t seed, int kind, int step,
   return mix32(seed ^ mix32(((uint32_t)kind << 24) ^ ((uint32_t)step << 8) ^ (uint32_t)layer));
 }
 __host__ __device__ inline bool drop_keep(uint32_t site, uint64_t idx, uint32_t thr) {
-  return (mix32(site ^ mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) + 0x9E3779B9U))) >> 8) >= thr;
+  return (mix32(site ^ (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x9E3779B9U)) >> 8) >= thr;
 }
 struct Drop {
   uint32_t seed;
