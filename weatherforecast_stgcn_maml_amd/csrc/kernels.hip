@@ -223,11 +223,10 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
 template <int H, bool DROP>
-__global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
-                                                      float* __restrict__ CsAll, float* __restrict__ GsAll,
-                                                      int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      FwdWave wv, int T, int M, Drop dr) {
-  __shared__ float smem[CfgGate::SMEM_FLOATS];
+__device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
+                                              float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
+                                              const float* __restrict__ theta, int64_t tstride, FwdWave wv, int T,
+                                              int M, const Drop& dr, float* smem) {
   int l, t, b0;
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
@@ -317,6 +316,24 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
   return fl;
 }
 
+// The dropout variant holds the mask state beside the 4-gate tile: it gets the register budget
+// of 3 waves/SIMD instead of 4 (no spill).
+template <int H>
+__global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
+                                                      float* __restrict__ CsAll, float* __restrict__ GsAll,
+                                                      int64_t lsz, const float* __restrict__ theta, int64_t tstride,
+                                                      FwdWave wv, int T, int M, Drop dr) {
+  __shared__ float smem[CfgGate::SMEM_FLOATS];
+  lstm_fwd_step<H, false>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem);
+}
+template <int H>
+__global__ __attribute__((amdgpu_waves_per_eu(3))) __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step_drop(
+    const float* __restrict__ F, float* __restrict__ HsAll, float* __restrict__ CsAll, float* __restrict__ GsAll,
+    int64_t lsz, const float* __restrict__ theta, int64_t tstride, FwdWave wv, int T, int M, Drop dr) {
+  __shared__ float smem[CfgGate::SMEM_FLOATS];
+  lstm_fwd_step<H, true>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem);
+}
+
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
@@ -328,11 +345,11 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
   if (w.drop.lstm()) {
-    SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT, true><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
+    SMAML_DISPATCH_H(d.H, k_lstm_fwd_step_drop<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
                                                                                    tstride, wv, d.T, w.M, w.drop));
     return;
   }
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT, false><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
+  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
                                                                            wv, d.T, w.M, w.drop));
 }
 
