@@ -8,7 +8,7 @@ if [ -x ./tools/gemm_micro ]; then timeout -k 10 300 ./tools/gemm_micro > gpurun
 : > gpurun_out/ab.log
 for round in $(seq 1 ${AB_ROUNDS:-2}); do
   for v in libsmaml.so ${AB_VARIANTS:-libsmaml_bk16.so libsmaml_gate16.so}; do
-    SMAML_LIB=weatherforecast_stgcn_maml_amd/$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-sample-steps 0 > gpurun_out/ab_tmp.log 2>&1 || exit $?
+    SMAML_LIB=weatherforecast_stgcn_maml_amd/$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-sample-steps 0 ${BENCH_ARGS:-} > gpurun_out/ab_tmp.log 2>&1 || exit $?
     echo "$v $(tail -1 gpurun_out/ab_tmp.log)" >> gpurun_out/ab.log
   done
 done

@@ -242,7 +242,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   const int64_t G = 4 * d.H;
   const int64_t seq = (int64_t)zbc * d.N;
   int max_cin = std::max(d.Hc, d.H);
-  const int64_t wpart = std::max<int64_t>((int64_t)zc * G * (max_cin + d.H + 1) * 32, 1 << 24);
+  const int64_t wpart = std::max<int64_t>((int64_t)zc * G * (max_cin + d.H + 1) * SMAML_WGRAD_MAXSPLIT, 1 << 24);
   const int64_t lblk = (int64_t)zc * ((seq + 127) / 128 + 1);
   std::vector<std::pair<void**, int64_t>> parts;  // (dst, bytes)
   Work w{};

@@ -100,6 +100,9 @@ struct Work {
 };
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
+#ifndef SMAML_WGRAD_MAXSPLIT
+#define SMAML_WGRAD_MAXSPLIT 128  // split-K slices per weight gradient (partial-slab capacity)
+#endif
 
 // One anti-diagonal of the (layer, step) grid of the LSTM forward: the problems (l, t) with
 // l + t = diag are independent ((l, t) reads only (l-1, t) and (l, t-1), both on the previous
