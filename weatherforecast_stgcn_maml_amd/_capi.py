@@ -24,7 +24,7 @@ EXPORTS = (
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
     "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",

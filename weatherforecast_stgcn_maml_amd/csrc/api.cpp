@@ -669,7 +669,7 @@ extern "C" {
 
 const char* smaml_last_error(void) { return g_err.c_str(); }
 
-int32_t smaml_abi_version(void) { return 2; }
+int32_t smaml_abi_version(void) { return 3; }
 
 int smaml_param_layout(const smaml_dims* dims, int32_t which, int64_t* offsets, int64_t* sizes, int32_t cap,
                        int32_t* count, int64_t* total) {
