@@ -138,13 +138,16 @@ __device__ __forceinline__ int acc_col(int j) {
   return wn * (C::WTN * 32) + j * 32 + (lane & 31);
 }
 
-// Optional per-K-tile hook run on the staged A tile (e.g. column sums for bias grads).
+// Optional hooks: operator() runs once per K-tile on the staged A tile; afrag(i, a) sees every
+// A fragment this lane feeds to the MFMAs (4 k-steps of tile row i), e.g. for column sums
+// of A (bias gradients) kept in registers instead of re-read from LDS.
 struct NoHook {
   __device__ __forceinline__ void operator()(const float*, int) const {}
+  __device__ __forceinline__ void afrag(int, const float4&) {}
 };
 
-template <class C>
-__device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C>& acc) {
+template <class C, class Hook = NoHook>
+__device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C>& acc, Hook& hook) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
   const int arow = wm * (C::WTM * 32) + (lane & 31);
@@ -158,6 +161,8 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
 #pragma unroll
     for (int j = 0; j < C::WTN; ++j) b[j] = frag4<C::B_KC, C::LDB, C::BK>(bs, brow + 32 * j, h, q);
 #pragma unroll
+    for (int i = 0; i < C::WTM; ++i) hook.afrag(i, a[i]);
+#pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int i = 0; i < C::WTM; ++i)
@@ -168,10 +173,9 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
 }
 
 // acc += sum_{k in [kbeg,kend)} A[m0+., k] * B[n0+., k]
-template <class C, class LA, class LB, class Hook = NoHook>
+template <class C, class LA, class LB, class Hook>
 __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg,
-                                              int kend, Acc<C>& acc, float* smem,
-                                              const Hook& hook = Hook()) {
+                                              int kend, Acc<C>& acc, float* smem, Hook& hook) {
   float* As = smem;
   float* Bs = smem + 2 * C::A_STAGE;
   constexpr int BKc = C::BK;
@@ -195,13 +199,20 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
     const float* as = As + cur * C::A_STAGE;
     const float* bs = Bs + cur * C::B_STAGE;
     hook(as, kt);
-    mma_tile<C>(as, bs, acc);
+    mma_tile<C>(as, bs, acc, hook);
     if (more) {
       store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(As + (cur ^ 1) * C::A_STAGE, ra);
       store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(Bs + (cur ^ 1) * C::B_STAGE, rb);
     }
     __syncthreads();
   }
+}
+
+template <class C, class LA, class LB>
+__device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg,
+                                              int kend, Acc<C>& acc, float* smem) {
+  NoHook hook;
+  gemm_mainloop<C>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
 }
 
 }  // namespace smaml

@@ -671,17 +671,49 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 // (the trailing column of ones is produced as column sums of A in tile column 0:
 //  the bias gradient). For LSTM layer l: A = dG [T*M][4H], B1 = x_l [T*M][cin],
 //  B2 = h_l (shifted one time block: h_{t-1}); for the head: A = dpred, B1 = h_T.
+#ifndef SMAML_COLSUM_LDS
+// Column sums of A (= the bias gradient) from the A fragments the MFMAs already hold in
+// registers: lane (row r = arow + 32 i, k-half h) sums its k-values; the halves are combined
+// with one cross-lane add after the mainloop (colsum_rows). No extra LDS traffic.
 struct ColSumHook {
-  float* acc;
-  __device__ __forceinline__ void operator()(const float* as, int) const {
-    if (threadIdx.x < CfgTN::BM) {
-      float s = *acc;
-#pragma unroll 8
-      for (int kk = 0; kk < CfgTN::BK; ++kk) s += as[kk * CfgTN::LDA + threadIdx.x];
-      *acc = s;
+  float s[CfgTN::WTM];
+  __device__ __forceinline__ ColSumHook() {
+#pragma unroll
+    for (int i = 0; i < CfgTN::WTM; ++i) s[i] = 0.f;
+  }
+  __device__ __forceinline__ void operator()(const float*, int) const {}
+  __device__ __forceinline__ void afrag(int i, const float4& a) { s[i] += (a.x + a.y) + (a.z + a.w); }
+  // lanes 0..31 own rows wm*(WTM*32) + 32 i + lane of the tile
+  __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias) {
+    const int lane = threadIdx.x & 63, wm = (threadIdx.x >> 6) / CfgTN::WAVES_N;
+#pragma unroll
+    for (int i = 0; i < CfgTN::WTM; ++i) {
+      const float v = s[i] + __shfl_xor(s[i], 32);
+      const int row = m0 + wm * (CfgTN::WTM * 32) + 32 * i + lane;
+      if (lane < 32 && (threadIdx.x >> 6) % CfgTN::WAVES_N == 0 && row < Mrows)
+        P[(int64_t)row * ldp + ncols] = with_bias ? v : 0.f;
     }
   }
 };
+#else
+// A/B baseline: column sums re-read from the staged A tile in LDS once per K-tile.
+struct ColSumHook {
+  float bsum = 0.f;
+  __device__ __forceinline__ void operator()(const float* as, int) {
+    if (threadIdx.x < CfgTN::BM) {
+      float s = bsum;
+#pragma unroll 8
+      for (int kk = 0; kk < CfgTN::BK; ++kk) s += as[kk * CfgTN::LDA + threadIdx.x];
+      bsum = s;
+    }
+  }
+  __device__ __forceinline__ void afrag(int, const float4&) {}
+  __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias) {
+    const int row = m0 + threadIdx.x;
+    if (threadIdx.x < CfgTN::BM && row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? bsum : 0.f;
+  }
+};
+#endif
 
 // B1 = drop(h_{l-1}) for the input weights of LSTM layer l >= 1 under dropout: row k of the
 // task's [T*M][H] slab is element (task * T*M + k) * H + unit of kind 2, layer l-1.
@@ -717,20 +749,18 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
   const int m0 = tm * CfgTN::BM, n0 = tn * CfgTN::BN;
   Acc<CfgTN> acc;
   acc.zero();
-  float bsum = 0.f;
+  ColSumHook hook;
   // k indices exceed int range only in the loaders (int64 there); the mainloop
   // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
   if (DROP) {
     const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
                               (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
     if (tn == 0 && with_bias) {
-      ColSumHook hook{&bsum};
       gemm_mainloop<CfgTN>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     } else {
       gemm_mainloop<CfgTN>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
   } else if (tn == 0 && with_bias) {
-    ColSumHook hook{&bsum};
     gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
     gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
@@ -749,10 +779,7 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
         if (row < Mrows) P[(int64_t)row * ldp + c] = acc.v[i][j][r];
       }
     }
-  if (tn == 0 && threadIdx.x < CfgTN::BM) {
-    const int row = m0 + threadIdx.x;
-    if (row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? bsum : 0.f;
-  }
+  if (tn == 0) hook.store(P, m0, Mrows, ldp, ncols, with_bias != 0);
 }
 
 __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int Mrows, int ldp, int c1, int c2,
