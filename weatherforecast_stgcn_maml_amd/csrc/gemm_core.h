@@ -24,6 +24,13 @@ namespace smaml {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;  // default K-tile (GemmCfg's BK_ parameter)
+#ifndef SMAML_PRIO
+#define SMAML_PRIO 1  // raise the wave priority around the MFMA phase of each K-tile (A/B: -0.5 %)
+#endif
+#ifndef SMAML_IGLP
+#define SMAML_IGLP 1  // LLVM iglp_opt DS/MFMA interleave strategy for the mainloops that ask for it
+#endif                // (IG template argument; A/B: fwd_dual -7, wgrad -7, GCN -2 ms; the primal
+                      // gate / BPTT / dual-BPTT loops are slower with it and keep the default order)
 constexpr int NT = 256;  // threads per workgroup of the 4-wave configurations
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
@@ -146,13 +153,14 @@ struct NoHook {
   __device__ __forceinline__ void afrag(int, const float4&) {}
 };
 
-template <class C, class Hook = NoHook>
+template <class C, int IG = -1, class Hook = NoHook>
 __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C>& acc, Hook& hook) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
   const int arow = wm * (C::WTM * 32) + (lane & 31);
   const int brow = wn * (C::WTN * 32) + (lane & 31);
   const int h = lane >> 5;
+  if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
 #pragma unroll
   for (int q = 0; q < C::BK / 8; ++q) {
     float4 a[C::WTM], b[C::WTN];
@@ -173,7 +181,8 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
 }
 
 // acc += sum_{k in [kbeg,kend)} A[m0+., k] * B[n0+., k]
-template <class C, class LA, class LB, class Hook>
+// IG >= 0: ask LLVM for iglp_opt strategy IG in the MFMA phase (set per call site by A/B).
+template <class C, int IG = -1, class LA, class LB, class Hook>
 __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg,
                                               int kend, Acc<C>& acc, float* smem, Hook& hook) {
   float* As = smem;
@@ -199,7 +208,13 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
     const float* as = As + cur * C::A_STAGE;
     const float* bs = Bs + cur * C::B_STAGE;
     hook(as, kt);
-    mma_tile<C>(as, bs, acc, hook);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);  // MFMA phase first in the SIMD's issue arbitration
+#endif
+    mma_tile<C, IG>(as, bs, acc, hook);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (more) {
       store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(As + (cur ^ 1) * C::A_STAGE, ra);
       store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(Bs + (cur ^ 1) * C::B_STAGE, rb);
@@ -208,11 +223,11 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
   }
 }
 
-template <class C, class LA, class LB>
+template <class C, int IG = -1, class LA, class LB>
 __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg,
                                               int kend, Acc<C>& acc, float* smem) {
   NoHook hook;
-  gemm_mainloop<C>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
+  gemm_mainloop<C, IG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
 }
 
 }  // namespace smaml
@@ -300,10 +315,16 @@ __device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2,
     const bool more = kt + 1 < nkt;
     if (more) fetch(k0 + BKc);
     const float* st = smem + cur * STAGE;
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     if (k0 >= a2_kbeg)
       dual_mma<C, true, PRIMAL>(st, arow, brow, h, accp, acct);
     else
       dual_mma<C, false, PRIMAL>(st, arow, brow, h, accp, acct);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (more) store(smem + (cur ^ 1) * STAGE, k0 + BKc);
     __syncthreads();
   }

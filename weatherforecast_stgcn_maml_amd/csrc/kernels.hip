@@ -113,10 +113,10 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
   // only tiles that reach a sample's t = 0 block (its first N rows) need the ELL gather
   const int q0 = m0 - (int)la.rps_div.div((uint32_t)m0) * la.rps;
   if (q0 < la.ell_rows || q0 + CfgGcn::BM > la.rps) {
-    gemm_mainloop<CfgGcn>(la, lb, m0, n0, 0, la.cin, acc, smem);
+    gemm_mainloop<CfgGcn, SMAML_IGLP>(la, lb, m0, n0, 0, la.cin, acc, smem);
   } else {
     const GcnPlain lp{la.tab, la.buf, la.rps_div, la.rps, la.cin, la.R};
-    gemm_mainloop<CfgGcn>(lp, lb, m0, n0, 0, la.cin, acc, smem);
+    gemm_mainloop<CfgGcn, SMAML_IGLP>(lp, lb, m0, n0, 0, la.cin, acc, smem);
   }
   const int64_t M = (int64_t)B * N;
   float bc[CfgGcn::WTN];
@@ -756,14 +756,14 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
     const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
                               (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
     if (tn == 0 && with_bias) {
-      gemm_mainloop<CfgTN>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+      gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     } else {
-      gemm_mainloop<CfgTN>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
+      gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
   } else if (tn == 0 && with_bias) {
-    gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
-    gemm_mainloop<CfgTN>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
   }
   const int ncols = lb.c1 + lb.c2;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;

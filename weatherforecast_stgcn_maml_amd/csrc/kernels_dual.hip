@@ -103,9 +103,9 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
     if (DROP && l > 0)
-      gemm_mainloop<CfgGateD>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
     else
-      gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh, ap, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(la, lb, m0, n0, 0, cin + wh, ap, smem);
     if (j < H) {
       float bp[4];
 #pragma unroll
@@ -139,9 +139,9 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegKC la{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M};
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     if (DROP && l > 0)
-      gemm_mainloop<CfgGateD>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else
-      gemm_mainloop<CfgGateD>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
   }
   if (j >= H) return;
   float bu[4];
