@@ -222,6 +222,44 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 };
 
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
+// Cell epilogue of one gate tile (acc = the i, f, g, o pre-activations of 32 units x 32 rows
+// per wave, bias not yet added): gates, c_t = f c_{t-1} + i g, h_t = o tanh(c_t).
+template <int H>
+__device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* __restrict__ th, const LayerOff& lo,
+                                         float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
+                                         int m0, int ug, int t, int M) {
+  constexpr int UPB = CfgGate::WAVES_N;
+  const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
+  if (j >= H) return;
+  float bsum[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bsum[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
+  const int rb = m0 + acc_row<CfgGate>(0, 0);
+  const bool full = m0 + CfgGate::BM <= M;
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = rb + racc(r);
+    if (!full && m >= M) continue;
+    const uint32_t row = tM + (uint32_t)m;
+    const uint32_t oh = row * H + j;
+    const uint32_t og = row * (4 * H) + j;
+    const float gi = sigmoidf_(acc.v[0][0][r] + bsum[0]);
+    const float gf = sigmoidf_(acc.v[0][1][r] + bsum[1]);
+    const float gg = tanhf_(acc.v[0][2][r] + bsum[2]);
+    const float go = sigmoidf_(acc.v[0][3][r] + bsum[3]);
+    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+    const float c = gf * cp + gi * gg;
+    const float h = go * tanhf_(c);
+    stb(Gz, 4u * (og), gi);
+    stb(Gz, 4u * (og + H), gf);
+    stb(Gz, 4u * (og + 2 * H), gg);
+    stb(Gz, 4u * (og + 3 * H), go);
+    stb(Cz, 4u * (oh), c);
+    stb(Hz, 4u * (oh), h);
+  }
+}
+
 template <int H, bool DROP>
 __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                               float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
@@ -261,35 +299,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   }
 
-  const int j = (ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (threadIdx.x & 31);
-  if (j >= H) return;
-  float bsum[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) bsum[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
-  const int rb = m0 + acc_row<CfgGate>(0, 0);
-  const bool full = m0 + CfgGate::BM <= M;
-  const uint32_t tM = (uint32_t)t * (uint32_t)M;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = rb + racc(r);
-    if (!full && m >= M) continue;
-    const uint32_t row = tM + (uint32_t)m;
-    const uint32_t oh = row * H + j;
-    const uint32_t og = row * (4 * H) + j;
-    const float gi = sigmoidf_(acc.v[0][0][r] + bsum[0]);
-    const float gf = sigmoidf_(acc.v[0][1][r] + bsum[1]);
-    const float gg = tanhf_(acc.v[0][2][r] + bsum[2]);
-    const float go = sigmoidf_(acc.v[0][3][r] + bsum[3]);
-    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-    const float c = gf * cp + gi * gg;
-    const float h = go * tanhf_(c);
-    stb(Gz, 4u * (og), gi);
-    stb(Gz, 4u * (og + H), gf);
-    stb(Gz, 4u * (og + 2 * H), gg);
-    stb(Gz, 4u * (og + 3 * H), go);
-    stb(Cz, 4u * (oh), c);
-    stb(Hz, 4u * (oh), h);
-  }
+  fwd_cell<H>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
 }
 
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
@@ -334,6 +344,121 @@ __global__ __attribute__((amdgpu_waves_per_eu(3))) __launch_bounds__(CfgGate::NT
   lstm_fwd_step<H, true>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem);
 }
 
+// ---- split-K variant for small grids (batch-1 adaptation: M = N = 441 sequences) ----------
+// A step's critical path is one wave's K loop; when the diagonal has too few gate tiles to fill
+// the chip, S workgroups share a tile, each over a contiguous range of K-tiles, and write their
+// accumulators to a partial slab (w.wpart, lane order); k_lstm_fwd_cell sums the S partials in
+// a fixed order (deterministic) and runs the cell epilogue. Dropout-free steps only.
+template <class C>
+__device__ __forceinline__ float* part_slab(float* part, int S, int split) {
+  constexpr int PER = C::WTM * C::WTN * 16 * C::NTH;
+  return part + (((int64_t)blockIdx.z * gridDim.x + blockIdx.x) * S + split) * PER;
+}
+template <class C>
+__device__ __forceinline__ void store_part(const Acc<C>& acc, float* slab) {
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = ((i * C::WTN + j) * 4 + q) * C::NTH + (int)threadIdx.x;
+        st4(slab + 4 * f, make_float4(acc.v[i][j][4 * q], acc.v[i][j][4 * q + 1], acc.v[i][j][4 * q + 2],
+                                      acc.v[i][j][4 * q + 3]));
+      }
+}
+template <class C>
+__device__ __forceinline__ void add_part(Acc<C>& acc, const float* slab) {
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = ld4(slab + 4 * (((i * C::WTN + j) * 4 + q) * C::NTH + (int)threadIdx.x));
+        acc.v[i][j][4 * q] += v.x;
+        acc.v[i][j][4 * q + 1] += v.y;
+        acc.v[i][j][4 * q + 2] += v.z;
+        acc.v[i][j][4 * q + 3] += v.w;
+      }
+}
+// K-tile range [kbeg, kend) of split `split` out of S over a K-long reduction.
+__device__ __forceinline__ void split_range(int K, int S, int split, int bk, int& kbeg, int& kend) {
+  const int kt = (K + bk - 1) / bk, per = (kt + S - 1) / S;
+  kbeg = split * per * bk;
+  kend = min(K, kbeg + per * bk);
+}
+
+template <int H>
+__global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
+    const float* __restrict__ F, const float* __restrict__ HsAll, int64_t lsz, const float* __restrict__ theta,
+    int64_t tstride, FwdWave wv, int T, int M, int S, float* __restrict__ part) {
+  __shared__ float smem[CfgGate::SMEM_FLOATS];
+  int l, t, b0;
+  LayerOff lo;
+  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  const float* X = l == 0 ? F : HsAll + (int64_t)(l - 1) * lsz;
+  const int z = blockIdx.z;
+  const float* th = theta + (int64_t)z * tstride;
+  const int cin = lo.cin;
+  const int64_t slab = (int64_t)z * T * M;
+  const float* Hp = t > 0 ? HsAll + (int64_t)l * lsz + (slab + (int64_t)(t - 1) * M) * H : nullptr;
+  int tm, ug;
+  constexpr int UPB = CfgGate::WAVES_N;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+    return;
+  const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
+  int kbeg, kend;
+  split_range(cin + (t > 0 ? H : 0), S, (int)blockIdx.y, CfgGate::BK, kbeg, kend);
+  Acc<CfgGate> acc;
+  acc.zero();
+  if (kbeg < kend) {
+    LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
+    LstmFwdA<H> la{X + (slab + (int64_t)t * M) * cin, Hp, M, cin, XDrop{}};
+    gemm_mainloop<CfgGate>(la, lb, m0, n0, kbeg, kend, acc, smem);
+  }
+  store_part<CfgGate>(acc, part_slab<CfgGate>(part, S, (int)blockIdx.y));
+}
+
+template <int H>
+__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restrict__ HsAll, float* __restrict__ CsAll,
+                                                               float* __restrict__ GsAll, int64_t lsz,
+                                                               const float* __restrict__ theta, int64_t tstride,
+                                                               FwdWave wv, int T, int M, int S,
+                                                               const float* __restrict__ part) {
+  int l, t, b0;
+  LayerOff lo;
+  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  int tm, ug;
+  constexpr int UPB = CfgGate::WAVES_N;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+    return;
+  Acc<CfgGate> acc;
+  acc.zero();
+  float* p0 = const_cast<float*>(part);
+  for (int q = 0; q < S; ++q) add_part<CfgGate>(acc, part_slab<CfgGate>(p0, S, q));
+  const int z = blockIdx.z;
+  const int64_t slab = (int64_t)z * T * M;
+  fwd_cell<H>(acc, theta + (int64_t)z * tstride, lo, GsAll + (int64_t)l * lsz * 4 + slab * (4 * H),
+              CsAll + (int64_t)l * lsz + slab * H, HsAll + (int64_t)l * lsz + slab * H, tm * CfgGate::BM, ug, t, M);
+}
+
+#ifndef SMAML_SPLIT_MAX
+#define SMAML_SPLIT_MAX 4  // split-K ways for small-grid LSTM steps (1 = off)
+#endif
+#ifndef SMAML_SPLIT_WGS
+#define SMAML_SPLIT_WGS 256  // split while the launch stays within this many workgroups
+#endif
+// Split count for a launch of `tiles` workgroup tiles over K (max over its problems): enough
+// workgroups for ~one per CU, each split keeping >= 4 K-tiles, bounded by the partial slab.
+static int small_grid_splits(int64_t tiles, int K, int bk, int64_t per_split_floats, int64_t cap_floats) {
+  int S = 1;
+  while (S < SMAML_SPLIT_MAX && tiles * (S * 2) <= SMAML_SPLIT_WGS && (K / bk) / (S * 2) >= 4 &&
+         per_split_floats * (S * 2) <= cap_floats)
+    S *= 2;
+  return S;
+}
+
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
@@ -348,6 +473,20 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     SMAML_DISPATCH_H(d.H, k_lstm_fwd_step_drop<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
                                                                                    tstride, wv, d.T, w.M, w.drop));
     return;
+  }
+  {
+    int kmax = 0;
+    for (int q = 0; q < wv.n; ++q) kmax = std::max(kmax, wv.lo[q].cin + (wv.t[q] > 0 ? d.H : 0));
+    const int64_t per = (int64_t)grid.x * grid.z * CfgGate::NTH * CfgGate::WTM * CfgGate::WTN * 16;
+    const int S = small_grid_splits((int64_t)wv.n * ntm * ngrp * w.Z, kmax, CfgGate::BK, per, w.wpart_floats);
+    if (S > 1) {
+      dim3 gp(grid.x, S, grid.z);
+      SMAML_DISPATCH_H(d.H, k_lstm_fwd_part<HT><<<gp, CfgGate::NTH, 0, s>>>(w.F, w.Hs, lsz, theta, tstride, wv,
+                                                                              d.T, w.M, S, w.wpart));
+      SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell<HT><<<grid, CfgGate::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
+                                                                               wv, d.T, w.M, S, w.wpart));
+      return;
+    }
   }
   SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
                                                                            wv, d.T, w.M, w.drop));
@@ -550,6 +689,49 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
   return fl;
 }
 
+// Cell backward of one BPTT tile (acc = dh from the fused K = 8H GEMM, head dh_T not yet added):
+// dc, dG (in place over G_t), the cell-state carry and (optionally) the kept dh.
+template <int H, class CfgNN>
+__device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, const float* Gz, float* dGz, float* __restrict__ dhz,
+                                         const float* __restrict__ Cz, const float* __restrict__ dHz,
+                                         float* __restrict__ dcz, int m0, int n0, int l, int t, int L, int T, int M) {
+  constexpr int G4 = 4 * H;
+  const bool first = (t == T - 1);
+  const bool head = first && l == L - 1;
+  const bool full = m0 + CfgNN::BM <= M;
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
+#pragma unroll
+  for (int i = 0; i < CfgNN::WTM; ++i)
+#pragma unroll
+  for (int jj = 0; jj < CfgNN::WTN; ++jj) {
+    const int j = n0 + acc_col<CfgNN>(jj);
+    const int rb = m0 + acc_row<CfgNN>(i, 0);
+    if (j >= H) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = rb + racc(r);
+      if (!full && m >= M) continue;
+      const uint32_t row = tM + (uint32_t)m;
+      const uint32_t oh = row * H + j;
+      const uint32_t og = row * G4 + j;
+      const uint32_t oc = (uint32_t)m * H + j;
+      const float dh = acc.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
+      const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
+      const float c = ldb(Cz, 4u * (oh));
+      const float tc = tanhf_(c);
+      const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+      const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
+      const float dct = dcin + dh * go * (1.f - tc * tc);
+      stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
+      stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
+      stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
+      stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
+      stb(dcz, 4u * (oc), dct * gf);
+      if (dhz) stb(dhz, 4u * (oh), dh);
+    }
+  }
+}
+
 // GsAll: gates in; dGAll: dG out (== GsAll: in place) and the neighbours' dG read by the GEMM;
 // dhAll (optional): the step's dh kept for the second-order sweep ([L][Z][T][M][H]).
 // DROP: the layer-above segment carries dX of layer l+1's input drop(h_l): its contribution
@@ -598,41 +780,67 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
       if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
   }
-  const bool first = (t == T - 1);
-  const bool head = first && l == L - 1;
-  const float* dHz = dHhead + (int64_t)z * M * H;
-  const bool full = m0 + CfgNN::BM <= M;
-  const uint32_t tM = (uint32_t)t * (uint32_t)M;
-#pragma unroll
-  for (int i = 0; i < CfgNN::WTM; ++i)
-#pragma unroll
-  for (int jj = 0; jj < CfgNN::WTN; ++jj) {
-    const int j = n0 + acc_col<CfgNN>(jj);
-    const int rb = m0 + acc_row<CfgNN>(i, 0);
-    if (j >= H) continue;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = rb + racc(r);
-      if (!full && m >= M) continue;
-      const uint32_t row = tM + (uint32_t)m;
-      const uint32_t oh = row * H + j;
-      const uint32_t og = row * G4 + j;
-      const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = acc.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
-      const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
-      const float c = ldb(Cz, 4u * (oh));
-      const float tc = tanhf_(c);
-      const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-      const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
-      const float dct = dcin + dh * go * (1.f - tc * tc);
-      stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
-      stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
-      stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
-      stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
-      stb(dcz, 4u * (oc), dct * gf);
-      if (dhz) stb(dhz, 4u * (oh), dh);
-    }
+  bwd_cell<H, CfgNN>(acc, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, l, t, L, T, M);
+}
+
+// Split-K BPTT step for small grids (see k_lstm_fwd_part): partial dh over a K-tile range of the
+// fused [above | next] GEMM, then k_lstm_bwd_cell sums the partials in order and runs bwd_cell.
+template <int H, class CfgNN>
+__global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_part(const float* dGAll, int64_t lsz,
+                                                                            const float* __restrict__ theta,
+                                                                            int64_t tstride, BwdWave wv, int L, int T,
+                                                                            int M, int S, float* __restrict__ part) {
+  __shared__ float smem[CfgNN::SMEM_FLOATS];
+  constexpr int G4 = 4 * H;
+  const int p = wave_index(wv, (int)blockIdx.x);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const LayerOff lo = wave_sel(wv.lo, p);
+  const int64_t wih_up = wave_sel(wv.wih_up, p);
+  const int z = blockIdx.z;
+  const int m0 = ((int)blockIdx.x - b0) * CfgNN::BM, n0 = blockIdx.y % ((H + CfgNN::BN - 1) / CfgNN::BN) * CfgNN::BN;
+  const int split = blockIdx.y / ((H + CfgNN::BN - 1) / CfgNN::BN);
+  const int64_t slab = (int64_t)z * T * M;
+  const float* th = theta + (int64_t)z * tstride;
+  const bool up = l + 1 < L, nx = t + 1 < T;
+  const float* pa = dGAll + (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
+  const float* pn = dGAll + (int64_t)l * lsz * 4 + (slab + (int64_t)(t + 1) * M) * G4;
+  const int ns = (up ? 1 : 0) + (nx ? 1 : 0);
+  int kbeg, kend;
+  split_range(ns * G4, S, split, CfgNN::BK, kbeg, kend);
+  Acc<CfgNN> acc;
+  acc.zero();
+  if (kbeg < kend) {
+    SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
+    SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
+    gemm_mainloop<CfgNN>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
+  // slab of (z, y = split * ntn + tn, x)
+  constexpr int PER = CfgNN::WTM * CfgNN::WTN * 16 * CfgNN::NTH;
+  store_part<CfgNN>(acc, part + (((int64_t)z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PER);
+}
+
+template <int H, class CfgNN>
+__global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell(const float* GsAll, float* dGAll,
+                                                             float* __restrict__ dhAll, const float* __restrict__ CsAll,
+                                                             const float* __restrict__ dHhead,
+                                                             float* __restrict__ dcAll, int64_t lsz, BwdWave wv, int L,
+                                                             int T, int M, int S, const float* __restrict__ part) {
+  constexpr int G4 = 4 * H;
+  const int p = wave_index(wv, (int)blockIdx.x);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const int z = blockIdx.z;
+  const int ntn = gridDim.y;
+  const int m0 = ((int)blockIdx.x - b0) * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
+  Acc<CfgNN> acc;
+  acc.zero();
+  // the part kernel's grid is (x, S * ntn, z): its slab of (x, split * ntn + tn, z)
+  constexpr int PER = CfgNN::WTM * CfgNN::WTN * 16 * CfgNN::NTH;
+  for (int q = 0; q < S; ++q)
+    add_part<CfgNN>(acc, part + (((int64_t)z * (S * ntn) + q * ntn + blockIdx.y) * gridDim.x + blockIdx.x) * PER);
+  const int64_t slab = (int64_t)z * T * M;
+  bwd_cell<H, CfgNN>(acc, GsAll + (int64_t)l * lsz * 4 + slab * G4, dGAll + (int64_t)l * lsz * 4 + slab * G4,
+                     dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr, CsAll + (int64_t)l * lsz + slab * H,
+                     dHhead + (int64_t)z * M * H, dcAll + ((int64_t)l * gridDim.z + z) * M * H, m0, n0, l, t, L, T, M);
 }
 
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
@@ -656,6 +864,19 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
     const int ntms = (w.M + CfgNNs::BM - 1) / CfgNNs::BM, ntns = (d.H + CfgNNs::BN - 1) / CfgNNs::BN;
     bwd_wave(d, w, po, e, ntms, false, wv);
     dim3 grid(wv.off[wv.n], ntns, w.Z);
+    if (!w.drop.lstm()) {
+      constexpr int64_t PER = CfgNNs::WTM * CfgNNs::WTN * 16 * CfgNNs::NTH;
+      const int S = small_grid_splits((int64_t)grid.x * ntns * w.Z, 8 * d.H, CfgNNs::BK,
+                                      (int64_t)grid.x * ntns * w.Z * PER, w.wpart_floats);
+      if (S > 1) {
+        dim3 gp(grid.x, S * ntns, w.Z);
+        SMAML_DISPATCH_H(d.H, (k_lstm_bwd_part<HT, CfgNNs><<<gp, CfgNNs::NTH, 0, s>>>(w.dG, lsz, theta, tstride, wv,
+                                                                                       d.L, d.T, w.M, S, w.wpart)));
+        SMAML_DISPATCH_H(d.H, (k_lstm_bwd_cell<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
+                                  w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, wv, d.L, d.T, w.M, S, w.wpart)));
+        return;
+      }
+    }
     if (w.drop.lstm()) {
       SMAML_BWD_STEP(CfgNNs, true);
     } else {
