@@ -224,7 +224,7 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
 // Cell epilogue of one gate tile (acc = the i, f, g, o pre-activations of 32 units x 32 rows
 // per wave, bias not yet added): gates, c_t = f c_{t-1} + i g, h_t = o tanh(c_t).
-template <int H>
+template <int H, bool PRE = false>
 __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* __restrict__ th, const LayerOff& lo,
                                          float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
                                          int m0, int ug, int t, int M) {
@@ -237,6 +237,16 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
   const int rb = m0 + acc_row<CfgGate>(0, 0);
   const bool full = m0 + CfgGate::BM <= M;
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
+  // PRE: c_{t-1} of all 16 rows before the first store: the stores (slab t) cannot alias these
+  // loads (slab t-1), but the compiler cannot prove it and serialises load latency row by row.
+  float cpv[16];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = rb + racc(r);
+      cpv[r] = (t > 0 && (full || m < M)) ? ldb(Cz, 4u * ((tM - (uint32_t)M + (uint32_t)m) * H + j)) : 0.f;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = rb + racc(r);
@@ -248,7 +258,7 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
     const float gf = sigmoidf_(acc.v[0][1][r] + bsum[1]);
     const float gg = tanhf_(acc.v[0][2][r] + bsum[2]);
     const float go = sigmoidf_(acc.v[0][3][r] + bsum[3]);
-    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+    const float cp = PRE ? cpv[r] : (t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f);
     const float c = gf * cp + gi * gg;
     const float h = go * tanhf_(c);
     stb(Gz, 4u * (og), gi);
@@ -299,7 +309,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   }
 
-  fwd_cell<H>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
+  fwd_cell<H, SMAML_EPI_PRELOAD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
 }
 
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
@@ -439,7 +449,7 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restric
   for (int q = 0; q < S; ++q) add_part<CfgGate>(acc, part_slab<CfgGate>(p0, S, q));
   const int z = blockIdx.z;
   const int64_t slab = (int64_t)z * T * M;
-  fwd_cell<H>(acc, theta + (int64_t)z * tstride, lo, GsAll + (int64_t)l * lsz * 4 + slab * (4 * H),
+  fwd_cell<H, true>(acc, theta + (int64_t)z * tstride, lo, GsAll + (int64_t)l * lsz * 4 + slab * (4 * H),
               CsAll + (int64_t)l * lsz + slab * H, HsAll + (int64_t)l * lsz + slab * H, tm * CfgGate::BM, ug, t, M);
 }
 
@@ -691,7 +701,7 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 
 // Cell backward of one BPTT tile (acc = dh from the fused K = 8H GEMM, head dh_T not yet added):
 // dc, dG (in place over G_t), the cell-state carry and (optionally) the kept dh.
-template <int H, class CfgNN>
+template <int H, class CfgNN, bool PRE = false>
 __device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, const float* Gz, float* dGz, float* __restrict__ dhz,
                                          const float* __restrict__ Cz, const float* __restrict__ dHz,
                                          float* __restrict__ dcz, int m0, int n0, int l, int t, int L, int T, int M) {
@@ -707,6 +717,51 @@ __device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, const float* Gz,
     const int j = n0 + acc_col<CfgNN>(jj);
     const int rb = m0 + acc_row<CfgNN>(i, 0);
     if (j >= H) continue;
+    if constexpr (PRE) {
+    // operands of 4 rows are loaded before their stores (each (row, unit) is read and then
+    // overwritten by this lane only; the compiler cannot prove the in-place dG stores do not
+    // alias the next rows' loads, so without this it serialises their latency row by row)
+#pragma unroll
+    for (int r0 = 0; r0 < 16; r0 += 4) {
+      float v[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = rb + racc(r0 + q);
+        const bool ok = full || m < M;
+        const uint32_t row = tM + (uint32_t)m;
+        const uint32_t oh = row * H + j, og = row * G4 + j, oc = (uint32_t)m * H + j;
+        v[q][0] = ok && head ? ldb(dHz, 4u * oc) : 0.f;
+        v[q][1] = ok ? ldb(Gz, 4u * og) : 0.f;
+        v[q][2] = ok ? ldb(Gz, 4u * (og + H)) : 0.f;
+        v[q][3] = ok ? ldb(Gz, 4u * (og + 2 * H)) : 0.f;
+        v[q][4] = ok ? ldb(Gz, 4u * (og + 3 * H)) : 0.f;
+        v[q][5] = ok ? ldb(Cz, 4u * oh) : 0.f;
+        v[q][6] = ok && t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+        v[q][7] = ok && !first ? ldb(dcz, 4u * oc) : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + q;
+        const int m = rb + racc(r);
+        if (!full && m >= M) continue;
+        const uint32_t row = tM + (uint32_t)m;
+        const uint32_t oh = row * H + j;
+        const uint32_t og = row * G4 + j;
+        const uint32_t oc = (uint32_t)m * H + j;
+        const float dh = acc.v[i][jj][r] + v[q][0];
+        const float gi = v[q][1], gf = v[q][2], gg = v[q][3], go = v[q][4];
+        const float tc = tanhf_(v[q][5]);
+        const float cp = v[q][6];
+        const float dct = v[q][7] + dh * go * (1.f - tc * tc);
+        stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
+        stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
+        stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
+        stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
+        stb(dcz, 4u * (oc), dct * gf);
+        if (dhz) stb(dhz, 4u * (oh), dh);
+      }
+    }
+    } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = rb + racc(r);
@@ -728,6 +783,7 @@ __device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, const float* Gz,
       stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
       stb(dcz, 4u * (oc), dct * gf);
       if (dhz) stb(dhz, 4u * (oh), dh);
+    }
     }
   }
 }
@@ -780,7 +836,7 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
       if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
   }
-  bwd_cell<H, CfgNN>(acc, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, l, t, L, T, M);
+  bwd_cell<H, CfgNN, SMAML_EPI_PRELOAD != 0>(acc, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, l, t, L, T, M);
 }
 
 // Split-K BPTT step for small grids (see k_lstm_fwd_part): partial dh over a K-tile range of the
@@ -838,7 +894,7 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell(const float* GsAll
   for (int q = 0; q < S; ++q)
     add_part<CfgNN>(acc, part + (((int64_t)z * (S * ntn) + q * ntn + blockIdx.y) * gridDim.x + blockIdx.x) * PER);
   const int64_t slab = (int64_t)z * T * M;
-  bwd_cell<H, CfgNN>(acc, GsAll + (int64_t)l * lsz * 4 + slab * G4, dGAll + (int64_t)l * lsz * 4 + slab * G4,
+  bwd_cell<H, CfgNN, true>(acc, GsAll + (int64_t)l * lsz * 4 + slab * G4, dGAll + (int64_t)l * lsz * 4 + slab * G4,
                      dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr, CsAll + (int64_t)l * lsz + slab * H,
                      dHhead + (int64_t)z * M * H, dcAll + ((int64_t)l * gridDim.z + z) * M * H, m0, n0, l, t, L, T, M);
 }

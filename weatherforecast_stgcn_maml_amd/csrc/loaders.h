@@ -48,6 +48,10 @@
 #ifndef SMAML_WGRAD_THREADS
 #define SMAML_WGRAD_THREADS (2048 * 256)  // split-K target: total threads of one weight-gradient launch
 #endif
+#ifndef SMAML_EPI_PRELOAD
+#define SMAML_EPI_PRELOAD 0  // fused step kernels: issue a row group's epilogue loads before its stores
+                             // (always on in the split-K cell kernels; spills the primal BPTT step)
+#endif
 #ifndef SMAML_TN_BK
 #define SMAML_TN_BK 16
 #endif
