@@ -189,6 +189,12 @@ struct smaml_ctx {
   float* so_F = nullptr;  // [K][Z][T][M][Hc] GCN features of every inner step (null: recompute)
   int64_t so_F_cap = 0;
   float* F_main = nullptr;  // the workspace's own F buffer
+  // batch-1 adaptation: GCN features per window of task 0 (the frozen GCN stack without dropout
+  // is a pure function of the window, F2), filled on first use and reused by later epochs.
+  // Invalidated by smaml_set_graph / _set_gcn_params / _set_tasks.
+  float* ad_F = nullptr;
+  int64_t ad_cap = 0;              // windows the cache holds
+  std::vector<uint8_t> ad_valid;   // per window start
   float *Hs_main = nullptr, *Cs_main = nullptr, *Gs_main = nullptr;  // the workspace's own activations
   // primal of the last inner steps kept for the second-order sweep (ensure_keep): slot 0 adds
   // dG + dh to the workspace's Hs/Cs/Gs, slot i >= 1 holds Hs/Cs/Gs/dG/dh of its own
@@ -229,6 +235,8 @@ int free_keep(smaml_ctx* c) {
   return SMAML_OK;
 }
 
+static void ad_cache_drop(smaml_ctx* c);
+
 int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   const int zb = Z * B;
   // per-task activation slabs are addressed with 32-bit offsets inside the kernels
@@ -236,6 +244,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
     return fail(SMAML_EINVAL, "batch too large: T*B*N*4H must stay below 2^31 per task");
   so = so || c->so_cap;
   if (zb <= c->zb_cap && Z <= c->z_cap && so == c->so_cap) return SMAML_OK;
+  ad_cache_drop(c);  // a growing workspace takes precedence over the adaptation feature cache
   const int zbc = std::max(zb, c->zb_cap), zc = std::max(Z, c->z_cap);
   const Dims& d = c->d;
   const int64_t rows = (int64_t)zbc * d.T * d.N;
@@ -543,6 +552,13 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   return SMAML_OK;
 }
 
+static void ad_cache_drop(smaml_ctx* c) {
+  if (c->ad_F) (void)hipFree(c->ad_F);
+  c->ad_F = nullptr;
+  c->ad_cap = 0;
+  c->ad_valid.clear();
+}
+
 int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev) {
   TRY(run_gcn(c, s, xtab_dev));
   return run_lstm(c, s, theta, tstride);
@@ -769,6 +785,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->so_norm) (void)hipFree(c->so_norm);
   if (c->so_coef) (void)hipFree(c->so_coef);
   if (c->so_F) (void)hipFree(c->so_F);
+  ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
   for (auto& r : c->tm.recs) {
     (void)hipEventDestroy(r.a);
@@ -785,6 +802,7 @@ int smaml_set_graph(smaml_ctx* c, const int64_t* edge_index_host, int64_t num_ed
   std::vector<int32_t> cols;
   std::vector<float> vals;
   TRY(build_ell(edge_index_host, num_edges, c->d.N, cols, vals));
+  ad_cache_drop(c);
   if (!c->ell_c) {
     HIP_TRY(hipMalloc((void**)&c->ell_c, cols.size() * 4));
     HIP_TRY(hipMalloc((void**)&c->ell_v, vals.size() * 4));
@@ -799,6 +817,7 @@ int smaml_set_gcn_params(smaml_ctx* c, const float* gcn_flat) {
   if (!c || !gcn_flat) return fail(SMAML_EINVAL, "NULL argument");
   if (!aligned16(gcn_flat)) return fail(SMAML_EINVAL, "gcn params must be 16-byte aligned");
   c->gcn = gcn_flat;
+  ad_cache_drop(c);  // cached features belong to the previous GCN parameters
   return SMAML_OK;
 }
 
@@ -874,6 +893,7 @@ int smaml_forward(smaml_ctx* c, void* stream, const float* theta, const float* c
 }
 
 int smaml_set_tasks(smaml_ctx* c, int32_t ntasks, const float* const* features_host, const int32_t* t_total_host) {
+  if (c) ad_cache_drop(c);
   if (!c || ntasks <= 0 || !features_host || !t_total_host) return fail(SMAML_EINVAL, "bad set_tasks arguments");
   c->feats.assign(features_host, features_host + ntasks);
   c->t_total.assign(t_total_host, t_total_host + ntasks);
@@ -1032,16 +1052,43 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
   const float inv = 1.f / ((float)d.N * d.HfC * B);
   const bool dropout = c->p_gcn > 0.f || c->p_lstm > 0.f;
   if (dropout) TRY(upload_task_ids(c, s, 1));
+  // Batch-1 steps without GCN dropout reuse each window's GCN features across epochs (F2).
+  const int64_t fsz = (int64_t)d.T * d.N * d.Hc;  // floats of one window's features
+  bool cache = B == 1 && !(c->p_gcn > 0.f) && c->t_total[0] > 0;
+  if (cache && !c->ad_F) {
+    const int64_t n = c->t_total[0];
+    size_t freeb = 0, totb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totb));
+    if ((int64_t)freeb > n * fsz * 4 + (8ll << 30) && hipMalloc((void**)&c->ad_F, (size_t)(n * fsz * 4)) == hipSuccess) {
+      c->ad_cap = n;
+      c->ad_valid.assign((size_t)n, 0);
+    } else {
+      (void)hipGetLastError();
+      c->ad_F = nullptr;
+    }
+  }
+  cache = cache && c->ad_F;
   for (int k = 0; k < nsteps; ++k) {
     const float* const* xt = c->xtab + (int64_t)k * B;
     if (dropout) set_step_drop(c, step0 + k);
-    TRY(run_forward(c, s, theta, 0, xt));
+    if (cache) {
+      const int wv = windows_host[k];
+      c->w.F = c->ad_F + (int64_t)wv * fsz;
+      if (!c->ad_valid[wv]) {
+        TRY(run_gcn(c, s, xt));  // writes the window's features straight into its cache slot
+        c->ad_valid[wv] = 1;
+      }
+      TRY(run_lstm(c, s, theta, 0));
+    } else {
+      TRY(run_forward(c, s, theta, 0, xt));
+    }
     launch_head_loss(s, d, c->w, theta, 0, c->po, xt, 2.f * inv, true);
     launch_loss_final(s, c->w, inv, losses + k);
     TRY(run_backward(c, s, theta, 0, c->grad));
     launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
                    weight_decay, max_norm);
   }
+  c->w.F = c->F_main;
   c->w.drop = Drop{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
