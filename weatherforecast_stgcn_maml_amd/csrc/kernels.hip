@@ -309,7 +309,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   }
 
-  fwd_cell<H, SMAML_EPI_PRELOAD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
+  fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
 }
 
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,

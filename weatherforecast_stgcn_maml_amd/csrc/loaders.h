@@ -52,6 +52,9 @@
 #define SMAML_EPI_PRELOAD 0  // fused step kernels: issue a row group's epilogue loads before its stores
                              // (always on in the split-K cell kernels; spills the primal BPTT step)
 #endif
+#ifndef SMAML_EPI_PRELOAD_FWD
+#define SMAML_EPI_PRELOAD_FWD SMAML_EPI_PRELOAD  // same, for the fused forward step kernel
+#endif
 #ifndef SMAML_TN_BK
 #define SMAML_TN_BK 16
 #endif
