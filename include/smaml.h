@@ -152,7 +152,10 @@ int smaml_adamw_step(smaml_ctx* ctx, void* stream, float* theta, const float* gr
  * backward, clip_grad_norm_(max_norm), torch.optim.Adam with coupled L2 weight decay
  * (create_climate_optimizer, adaptive_scheduler.py:68-94) at learning rate lr_dev[k]
  * (device floats; ClimateAwareLRScheduler values) and Adam step step0+k+1.
- * theta, m, v: flat trainable vectors (device). losses [nsteps] (device): per-step MSE. */
+ * theta, m, v: flat trainable vectors (device). losses [nsteps] (device): per-step MSE.
+ * At batch 1 without GCN dropout each window's GCN features are cached on first use and reused
+ * by later calls (frozen GCN): call smaml_set_gcn_params again after changing the GCN
+ * parameters in place (it, smaml_set_graph and smaml_set_tasks drop the cache). */
 int smaml_adapt_steps(smaml_ctx* ctx, void* stream, float* theta, float* m, float* v, int32_t step0,
                       int32_t nsteps, int32_t batch, const int32_t* windows_host, const float* lr_dev,
                       float beta1, float beta2, float eps, float weight_decay, float max_norm,
