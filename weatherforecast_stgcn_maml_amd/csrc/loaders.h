@@ -46,7 +46,8 @@
 // tile (8 waves of 64 x 128), so the split-K slices read each [x | h] row once
 // (profiles/r01_ab_wgrad_tiles.log: 874 -> 798 ms/meta-step against 128 x 128, BK 32)
 #ifndef SMAML_WGRAD_THREADS
-#define SMAML_WGRAD_THREADS (2048 * 256)  // split-K target: total threads of one weight-gradient launch
+#define SMAML_WGRAD_THREADS (3072 * 256)  // split-K target: total threads of one weight-gradient launch
+                                          // (A/B at config 2: 2048 -> 3072 x 256: wgrad 747 -> 711 ms)
 #endif
 #ifndef SMAML_EPI_PRELOAD
 #define SMAML_EPI_PRELOAD 0  // fused step kernels: issue a row group's epilogue loads before its stores
