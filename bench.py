@@ -124,8 +124,28 @@ def measured_traffic(category, workload, world):
     return c
 
 
+def relaunch(args) -> int:
+    """``--gpus N`` without a torch.distributed launcher: start N ranks (one per GPU) through
+    torch.distributed.run as a child process, before this process touches the GPU, and return
+    its exit code (never an exec: see the contract in the module docstring)."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={os.environ.get('WORLD_SIZE')} but --gpus {args.gpus}")
     import torch
     import torch.distributed as dist
 
@@ -141,7 +161,8 @@ def main():
     # single-GPU box rehearse the N>1 path (the driver's 8-GPU runs use RCCL, one GPU each)
     dev_idx = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_idx)
-    init_from_env(os.environ.get("SMAML_DIST_BACKEND", "nccl"), torch.device("cuda", dev_idx))
+    backend = os.environ.get("SMAML_DIST_BACKEND", "nccl")
+    init_from_env(backend, torch.device("cuda", dev_idx))
     local = dev_idx
 
     d = ModelDims(num_nodes=args.nodes, hidden_channels=args.hidden_channels or 256)
@@ -180,10 +201,11 @@ def main():
     if not args.no_timing:
         ml.ctx.timing(False)
         kern = ml.ctx.timing_collect()
-    qmse = float(res.losses[-1].mean().item())
+    qsum = float(res.losses[-1].sum().item())
+    qmse = qsum / max(len(mine), 1)
     if world > 1:
         elapsed = max_over_ranks(elapsed, f"cuda:{local}")
-        q = torch.tensor([qmse * len(mine)], device=f"cuda:{local}", dtype=torch.float64)
+        q = torch.tensor([qsum], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(q)
         qmse = float(q.item()) / args.tasks
 
@@ -209,10 +231,12 @@ def main():
                         f"N={d.num_nodes} x C={d.input_channels}, Hc={d.hidden_channels}, "
                         f"LSTM {d.lstm_num_layers}x{d.lstm_hidden_size}, K={cfg.inner_steps} inner steps",
             "tasks": args.tasks, "batch": cfg.batch, "inner_steps": cfg.inner_steps,
-            "maml_order": cfg.order, "parallelism": f"task-sharded x{world} + RCCL all-reduce",
+            "maml_order": cfg.order,
+            "parallelism": (f"task-sharded x{world} + one {'RCCL' if backend == 'nccl' else backend} all-reduce "
+                            f"per meta-step" if world > 1 else "single GPU, no collective"),
             "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
             "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
-            "task_group": len(ml._groups[0][1]),
+            "task_group": len(ml._groups[0][1]) if ml._groups else 0,
             "dropout": list(args.dropout),
         },
         "meta_step_tflop": flops_meta / 1e12,

@@ -86,7 +86,7 @@ int64_t smaml_workspace_bytes(const smaml_ctx* ctx);
 
 /* Inner steps whose primal activations the last second-order smaml_meta_step kept for its
  * meta-backward sweep (tangent-only dual kernels there; the rest are recomputed). Sized to
- * free HBM, capped by the SMAML_KEEP environment variable. New; no reference counterpart. */
+ * free HBM, capped by smaml_set_option("keep") / the SMAML_KEEP environment variable. New; no reference counterpart. */
 int32_t smaml_so_kept_steps(const smaml_ctx* ctx);
 
 /* Train-mode dropout of smaml_meta_step / smaml_adapt_steps (replaces the nn.Dropout calls at
@@ -224,9 +224,25 @@ int smaml_comm_destroy(smaml_ctx* ctx);
 int smaml_timing(smaml_ctx* ctx, int32_t enable);
 
 /* Synchronise, then report and reset per category: summed kernel milliseconds, summed
- * algorithmic FLOPs, launch counts. Categories (index): 0 gcn_layer, 1 lstm_fwd_step,
- * 2 head_loss, 3 head_dh, 4 lstm_bwd_step, 5 wgrad (split-K + reduce), 6 dx, 7 misc. */
+ * algorithmic FLOPs, launch counts. One kernel symbol per category (index): 0 gcn_layer,
+ * 1 lstm_fwd_step, 2 lstm_fwd_dual, 3 head_loss, 4 head_dh, 5 lstm_bwd_step, 6 lstm_bwd_dual,
+ * 7 wgrad (split-K GEMM), 8 wgrad_reduce, 9 misc. */
 int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* count, int32_t cap);
+
+/* Launch counts per kernel variant (tile configuration) since the last reset, in the order of
+ * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_dual, fwd_dual_kept,
+ * bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept, bwd_dual_small,
+ * bwd_dual_small_kept. Writes min(cap, count) entries, *count = number of variants; reset != 0
+ * zeroes them. Host-side counters: no synchronisation. Lets tests assert which configurations ran. */
+int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
+
+/* Run-time knobs (tests / A-B; defaults = build-time values):
+ *   "bwd_big_min", "bwdd_big_min": primal / tangent BPTT launches with at least this many
+ *                                  64x128 tiles use them (else 64x64 or split-K tiles);
+ *   "split_max":                   split-K ways of small-grid LSTM steps (1 = off);
+ *   "keep":                        cap on second-order inner steps whose primal is kept
+ *                                  (-1 = the SMAML_KEEP environment variable / all that fit). */
+int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus
 }

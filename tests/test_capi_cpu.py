@@ -95,15 +95,28 @@ def test_create_fails_loudly_without_gpu():
 
 
 def test_window_table_reference_schedule():
+    """Support: the reference's 6 epochs x first 15 support samples at batch 1; query:
+    query_ds[0] = sample int(0.75 * min(600, len(dataset))) (train_hybrid_maml_v5.py:97-104,
+    162-164), e.g. 450 for a full 600-sample task."""
+    from weatherforecast_stgcn_maml_amd.maml import reference_query_start
     cfg = MamlConfig(inner_steps=90, batch=1, order=0, support_samples=15)
-    w = window_table(cfg, 2)
+    w = window_table(cfg, 2, query_start=reference_query_start(600))
     assert w.shape == (91, 2, 1)
     assert list(w[:, 0, 0][:16]) == list(range(15)) + [0]
-    assert w[-1, 0, 0] == 15
+    assert w[-1, 0, 0] == 450 and w[-1, 1, 0] == 450
+    assert reference_query_start(20) == 15 and reference_query_start(1000) == 450
+    w = window_table(cfg, 2, query_start=[7, 9])
+    assert list(w[-1, :, 0]) == [7, 9]
     cfg2 = MamlConfig(inner_steps=5, batch=32)
     w2 = window_table(cfg2, 15)
     assert w2[4, 3, 31] == 159 and w2[5, 0, 0] == 160
-    assert stream_len_for(cfg2, CONFIG2) == 160 + 32 + 24 + 8
+    # the bench's streams: the reference split puts the query batch right after the support
+    n = synth.num_samples(stream_len_for(cfg2, CONFIG2))
+    assert reference_query_start(n) == 160 and n - 160 >= 32
+    for K, B in [(2, 2), (2, 1), (1, 2), (10, 32)]:
+        c = MamlConfig(inner_steps=K, batch=B)
+        n = synth.num_samples(stream_len_for(c, CONFIG2))
+        assert reference_query_start(n) >= K * B and n - reference_query_start(n) >= B
 
 
 def test_shard_tasks_round_robin():

@@ -36,12 +36,12 @@ def worker(rank, world, port, out_q):
     r, w = D.init_from_env("gloo")
     assert (r, w) == (rank, world) and D.active()
     mine = D.shard_tasks(TASKS, r, w)
-    g = torch.zeros(P)
-    q = torch.zeros(1)
+    buf = torch.zeros(P + 1)  # MetaLearner's [meta-gradient | query-loss sum]: one collective
+    g, q = buf[:P], buf[P:]
     for j in mine:
         g += task_grad(j)
         q += 0.5 * (1.0 + 0.01 * j)
-    D.reduce_meta(g, q)
+    D.reduce_meta(buf)
     theta = {"p": torch.linspace(-1, 1, P)}
     state = {}
     refcpu.adamw_step(theta, {"p": g}, state, lr=1e-3)

@@ -196,7 +196,7 @@ def test_meta_step_matches_oracle_cfg2_batched():
     Pg = {k: v for k, v in PT.items() if k not in names}
     S = cfg.inner_steps * cfg.batch
     tasks = [refcpu.TaskData(f, ei, d) for f in feats]
-    ref = refcpu.meta_step({k: PT[k] for k in names}, Pg, tasks, list(range(S, S + cfg.batch)),
+    ref = refcpu.meta_step({k: PT[k] for k in names}, Pg, tasks, list(ml.default_windows()[-1, 0]),
                            cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, 1)
     losses = res.losses.cpu().numpy()
     for j in range(2):
@@ -343,7 +343,7 @@ def test_second_order_matches_oracle_cfg2(max_norm, keep, monkeypatch):
     Pg = {k: v for k, v in PT.items() if k not in names}
     S = cfg.inner_steps * cfg.batch
     tasks = [refcpu.TaskData(f, ei, d) for f in feats]
-    ref = refcpu.meta_step({k: PT[k] for k in names}, Pg, tasks, list(range(S, S + cfg.batch)),
+    ref = refcpu.meta_step({k: PT[k] for k in names}, Pg, tasks, list(ml.default_windows()[-1, 0]),
                            cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, 2)
     losses = res.losses.cpu().numpy()
     for j in range(2):
@@ -369,7 +369,7 @@ def test_second_order_matches_oracle_cfg5():
     PT = refcpu.to_torch(P)
     S = cfg.inner_steps * cfg.batch
     ref = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
-                           [refcpu.TaskData(feats[0], ei, d)], list(range(S, S + cfg.batch)),
+                           [refcpu.TaskData(feats[0], ei, d)], list(ml.default_windows()[-1, 0]),
                            cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, 2)
     q = float(res.losses[-1, 0].item())
     assert abs(q - ref["query_losses"][0]) < 1e-4 * ref["query_losses"][0]
@@ -419,7 +419,7 @@ def test_dropout_matches_oracle(order):
     PT = refcpu.to_torch(P)
     S = cfg.inner_steps * cfg.batch
     ref = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
-                           [refcpu.TaskData(f, ei, d) for f in feats], list(range(S, S + cfg.batch)),
+                           [refcpu.TaskData(f, ei, d) for f in feats], list(ml.default_windows()[-1, 0]),
                            cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, order,
                            dropout=(seed, 0.2, 0.2), task_ids=[3, 7])
     losses = res.losses.cpu().numpy()
@@ -453,3 +453,96 @@ def test_dropout_masks_follow_task_ids_not_groups():
         out.append((ml.meta_step().losses.cpu().numpy(), ml.meta_grad.cpu().numpy()))
     assert rel(out[1][0], out[0][0]) < 1e-6
     assert rel(out[1][1], out[0][1]) < 1e-5
+
+
+# ----------------------------------------------------------------------------- bench tile configs
+# The config-2 bench launches 4,420 BPTT workgroups per diagonal and runs the 64x128-tile
+# k_lstm_bwd_step / k_lstm_bwd_dual; launches under `bwd_big_min` (768) workgroups take the
+# 64x64 or split-K variants instead. These tests run every variant against the oracle and
+# assert through the library's launch counters (smaml_variant_counts) which ones ran.
+_ORACLE = {}
+
+
+def _oracle_meta_step(key, d, P, names, feats, ei, cfg, qidx):
+    if key not in _ORACLE:
+        PT = refcpu.to_torch(P)
+        S = cfg.inner_steps * cfg.batch
+        _ORACLE[key] = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
+                                        [refcpu.TaskData(f, ei, d) for f in feats], qidx, cfg.inner_steps,
+                                        cfg.batch, S, cfg.inner_lr, cfg.max_norm, cfg.order)
+    return _ORACLE[key]
+
+
+def _check_meta_step(res, ml, ref, d, names, n_tasks, K):
+    losses = res.losses.cpu().numpy()
+    for j in range(n_tasks):
+        assert rel(losses[:K, j], [r[0] for r in ref["step_records"][j]]) < 1e-5
+        assert abs(losses[-1, j] - ref["query_losses"][j]) < 1e-4 * ref["query_losses"][j]
+    mg = params.unpack(ml.meta_grad, d, 0)
+    for k in names:
+        assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
+
+
+@pytest.mark.parametrize("keep", [-1, 0, 1])
+def test_second_order_bench_tiles_b32(keep):
+    """1 task x B=32 x K=2 at config-2 shapes (M = 14,112 sequences): a diagonal with all 4
+    layers holds 4 x 221 = 884 >= 768 BPTT tiles, so the bench's 64x128 k_lstm_bwd_step and
+    k_lstm_bwd_dual run (kept-primal and recomputed-primal forms by `keep`); the short corner
+    diagonals run the 64x64 tiles. Per-step losses, query MSE and the second-order
+    meta-gradient against the oracle (train_hybrid_maml_v5.py:110-184 + torch autograd)."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=32, order=2)
+    P = synth.init_params(13, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1700, d.num_nodes, stream_len_for(cfg, d))]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=None)
+    ml.set_tasks(feats)
+    ml.ctx.set_option("keep", keep)
+    ml.ctx.variant_counts(reset=True)
+    res = ml.meta_step()
+    vc = ml.ctx.variant_counts()
+    assert vc["bwd_big"] > 0 and vc["bwd_small"] > 0, vc
+    if keep == 0:
+        assert vc["bwd_dual_big"] > 0 and vc["bwd_dual_big_kept"] == 0, vc
+    elif keep == 1:
+        assert vc["bwd_dual_big"] > 0 and vc["bwd_dual_big_kept"] > 0, vc
+    else:
+        assert ml.ctx.so_kept_steps() == 2
+        assert vc["bwd_dual_big"] == 0 and vc["bwd_dual_big_kept"] > 0, vc
+    ref = _oracle_meta_step("b32", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
+    _check_meta_step(res, ml, ref, d, names, 1, cfg.inner_steps)
+
+
+@pytest.mark.parametrize("tiles", ["big", "small", "split"])
+@pytest.mark.parametrize("keep", [-1, 0])
+def test_second_order_tile_variants_task_groups(tiles, keep):
+    """Every BPTT tile variant forced at config-2 shapes (B=1, K=2, 3 tasks run in task groups
+    of 2): 64x128 tiles (the bench's), 64x64 tiles, and the split-K small-grid steps."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=1, order=2)
+    P = synth.init_params(14, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1800 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(3)]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=2)
+    ml.set_tasks(feats)
+    assert len(ml._groups) == 2
+    big = 0 if tiles == "big" else 1 << 30
+    ml.ctx.set_option("bwd_big_min", big)
+    ml.ctx.set_option("bwdd_big_min", big)
+    ml.ctx.set_option("split_max", 4 if tiles == "split" else 1)
+    ml.ctx.set_option("keep", keep)
+    ml.ctx.variant_counts(reset=True)
+    res = ml.meta_step()
+    vc = ml.ctx.variant_counts()
+    dual = ("bwd_dual_big" if tiles == "big" else "bwd_dual_small") + ("_kept" if keep else "")
+    assert vc[dual] > 0, vc
+    if tiles == "big":
+        assert vc["bwd_big"] > 0 and vc["bwd_small"] == vc["bwd_split"] == 0, vc
+    elif tiles == "small":
+        assert vc["bwd_small"] > 0 and vc["bwd_big"] == vc["bwd_split"] == 0 and vc["fwd_split"] == 0, vc
+    else:
+        assert vc["bwd_split"] > 0 and vc["fwd_split"] > 0 and vc["bwd_big"] == 0, vc
+    ref = _oracle_meta_step("groups", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
+    _check_meta_step(res, ml, ref, d, names, 3, cfg.inner_steps)

@@ -22,9 +22,13 @@ EXPORTS = (
     "smaml_meta_step", "smaml_adamw_step", "smaml_adapt_steps", "smaml_timing", "smaml_timing_collect",
     "smaml_backward", "smaml_gcn_forward", "smaml_lstm_forward", "smaml_lstm_backward", "smaml_head_loss",
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
-    "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy",
+    "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy", "smaml_variant_counts", "smaml_set_option",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
+
+# kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
+VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_dual", "fwd_dual_kept", "bwd_big", "bwd_small", "bwd_split",
+            "bwd_dual_big", "bwd_dual_big_kept", "bwd_dual_small", "bwd_dual_small_kept")
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",
@@ -98,6 +102,8 @@ _SIGS = {
     "smaml_comm_destroy": ([P], I32),
     "smaml_timing_collect": ([P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               PI64, I32], I32),
+    "smaml_variant_counts": ([P, PI64, I32, PI32, I32], I32),
+    "smaml_set_option": ([P, ctypes.c_char_p, I64], I32),
 }
 
 
@@ -311,6 +317,18 @@ class Context:
         check(self._L.smaml_timing_collect(self._h, ms, fl, cnt, n))
         return {name: {"ms": ms[i], "flops": fl[i], "launches": cnt[i]}
                 for i, name in enumerate(TIMING_CATEGORIES)}
+
+    def variant_counts(self, reset: bool = False):
+        """{variant: launches} since the last reset (host counters, no sync)."""
+        n = len(VARIANTS)
+        buf = (ctypes.c_int64 * n)()
+        cnt = ctypes.c_int32()
+        check(self._L.smaml_variant_counts(self._h, buf, n, ctypes.byref(cnt), 1 if reset else 0))
+        assert cnt.value == n, (cnt.value, n)
+        return {name: int(buf[i]) for i, name in enumerate(VARIANTS)}
+
+    def set_option(self, key: str, value: int):
+        check(self._L.smaml_set_option(self._h, key.encode(), int(value)))
 
     def adamw_step(self, stream, theta, grad, m, v, step, lr, betas, eps, wd, max_norm, norm_out=None):
         check(self._L.smaml_adamw_step(self._h, stream, ptr(theta), ptr(grad), ptr(m), ptr(v),

@@ -31,15 +31,29 @@ def up_to_date() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
-    """Compile libsmaml.so; ``defines`` (e.g. ["SMAML_GATE_BK=16"]) build A/B variants."""
+    """Compile libsmaml.so (one hipcc per translation unit, in parallel, then link);
+    ``defines`` (e.g. ["SMAML_GATE_BK=16"]) build A/B variants."""
     if not force and not defines and out == OUT and up_to_date():
         return out
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(REPO, "include"), "-I", CSRC, *[f"-D{d}" for d in defines], *SOURCES,
-           "-o", out + ".tmp"]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(REPO, "include"),
+             "-I", CSRC, *[f"-D{d}" for d in defines]]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = f"{out}.{os.path.basename(src)}.o"
+        cmd = [hipcc(), *flags, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", out + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        print(" ".join(link))
+    subprocess.run(link, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(out + ".tmp", out)
     return out
 

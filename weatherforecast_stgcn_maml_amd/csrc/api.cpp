@@ -152,6 +152,48 @@ struct Timer {
   }
 };
 
+// Pinned host staging ring for small host -> device uploads (window pointer tables, task ids):
+// each upload takes the next slot, waits only for that slot's previous copy (event), then issues
+// an async copy on the caller's stream -- no stream drain, the queue keeps running.
+struct Staging {
+  static constexpr int NSLOT = 4;
+  char* host[NSLOT] = {};
+  hipEvent_t evt[NSLOT] = {};
+  int64_t cap = 0;  // bytes per slot
+  int next = 0;
+  int upload(hipStream_t s, void* dev, const void* src, int64_t bytes) {
+    if (bytes > cap) {
+      TRY(release());
+      const int64_t c = std::max<int64_t>(bytes, 8192);
+      for (int i = 0; i < NSLOT; ++i) {
+        HIP_TRY(hipHostMalloc((void**)&host[i], c, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&evt[i], hipEventDisableTiming));
+      }
+      cap = c;
+    }
+    const int i = next;
+    next = (next + 1) % NSLOT;
+    HIP_TRY(hipEventSynchronize(evt[i]));  // this slot's previous copy has been consumed
+    std::memcpy(host[i], src, bytes);
+    HIP_TRY(hipMemcpyAsync(dev, host[i], bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(evt[i], s));
+    return SMAML_OK;
+  }
+  int release() {
+    for (int i = 0; i < NSLOT; ++i) {
+      if (evt[i]) {
+        HIP_TRY(hipEventSynchronize(evt[i]));
+        HIP_TRY(hipEventDestroy(evt[i]));
+      }
+      if (host[i]) HIP_TRY(hipHostFree(host[i]));
+      evt[i] = nullptr;
+      host[i] = nullptr;
+    }
+    cap = 0;
+    return SMAML_OK;
+  }
+};
+
 }  // namespace
 
 struct smaml_ctx {
@@ -172,11 +214,14 @@ struct smaml_ctx {
   float* grad = nullptr;
   float* scratch_loss = nullptr;  // [(steps+1)*Z] fallback when the caller passes no buffer
   int64_t scratch_loss_cap = 0;
-  // device pointer table for sample windows + pinned staging
+  // device pointer table for sample windows (uploaded through the pinned staging ring)
   const float** xtab = nullptr;
-  const float** xtab_pinned = nullptr;
   int64_t xtab_cap = 0;
-  hipEvent_t xtab_evt = nullptr;
+  Staging stage;
+  // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
+  int64_t vcount[NVAR] = {};
+  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX};
+  int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
   std::vector<int> t_total;
@@ -202,6 +247,7 @@ struct smaml_ctx {
   int keep_n = 0;
   int64_t keep_rows = 0;  // rows * L the slots were sized for
   int keep_tried_K = -1;
+  int keep_want = 0;  // slots the current second-order meta-step may use (<= keep_n)
   int keep_last = 0;  // slots the last second-order meta-step used
   // train-mode dropout (smaml_set_dropout / smaml_set_task_ids); p = 0: off
   float p_gcn = 0.f, p_lstm = 0.f;
@@ -378,8 +424,12 @@ int ensure_so_store(smaml_ctx* c, int K, int Z, int B) {
 int ensure_keep(smaml_ctx* c, int K, int Z, int B) {
   const Dims& d = c->d;
   int want = c->so_F ? K : 0;
-  if (const char* e = std::getenv("SMAML_KEEP")) want = std::min(want, std::max(0, std::atoi(e)));
+  if (c->keep_max >= 0)
+    want = std::min(want, c->keep_max);
+  else if (const char* e = std::getenv("SMAML_KEEP"))
+    want = std::min(want, std::max(0, std::atoi(e)));
   const int64_t rowsL = (int64_t)Z * B * d.T * d.N * d.L;
+  c->keep_want = want;
   if (want <= c->keep_n && rowsL <= c->keep_rows) return SMAML_OK;
   if (want == c->keep_tried_K && rowsL == c->keep_tried_rows) return SMAML_OK;  // already as many as fit
   TRY(free_keep(c));
@@ -438,9 +488,7 @@ void use_primal(smaml_ctx* c, int slot) {
 int upload_task_ids(smaml_ctx* c, hipStream_t s, int Z) {
   std::vector<int32_t> ids(Z);
   for (int z = 0; z < Z; ++z) ids[z] = z < (int)c->task_ids.size() ? c->task_ids[z] : z;
-  HIP_TRY(hipMemcpyAsync(c->task_id_dev, ids.data(), (size_t)Z * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipStreamSynchronize(s));  // ids is a stack buffer
-  return SMAML_OK;
+  return c->stage.upload(s, c->task_id_dev, ids.data(), (int64_t)Z * 4);  // pinned ring: no stream drain
 }
 
 void set_step_drop(smaml_ctx* c, int step) {
@@ -461,22 +509,16 @@ int ensure_xtab(smaml_ctx* c, int64_t n) {
   if (c->xtab) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipFree((void*)c->xtab));
-    HIP_TRY(hipHostFree((void*)c->xtab_pinned));
   }
   const int64_t cap = std::max<int64_t>(n, 1024);
   HIP_TRY(hipMalloc((void**)&c->xtab, cap * sizeof(float*)));
-  HIP_TRY(hipHostMalloc((void**)&c->xtab_pinned, cap * sizeof(float*), hipHostMallocDefault));
   c->xtab_cap = cap;
   return SMAML_OK;
 }
 
 int upload_xtab(smaml_ctx* c, hipStream_t s, const float* const* ptrs, int64_t n) {
   TRY(ensure_xtab(c, n));
-  HIP_TRY(hipEventSynchronize(c->xtab_evt));  // previous upload has consumed the staging table
-  std::memcpy((void*)c->xtab_pinned, ptrs, n * sizeof(float*));
-  HIP_TRY(hipMemcpyAsync((void*)c->xtab, c->xtab_pinned, n * sizeof(float*), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipEventRecord(c->xtab_evt, s));
-  return SMAML_OK;
+  return c->stage.upload(s, (void*)c->xtab, ptrs, n * (int64_t)sizeof(float*));
 }
 
 void set_work(smaml_ctx* c, int Z, int B) {
@@ -488,6 +530,8 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.F = c->F_main;
   c->w.primal_kept = 0;
   c->w.drop = Drop{};  // dropout only inside smaml_meta_step / smaml_adapt_steps (set_step_drop)
+  c->w.vcount = c->vcount;
+  c->w.kn = c->kn;
   if (c->Hs_main) use_primal(c, SET_MAIN);
 }
 
@@ -685,7 +729,7 @@ extern "C" {
 
 const char* smaml_last_error(void) { return g_err.c_str(); }
 
-int32_t smaml_abi_version(void) { return 3; }
+int32_t smaml_abi_version(void) { return 4; }
 
 int smaml_param_layout(const smaml_dims* dims, int32_t which, int64_t* offsets, int64_t* sizes, int32_t cap,
                        int32_t* count, int64_t* total) {
@@ -758,8 +802,9 @@ int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out) {
     c->go.cin[k] = k == 0 ? d.Cin0 : d.Hc;
   }
   c->go.total = tot;
+  if (const char* e = std::getenv("SMAML_BWD_BIG_MIN")) c->kn.bwd_big_min = std::atoi(e);
+  if (const char* e = std::getenv("SMAML_BWDD_BIG_MIN")) c->kn.bwdd_big_min = std::atoi(e);
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->xtab_evt, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
     return fail(SMAML_EHIP, std::string("context init: ") + hipGetErrorString(e));
@@ -777,9 +822,8 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->ell_c) (void)hipFree(c->ell_c);
   if (c->ell_v) (void)hipFree(c->ell_v);
   if (c->xtab) (void)hipFree((void*)c->xtab);
-  if (c->xtab_pinned) (void)hipHostFree((void*)c->xtab_pinned);
+  (void)c->stage.release();
   if (c->scratch_loss) (void)hipFree(c->scratch_loss);
-  if (c->xtab_evt) (void)hipEventDestroy(c->xtab_evt);
   if (c->so_theta) (void)hipFree(c->so_theta);
   if (c->so_grad) (void)hipFree(c->so_grad);
   if (c->so_norm) (void)hipFree(c->so_norm);
@@ -921,7 +965,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z, B));
   if (order == 2) TRY(ensure_keep(c, steps, Z, B));
   set_work(c, Z, B);
-  const int nkeep = order == 2 ? std::min(c->keep_n, steps) : 0;
+  const int nkeep = order == 2 ? std::min(std::min(c->keep_n, c->keep_want), steps) : 0;
   c->keep_last = nkeep;
   // sample window table for every step (support steps then the query batch)
   const int64_t nptr = (int64_t)(steps + 1) * Z * B;
@@ -1121,6 +1165,33 @@ int smaml_timing_collect(smaml_ctx* c, double* ms, double* flops, int64_t* count
     c->tm.ms[i] = 0;
     c->tm.flops[i] = 0;
     c->tm.count[i] = 0;
+  }
+  return SMAML_OK;
+}
+
+int smaml_variant_counts(smaml_ctx* c, int64_t* counts, int32_t cap, int32_t* count, int32_t reset) {
+  if (!c || cap < 0 || (cap > 0 && !counts)) return fail(SMAML_EINVAL, "bad variant_counts arguments");
+  for (int i = 0; i < NVAR && i < cap; ++i) counts[i] = c->vcount[i];
+  if (count) *count = NVAR;
+  if (reset)
+    for (auto& v : c->vcount) v = 0;
+  return SMAML_OK;
+}
+
+int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
+  if (!c || !key) return fail(SMAML_EINVAL, "NULL argument");
+  const std::string k(key);
+  if (k == "bwd_big_min" && value >= 0) {
+    c->kn.bwd_big_min = (int)std::min<int64_t>(value, 1 << 30);
+  } else if (k == "bwdd_big_min" && value >= 0) {
+    c->kn.bwdd_big_min = (int)std::min<int64_t>(value, 1 << 30);
+  } else if (k == "split_max" && value >= 1) {
+    c->kn.split_max = (int)std::min<int64_t>(value, 64);
+  } else if (k == "keep" && value >= -1) {
+    c->keep_max = (int)std::min<int64_t>(value, 1 << 20);
+    c->keep_tried_K = -1;  // re-plan the kept slots on the next second-order meta-step
+  } else {
+    return fail(SMAML_EINVAL, "unknown option or bad value: " + k);
   }
   return SMAML_OK;
 }

@@ -72,9 +72,47 @@ struct Drop {
   __host__ __device__ bool lstm() const { return thr_lstm != 0; }
 };
 
+// Launch counters per kernel variant (tile configuration), read through smaml_variant_counts so
+// the parity tests can assert which configurations they exercised. Order = _capi.VARIANTS.
+enum Variant {
+  V_FWD = 0,         // k_lstm_fwd_step (fused gate GEMM + cell)
+  V_FWD_DROP,        // k_lstm_fwd_step_drop
+  V_FWD_SPLIT,       // k_lstm_fwd_part + k_lstm_fwd_cell (small grids)
+  V_FWDD,            // k_lstm_fwd_dual, primal recomputed
+  V_FWDD_KEPT,       // k_lstm_fwd_dual, tangent only (primal kept)
+  V_BWD_BIG,         // k_lstm_bwd_step, 64x128 tiles
+  V_BWD_SMALL,       // k_lstm_bwd_step, 64x64 tiles
+  V_BWD_SPLIT,       // k_lstm_bwd_part + k_lstm_bwd_cell (small grids)
+  V_BWDD_BIG,        // k_lstm_bwd_dual, 64x128 tiles, primal recomputed
+  V_BWDD_BIG_KEPT,   // k_lstm_bwd_dual, 64x128 tiles, tangent only
+  V_BWDD_SMALL,      // k_lstm_bwd_dual, 64x64 tiles, primal recomputed
+  V_BWDD_SMALL_KEPT, // k_lstm_bwd_dual, 64x64 tiles, tangent only
+  NVAR
+};
+
+// Build-time defaults of the run-time knobs below.
+#ifndef SMAML_BWD_BIG_MIN
+#define SMAML_BWD_BIG_MIN (3 * 256)  // BPTT launches with >= this many 64x128 tiles use them
+#endif
+#ifndef SMAML_BWDD_BIG_MIN
+#define SMAML_BWDD_BIG_MIN (3 * 256)
+#endif
+#ifndef SMAML_SPLIT_MAX
+#define SMAML_SPLIT_MAX 4  // split-K ways for small-grid LSTM steps (1 = off)
+#endif
+
+// Run-time tile-selection knobs (smaml_set_option; defaults = the build-time thresholds).
+struct Knobs {
+  int bwd_big_min;   // BPTT launches with >= this many 64x128 tiles use them (else 64x64 / split-K)
+  int bwdd_big_min;  // same, tangent BPTT
+  int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
+};
+
 // Activations of one forward pass for Z tasks x B samples (M = B*N sequences per task).
 struct Work {
   int Z, B, M;
+  int64_t* vcount;         // [NVAR] launch counters (ctx-owned; may be null)
+  Knobs kn;
   float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
   float* F;                // [Z][T][M][Hc] LSTM layer-0 input
   float *Hs, *Cs, *Gs;     // [L][Z][T][M][H] / [L][Z][T][M][H] / [L][Z][T][M][4H]
@@ -98,6 +136,10 @@ struct Work {
   Drop drop;
   float *hTd, *RhTd;
 };
+
+inline void count_variant(const Work& w, Variant v) {
+  if (w.vcount) ++w.vcount[v];
+}
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
 #ifndef SMAML_WGRAD_MAXSPLIT

@@ -453,17 +453,15 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restric
               CsAll + (int64_t)l * lsz + slab * H, HsAll + (int64_t)l * lsz + slab * H, tm * CfgGate::BM, ug, t, M);
 }
 
-#ifndef SMAML_SPLIT_MAX
-#define SMAML_SPLIT_MAX 4  // split-K ways for small-grid LSTM steps (1 = off)
-#endif
 #ifndef SMAML_SPLIT_WGS
 #define SMAML_SPLIT_WGS 256  // split while the launch stays within this many workgroups
 #endif
 // Split count for a launch of `tiles` workgroup tiles over K (max over its problems): enough
 // workgroups for ~one per CU, each split keeping >= 4 K-tiles, bounded by the partial slab.
-static int small_grid_splits(int64_t tiles, int K, int bk, int64_t per_split_floats, int64_t cap_floats) {
+static int small_grid_splits(int64_t tiles, int K, int bk, int64_t per_split_floats, int64_t cap_floats,
+                             int smax) {
   int S = 1;
-  while (S < SMAML_SPLIT_MAX && tiles * (S * 2) <= SMAML_SPLIT_WGS && (K / bk) / (S * 2) >= 4 &&
+  while (S < smax && tiles * (S * 2) <= SMAML_SPLIT_WGS && (K / bk) / (S * 2) >= 4 &&
          per_split_floats * (S * 2) <= cap_floats)
     S *= 2;
   return S;
@@ -480,6 +478,7 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
   if (w.drop.lstm()) {
+    count_variant(w, V_FWD_DROP);
     SMAML_DISPATCH_H(d.H, k_lstm_fwd_step_drop<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
                                                                                    tstride, wv, d.T, w.M, w.drop));
     return;
@@ -488,8 +487,10 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     int kmax = 0;
     for (int q = 0; q < wv.n; ++q) kmax = std::max(kmax, wv.lo[q].cin + (wv.t[q] > 0 ? d.H : 0));
     const int64_t per = (int64_t)grid.x * grid.z * CfgGate::NTH * CfgGate::WTM * CfgGate::WTN * 16;
-    const int S = small_grid_splits((int64_t)wv.n * ntm * ngrp * w.Z, kmax, CfgGate::BK, per, w.wpart_floats);
+    const int S = small_grid_splits((int64_t)wv.n * ntm * ngrp * w.Z, kmax, CfgGate::BK, per, w.wpart_floats,
+                                    w.kn.split_max);
     if (S > 1) {
+      count_variant(w, V_FWD_SPLIT);
       dim3 gp(grid.x, S, grid.z);
       SMAML_DISPATCH_H(d.H, k_lstm_fwd_part<HT><<<gp, CfgGate::NTH, 0, s>>>(w.F, w.Hs, lsz, theta, tstride, wv,
                                                                               d.T, w.M, S, w.wpart));
@@ -498,6 +499,7 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
       return;
     }
   }
+  count_variant(w, V_FWD);
   SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
                                                                            wv, d.T, w.M, w.drop));
 }
@@ -909,7 +911,8 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 #define SMAML_BWD_STEP(CFG, D_)                                                                               \
   SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
                             w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
-  if ((int64_t)wv.n * ntm * ntn * w.Z >= SMAML_BWD_BIG_MIN) {
+  if ((int64_t)wv.n * ntm * ntn * w.Z >= w.kn.bwd_big_min) {
+    count_variant(w, V_BWD_BIG);
     dim3 grid(wv.off[wv.n], ntn, w.Z);
     if (w.drop.lstm()) {
       SMAML_BWD_STEP(CfgBwd, true);
@@ -923,8 +926,9 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
     if (!w.drop.lstm()) {
       constexpr int64_t PER = CfgNNs::WTM * CfgNNs::WTN * 16 * CfgNNs::NTH;
       const int S = small_grid_splits((int64_t)grid.x * ntns * w.Z, 8 * d.H, CfgNNs::BK,
-                                      (int64_t)grid.x * ntns * w.Z * PER, w.wpart_floats);
+                                      (int64_t)grid.x * ntns * w.Z * PER, w.wpart_floats, w.kn.split_max);
       if (S > 1) {
+        count_variant(w, V_BWD_SPLIT);
         dim3 gp(grid.x, S * ntns, w.Z);
         SMAML_DISPATCH_H(d.H, (k_lstm_bwd_part<HT, CfgNNs><<<gp, CfgNNs::NTH, 0, s>>>(w.dG, lsz, theta, tstride, wv,
                                                                                        d.L, d.T, w.M, S, w.wpart)));
@@ -933,6 +937,7 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
         return;
       }
     }
+    count_variant(w, V_BWD_SMALL);
     if (w.drop.lstm()) {
       SMAML_BWD_STEP(CfgNNs, true);
     } else {

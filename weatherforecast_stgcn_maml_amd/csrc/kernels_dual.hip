@@ -185,6 +185,7 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
   const bool kept = w.primal_kept != 0, drop = w.drop.lstm();
+  count_variant(w, kept ? V_FWDD_KEPT : V_FWDD);
 #define SMAML_FWD_DUAL(K_, D_)                                                                  \
   SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, K_, D_><<<grid, CfgGateD::NTH, 0, s>>>(              \
                             w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
@@ -469,7 +470,8 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
   const bool kept = w.primal_kept != 0;
-  if ((int64_t)wv.n * ntm * ntn * w.Z >= SMAML_BWDD_BIG_MIN) {
+  if ((int64_t)wv.n * ntm * ntn * w.Z >= w.kn.bwdd_big_min) {
+    count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
     if (kept)
       bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
     else
@@ -477,6 +479,7 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   } else {
     const int ntms = (w.M + CfgNNDs::BM - 1) / CfgNNDs::BM, ntns = (d.H + CfgNNDs::BN - 1) / CfgNNDs::BN;
     bwd_wave(d, w, po, e, ntms, true, wv);
+    count_variant(w, kept ? V_BWDD_SMALL_KEPT : V_BWDD_SMALL);
     if (kept)
       bwd_dual_grid<CfgNNDs, true>(s, d, w, wv, ntns, theta, U, tstride);
     else

@@ -25,14 +25,6 @@
 #ifndef SMAML_BWD_BM
 #define SMAML_BWD_BM 64  // BPTT step tile rows (x 128 units)
 #endif
-// BPTT launches with at least this many 64x128 tiles use them, else 64x64 tiles (primal /
-// tangent kernels; A/B-able at build time)
-#ifndef SMAML_BWD_BIG_MIN
-#define SMAML_BWD_BIG_MIN (3 * 256)
-#endif
-#ifndef SMAML_BWDD_BIG_MIN
-#define SMAML_BWDD_BIG_MIN (3 * 256)
-#endif
 #ifndef SMAML_BWD_WM
 #define SMAML_BWD_WM 2
 #endif

@@ -1,5 +1,5 @@
 """Multi-GPU plumbing: one process per GPU, tasks sharded round-robin, ONE collective per
-meta-step (sum of the flat meta-gradient + the query-loss scalar), replicated outer update.
+meta-step (sum of the flat [meta-gradient | query-loss scalar] buffer), replicated outer update.
 
 Backend "nccl" is RCCL over xGMI on ROCm; "gloo" runs the same logic on CPU for tests.
 """
@@ -35,13 +35,12 @@ def shard_tasks(n_tasks: int, rank: int, world: int) -> List[int]:
     return [j for j in range(n_tasks) if j % world == rank]
 
 
-def reduce_meta(meta_grad: Optional[torch.Tensor], qsum: torch.Tensor, group=None):
-    """In place: meta_grad <- sum over ranks; qsum <- sum over ranks."""
+def reduce_meta(buf: torch.Tensor, group=None):
+    """In place: buf <- sum over ranks. ``buf`` is the flat [meta-gradient | query-loss sum]
+    buffer of MetaLearner (one collective per meta-step; just the scalar in reference mode)."""
     if not active():
         return
-    if meta_grad is not None:
-        dist.all_reduce(meta_grad, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(qsum, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
 
 
 def max_over_ranks(x: float, device) -> float:

@@ -24,24 +24,38 @@ from .config import MamlConfig, ModelDims
 from .distributed import reduce_meta, shard_tasks  # noqa: F401  (shard_tasks re-exported)
 
 
+def reference_query_start(n_samples: int) -> int:
+    """First query sample of a task with ``n_samples`` windows: the reference splits
+    ``min(600, len(dataset))`` samples 75/25 into support / query and queries ``query_ds[0]``
+    (train_hybrid_maml_v5.py:97-104,162-164)."""
+    return int(0.75 * min(600, n_samples))
+
+
 def window_table(cfg: MamlConfig, n_tasks: int, support: Optional[int] = None,
-                 query_start: Optional[int] = None) -> np.ndarray:
+                 query_start=None) -> np.ndarray:
     """int32 [(K+1)][tasks][B]: support step k uses samples (k*B + b) mod S (with B=1,
     S=15 this is the reference's 6 epochs x first 15 support samples, :124-127); the
-    query batch uses samples S .. S+B-1 (query_ds[0] when B=1, :162-164)."""
+    query batch uses samples q0 .. q0+B-1 (``query_ds[0]`` when B=1, :162-164). ``query_start``:
+    one int or one per task (default S; MetaLearner passes ``reference_query_start`` of each
+    task's stream)."""
     K, B = cfg.inner_steps, cfg.batch
     S = support or cfg.support_samples or K * B
-    q0 = S if query_start is None else query_start
+    q0 = np.broadcast_to(np.asarray(S if query_start is None else query_start, np.int64), (n_tasks,))
     w = np.empty((K + 1, n_tasks, B), np.int32)
     for k in range(K):
         w[k] = ((k * B + np.arange(B)) % S)[None, :]
-    w[K] = (q0 + np.arange(B))[None, :]
+    w[K] = q0[:, None] + np.arange(B)[None, :]
     return w
 
 
 def stream_len_for(cfg: MamlConfig, dims: ModelDims, support: Optional[int] = None) -> int:
+    """Shortest feature stream whose reference split (``reference_query_start``) puts the query
+    batch after the S support samples, with B query samples available."""
     S = support or cfg.support_samples or cfg.inner_steps * cfg.batch
-    return synth.t_total_for(S + cfg.batch, dims.window_size, dims.forecast_horizon)
+    n = S + cfg.batch
+    while reference_query_start(n) < min(S, 450) or n - reference_query_start(n) < cfg.batch:
+        n += 1
+    return synth.t_total_for(n, dims.window_size, dims.forecast_horizon)
 
 
 KEEP_MARGIN = 8 << 30   # matches api.cpp ensure_keep's free-HBM margin
@@ -110,22 +124,31 @@ class MetaLearner:
         self.ctx.set_gcn_params(self.gcn)
         self.theta = params.pack(theta, dims, which=0, device=self.device)
         P = self.theta.numel()
-        self.meta_grad = torch.zeros(P, device=self.device)
+        # ONE collective per meta-step: the meta-gradient and the query-loss sum share a buffer
+        self._reduce = torch.zeros(P + 64, device=self.device)
+        self.meta_grad = self._reduce[:P]
+        self._qsum = self._reduce[P:P + 1]
         self.m = torch.zeros(P, device=self.device)
         self.v = torch.zeros(P, device=self.device)
-        self.step = 0
+        self.step = 0          # outer (AdamW) steps taken
+        self.meta_steps = 0    # meta-steps run (any order): keys each meta-step's dropout masks
         self.pg = process_group
         self.tasks: List[torch.Tensor] = []
+        self._groups = []
 
     # tasks are [t_total, N, 24] float32 feature streams resident in HBM
     def set_tasks(self, features: Sequence, task_ids: Optional[Sequence[int]] = None):
-        """``task_ids``: global ids of these tasks (dropout mask keys; default 0..n-1)."""
+        """``task_ids``: global ids of these tasks (dropout mask keys; default 0..n-1). An empty
+        list is allowed (a rank with no task still joins the all-reduce with zeros)."""
         feats = []
         for f in features:
             t = f if torch.is_tensor(f) else torch.from_numpy(np.ascontiguousarray(f))
             feats.append(t.to(self.device, torch.float32).contiguous())
         self.tasks = feats
         self.task_ids = np.asarray(task_ids if task_ids is not None else np.arange(len(feats)), np.int32)
+        if not feats:
+            self._groups = []
+            return
         tg = self.task_group
         if tg == "auto":
             free, _ = torch.cuda.mem_get_info(self.device)
@@ -136,20 +159,31 @@ class MetaLearner:
         self.ctx.reserve(G, self.cfg.batch)
         self._mg_part = torch.zeros_like(self.meta_grad) if len(self._groups) > 1 else None
 
+    def default_windows(self) -> np.ndarray:
+        """The window table meta_step uses without an explicit one: support samples
+        (k*B + b) mod S, query batch from ``reference_query_start`` of each task's stream."""
+        n = [synth.num_samples(f.shape[0], self.dims.window_size, self.dims.forecast_horizon) for f in self.tasks]
+        return window_table(self.cfg, len(self.tasks), query_start=[reference_query_start(x) for x in n])
+
     def meta_step(self, windows: Optional[np.ndarray] = None, fast_out=None, sync=True,
                   lr: Optional[float] = None) -> StepResult:
         cfg = self.cfg
         Z = len(self.tasks)
-        if windows is None:
-            windows = window_table(cfg, Z)
+        if windows is None and Z:
+            windows = self.default_windows()
         K = cfg.inner_steps
         stream = _capi.stream_ptr(torch)
         if self.dropout != (0.0, 0.0):  # fresh masks every meta-step
             self.ctx.set_dropout(self.dropout[0], self.dropout[1],
-                                 (self.dropout_seed * 1000003 + self.step * 7919 + 1) & 0xFFFFFFFF)
+                                 (self.dropout_seed * 1000003 + self.meta_steps * 7919 + 1) & 0xFFFFFFFF)
         else:
             self.ctx.set_dropout(0.0, 0.0, 0)
-        if len(self._groups) == 1:
+        self.meta_steps += 1
+        if Z == 0:  # nothing sharded here: contribute zeros to the reduction
+            losses = torch.empty(K + 1, 0, device=self.device)
+            norms = torch.empty(max(K, 1), 0, device=self.device)
+            self._reduce.zero_()
+        elif len(self._groups) == 1:
             self.ctx.set_task_ids(self.task_ids)
             losses = torch.empty(K + 1, Z, device=self.device)
             norms = torch.empty(max(K, 1), Z, device=self.device)
@@ -175,8 +209,10 @@ class MetaLearner:
                 nparts.append(ng)
             losses = torch.cat(lparts, 1)
             norms = torch.cat(nparts, 1)
-        qsum = (losses[K].sum() * cfg.query_loss_scale).reshape(1)
-        reduce_meta(self.meta_grad if cfg.order >= 1 else None, qsum, self.pg)
+        if Z:
+            self._qsum.copy_((losses[K].sum() * cfg.query_loss_scale).reshape(1))
+        # one all_reduce of [meta_grad | query-loss sum] (just the scalar in reference mode)
+        reduce_meta(self._reduce if cfg.order >= 1 else self._qsum, self.pg)
         if cfg.order >= 1:
             self.step += 1
             norm_out = torch.empty(1, device=self.device)
@@ -187,7 +223,7 @@ class MetaLearner:
             norm_out = None
         if not sync:
             return StepResult(losses, norms, float("nan"), None)
-        return StepResult(losses, norms, float(qsum.item()),
+        return StepResult(losses, norms, float(self._qsum.item()),
                           float(norm_out.item()) if norm_out is not None else None)
 
     def theta_named(self):
