@@ -111,7 +111,9 @@ int smaml_gcn_conv(smaml_ctx* ctx, void* stream, const float* x, int32_t rows, i
 /* HybridSTGCN_LSTM.forward(x, edge_index) (hybrid_model.py:80-117) for `nsamples` samples:
  * x_host[s] = device pointer to sample s's x [T*N, input_channels] (time-major rows);
  * pred [nsamples][N*Hf][C] (rows n*Hf + h); feats (optional) [nsamples][T*N][Hc] = the
- * extract_base_features output (hybrid_model.py:60-78). */
+ * extract_base_features output (hybrid_model.py:60-78). With smaml_set_dropout p > 0 this is the
+ * train-mode forward (masks of (seed, task id 0 of smaml_set_task_ids, step 0)); the following
+ * smaml_backward applies the same masks. */
 int smaml_forward(smaml_ctx* ctx, void* stream, const float* theta, const float* const* x_host,
                   int32_t nsamples, float* pred, float* feats);
 
@@ -168,6 +170,11 @@ int smaml_adapt_steps(smaml_ctx* ctx, void* stream, float* theta, float* m, floa
  * What loss.backward() computes through HybridSTGCN_LSTM.forward (hybrid_model.py:80-117,
  * train_hybrid_maml_v5.py:134). Consumes the saved activations (ESTATE if there are none). */
 int smaml_backward(smaml_ctx* ctx, void* stream, const float* theta, const float* dpred, float* grad);
+
+/* In-place train-mode dropout of one STGCN conv output (model.py:33,36,39,42: after conv
+ * layer+1's ReLU, STGCN.forward): x [n] (device) gets the counter-based mask of the GCN site
+ * `layer` (0..3), seed `seed`, and the 1/(1-p) scale. */
+int smaml_dropout(smaml_ctx* ctx, void* stream, float* x, int64_t n, float p, uint32_t seed, int32_t layer);
 
 /* GCN x4 of extract_base_features (hybrid_model.py:60-78, no_grad): x_host[s] = device
  * pointer to sample s's window [T*N][Cin0] -> feats [nsamples][T*N][Hc] (device). */

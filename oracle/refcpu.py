@@ -14,6 +14,7 @@ absent from this image): it is restated from PyG 2.x's published ``gcn_norm`` +
 What each function follows:
   * ``gcn_conv``            PyG 2.x GCNConv (called at model.py:23-26, hybrid_model.py:65-74)
   * ``stgcn_features``      hybrid_model.py:60-78 (no_grad GCN x4 + ReLU, dropout p=0)
+  * ``stgcn_forward``       model.py:30-52 (STGCN's own forward: last time block + output_layer)
   * ``lstm_stack``          nn.LSTM(batch_first) semantics, gates [i,f,g,o] (hybrid_model.py:42-49,93-102)
   * ``hybrid_forward``      hybrid_model.py:80-117 (F3, F4 layouts)
   * ``mse``                 nn.MSELoss on the F4-permuted rows (train_hybrid_maml_v5.py:119,133)
@@ -21,6 +22,11 @@ What each function follows:
   * ``inner_loop``          train_hybrid_maml_v5.py:110-141 (SGD lr 0.01, batch of B samples)
   * ``meta_step``           train_hybrid_maml_v5.py:144-184 (+ FO / second-order meta-grad)
   * ``ReferencePort``       op-for-op mirror (per-node nn.LSTM loop, batch 1) for CPU timing
+  * ``regional_eval``       validate_hybrid_v5.py:189-237,337-358 (denormalised per-variable metrics),
+                            pinned to validateAdapted itself run on synthetic data (cfg*_validate.npz)
+  * ``climate_lr``          adaptive_scheduler.py:29-55 (ClimateAwareLRScheduler.step)
+  * ``adapt_reference``     adapt_hybrid_v5.py:152-231 (adaptModel's fine-tune + validation),
+                            pinned to adaptModel itself run on synthetic data (cfg4_adapt.npz)
   * ``Dropout``             train-mode dropout (hybrid_model.py:67,70,73,108; nn.LSTM dropout :47)
                             with the HIP path's counter-based masks (kernels.h drop_keep),
                             restated here so masks agree bit for bit; the reference draws its
@@ -124,6 +130,21 @@ def stgcn_features(x: torch.Tensor, edge_index: torch.Tensor, P: Dict[str, torch
         if drop is not None and k < 4:
             h = drop.gcn(h, k - 1, b, B)
     return h
+
+
+def stgcn_forward(x: torch.Tensor, edge_index: torch.Tensor, P: Dict[str, torch.Tensor], dims,
+                  drop: "Dropout" = None) -> torch.Tensor:
+    """model.STGCN.forward (model.py:30-52): conv1..conv4 + ReLU, dropout after EACH of the four
+    (train mode; drop = masks of kind 1, layers 0..3), last time block (x[-N:]), output_layer,
+    view(N, Hf, C).reshape(-1, C)."""
+    h = x
+    for k in range(1, 5):
+        h = F.relu(gcn_conv(h, edge_index, P[f"base_stgcn.conv{k}.lin.weight"], P[f"base_stgcn.conv{k}.bias"]))
+        if drop is not None:
+            h = drop.gcn(h, k - 1, 0, 1)
+    N = h.shape[0] // dims.window_size
+    out = h[-N:] @ P["base_stgcn.output_layer.weight"].t() + P["base_stgcn.output_layer.bias"]
+    return out.view(N, dims.forecast_horizon, dims.output_channels).reshape(-1, dims.output_channels)
 
 
 # ----------------------------------------------------------------------------- LSTM
@@ -365,6 +386,38 @@ class ReferencePort:
         return float(loss)
 
 
+# ----------------------------------------------------------------------------- evaluation
+def regional_eval(P: Dict[str, torch.Tensor], features: np.ndarray, edge_index, stats, dims, num_samples: int = 3):
+    """validate_hybrid_v5.validateAdapted's metric path (validate_hybrid_v5.py:189-237,337-358):
+    no-grad forward of the first min(3, len) windows, sample means (numpy, fp32), reshape both as
+    [Hf, N, 12] (the F4 pairing), node means, denormalise variables 0-5 with stats, MSE / MAE per
+    variable, average without sp."""
+    d = dims
+    T, Hf, N = d.window_size, d.forecast_horizon, d.num_nodes
+    n = min(num_samples, features.shape[0] - T - Hf)
+    ei = torch.as_tensor(np.asarray(edge_index)).long()
+    preds, trues = [], []
+    for i in range(n):
+        x, y = TaskData(features, ei.numpy(), d).xy(i)
+        with torch.no_grad():
+            preds.append(hybrid_forward(P, x, ei, d).numpy())
+        trues.append(y.numpy())
+    y_pred = np.mean(preds, axis=0).reshape(Hf, N, 12).mean(axis=1)
+    y_true = np.mean(trues, axis=0).reshape(Hf, N, 12).mean(axis=1)
+    mean, std = np.array(stats["mean"]), np.array(stats["std"])
+    names = ["u10", "v10", "t2m", "d2m", "sp", "tp"]
+    res, tot, cnt = {}, 0.0, 0
+    for v, name in enumerate(names):
+        t = y_true[:, v] * std[v] + mean[v]
+        p = y_pred[:, v] * std[v] + mean[v]
+        res[name] = {"mse": np.mean((p - t) ** 2), "mae": np.mean(np.abs(p - t))}
+        if name != "sp":
+            tot += res[name]["mse"]
+            cnt += 1
+    res["average_mse"] = tot / cnt
+    return res
+
+
 # ----------------------------------------------------------------------------- adaptation
 def climate_lr(region_name, epoch_idx, base_lr, epoch_loss):
     """adaptive_scheduler.ClimateAwareLRScheduler.step (adaptive_scheduler.py:29-55) after
@@ -383,12 +436,13 @@ def climate_lr(region_name, epoch_idx, base_lr, epoch_loss):
 
 
 def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_samples: int = 1200,
-                    base_lr: float = 0.0006, dropout=None):
+                    base_lr: float = 0.0006, dropout=None, orders=None):
     """adapt_hybrid_v5.adaptModel's fine-tuning loop (adapt_hybrid_v5.py:152-231): batch-1
-    samples in DataLoader(shuffle=True) order, MSE, backward, clip_grad_norm_(1.0),
-    torch.optim.Adam(lr, weight_decay) from create_climate_optimizer, scheduler per epoch,
-    then the validation MSE. Returns (params, epoch_losses, lrs, val_loss). dropout = (seed,
-    p_gcn, p_lstm): train-step masks keyed by the global step index (task id 0)."""
+    samples in DataLoader(shuffle=True) order (a real torch DataLoader draws it, as PyG's
+    loader does), MSE, backward, clip_grad_norm_(1.0), torch.optim.Adam(lr, weight_decay) from
+    create_climate_optimizer, scheduler per epoch, then the validation MSE. Returns (params,
+    epoch_losses, lrs, val_loss, step_losses). dropout = (seed, p_gcn, p_lstm): train-step masks
+    keyed by the global step index (task id 0). orders: optional per-epoch permutations."""
     n_all = task.features.shape[0] - task.dims.window_size - task.dims.forecast_horizon
     n_max = min(max_samples, n_all)
     n_train = int(0.8 * n_max)
@@ -401,11 +455,10 @@ def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_s
     opt = torch.optim.Adam(leaves, lr=lr0, weight_decay=wd)
     epoch_losses, lrs = [], []
     gstep = 0
+    loader = torch.utils.data.DataLoader(range(n_train), batch_size=1, shuffle=True)
+    step_losses = []
     for ep in range(epochs):
-        seed = int(torch.empty((), dtype=torch.int64).random_().item())
-        g = torch.Generator()
-        g.manual_seed(seed)
-        order = torch.randperm(n_train, generator=g).tolist()
+        order = list(orders[ep]) if orders is not None else [int(b) for b in loader]
         ls = []
         lrs.append(opt.param_groups[0]["lr"])
         for i in order:
@@ -419,9 +472,11 @@ def adapt_reference(Pt, Pg, task: TaskData, region_name: str, epochs: int, max_s
             ls.append(float(loss.detach()))
         avg = sum(ls) / len(ls)
         epoch_losses.append(avg)
+        step_losses.append(ls)
         new_lr = climate_lr(region_name, ep + 1, lr0, avg)
         for pg in opt.param_groups:
             pg["lr"] = new_lr
     with torch.no_grad():
         vals = [float(batch_loss(dict(zip(names, leaves)), Pg, task, [i])[0]) for i in range(n_train, n_max)]
-    return dict(zip(names, [l.detach() for l in leaves])), epoch_losses, lrs, sum(vals) / max(len(vals), 1)
+    return (dict(zip(names, [l.detach() for l in leaves])), epoch_losses, lrs, sum(vals) / max(len(vals), 1),
+            step_losses)

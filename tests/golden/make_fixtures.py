@@ -94,18 +94,31 @@ class DataStub:
         return DataStub(**{k: (v.to(device) if torch.is_tensor(v) else v) for k, v in self.__dict__.items()})
 
 
-class DataLoaderStub:
-    def __init__(self, ds, batch_size=1, shuffle=False, **kw):
-        assert batch_size == 1
-        self.ds, self.shuffle = ds, shuffle
+class _Recording(torch.utils.data.Dataset):
+    """Delegates to the wrapped dataset and records the indices the loader fetches."""
 
-    def __iter__(self):
-        order = torch.randperm(len(self.ds)).tolist() if self.shuffle else range(len(self.ds))
-        for i in order:
-            yield self.ds[i]
+    def __init__(self, ds, record):
+        self.ds, self.record = ds, record
 
     def __len__(self):
         return len(self.ds)
+
+    def __getitem__(self, i):
+        self.record.append(int(i))
+        return self.ds[i]
+
+
+class DataLoaderStub(torch.utils.data.DataLoader):
+    """PyG ``DataLoader`` at batch_size 1: it IS torch's DataLoader (PyG's subclasses it), so the
+    sampler and its draws from the global torch RNG are the real ones; the collate returns the
+    single ``Data`` object (PyG's Collater at batch 1 yields the same x, edge_index, y).
+    ``record`` holds the dataset indices in the order they were fetched."""
+
+    def __init__(self, dataset, batch_size=1, shuffle=False, **kw):
+        assert batch_size == 1
+        self.record = []
+        super().__init__(_Recording(dataset, self.record), batch_size=1, shuffle=shuffle,
+                         collate_fn=lambda b: b[0], **kw)
 
 
 def install_stubs():
@@ -119,6 +132,8 @@ def install_stubs():
     pyg_loader.DataLoader = DataLoaderStub
     xr = _module("xarray")
     xr.Dataset = object
+    xr.open_dataset = lambda path, *a, **kw: None   # replaced per fixture (validate)
+    xr.merge = lambda dss, *a, **kw: None
 
 
 def import_reference(ref_dir):
@@ -130,8 +145,13 @@ def import_reference(ref_dir):
     import graphBuilder as ref_graph  # noqa
     import embed_utils as ref_embed  # noqa
     import train_hybrid_maml_v5 as ref_train  # noqa
+    import adaptive_scheduler as ref_sched  # noqa
+    import adapt_hybrid_v5 as ref_adapt  # noqa
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    import validate_hybrid_v5 as ref_validate  # noqa
     return types.SimpleNamespace(model=ref_model, hybrid=ref_hybrid, dataset=ref_dataset,
-                                 graph=ref_graph, embed=ref_embed, train=ref_train)
+                                 graph=ref_graph, embed=ref_embed, train=ref_train, sched=ref_sched,
+                                 adapt=ref_adapt, validate=ref_validate)
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -331,9 +351,229 @@ def fixture_maml(R, d, name, feat_seed, param_seed, steps, batch, support, qbatc
     print("wrote", path)
 
 
+class _GridDS:
+    """The xarray Dataset surface adaptModel touches: coordinates for build_spatial_graph,
+    ``sizes`` for a print, and ``"day_of_year_sin" in ds`` (time features already present)."""
+
+    def __init__(self, d):
+        g = grid_ds(d)
+        self.latitude, self.longitude, self.sizes = g.latitude, g.longitude, {}
+
+    def __contains__(self, key):
+        return True
+
+
+def fixture_adapt(R, d, name, feat_seed, param_seed, n_samples, regions, sched_losses):
+    """adapt_hybrid_v5.adaptModel run UNMODIFIED on synthetic data (adapt_hybrid_v5.py:65-271):
+    the ERA5 loader / preprocessing are replaced by a synthetic feature stream, the checkpoint
+    load by an in-memory dict, torch.save by a capture; dropout is set to 0 (the parity setting:
+    STGCN dropout_rate, hard-coded 0.2 at :106, is overridden, lstm_dropout comes from the
+    checkpoint's hybrid_config). Records the per-epoch shuffle orders, per-step train losses,
+    the scheduler's learning rates, the validation MSE and the adapted parameters. Also pins
+    ClimateAwareLRScheduler / create_climate_optimizer (adaptive_scheduler.py:7-94) directly."""
+    import tempfile
+
+    params = synth.init_params(param_seed, d, gcn_bias_scale=0.1)
+    feats = torch.from_numpy(synth.make_features(feat_seed, d.num_nodes, synth.t_total_for(n_samples)))
+    out = {"param_seed": np.array(param_seed), "feat_seed": np.array(feat_seed), "n_samples": np.array(n_samples),
+           "regions": np.array(regions), "sched_losses": np.array(sched_losses)}
+    # -- the scheduler and optimizer factory on their own
+    for region in regions:
+        opt, lr0 = R.sched.create_climate_optimizer([torch.nn.Parameter(torch.zeros(1))], region)
+        sch = R.sched.ClimateAwareLRScheduler(opt, region, lr0)
+        out[f"sched/{region}/lr0"] = np.array(lr0)
+        out[f"sched/{region}/wd"] = np.array(opt.param_groups[0]["weight_decay"])
+        out[f"sched/{region}/lrs"] = np.array([sch.step(x) for x in sched_losses])
+    # -- the full adaptation loop
+    ckpt = {"config": {"input_channels": d.input_channels, "hidden_channels": d.hidden_channels,
+                       "output_channels": d.output_channels, "window_size": d.window_size,
+                       "forecast_horizon": d.forecast_horizon},
+            "hybrid_config": {"lstm_hidden_size": d.lstm_hidden_size, "lstm_num_layers": d.lstm_num_layers,
+                              "lstm_dropout": 0.0},
+            "hybrid_model_state_dict": {k: torch.from_numpy(v) for k, v in params.items()},
+            "koppen_embed_state_dict": {"embedding.weight": torch.zeros(31, 8)},
+            "model_version": "5.0", "total_params": int(sum(v.size for v in params.values()))}
+    stats = {"mean": np.zeros(12), "std": np.ones(12)}
+    saved, losses, loaders = {}, [], []
+    orig = dict(load=torch.load, save=torch.save, mse=torch.nn.MSELoss, stgcn=R.adapt.STGCN,
+                lda=R.adapt.load_adaptation_data, pmi=R.adapt.prepare_model_input,
+                sched=R.adapt.ClimateAwareLRScheduler, dl=R.adapt.DataLoader)
+
+    class RecMSE(orig["mse"]):
+        def forward(self, a, b):
+            out_ = super().forward(a, b)
+            losses.append(float(out_))
+            return out_
+
+    class RecSched(orig["sched"]):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            self.calls = []
+            saved["sched"] = self
+
+        def step(self, epoch_loss=None):
+            lr = super().step(epoch_loss)
+            self.calls.append((epoch_loss, lr))
+            return lr
+
+    class RecLoader(orig["dl"]):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            loaders.append(self)
+
+    for region in regions:
+        saved.clear()
+        losses.clear()
+        loaders.clear()
+        torch.load = lambda *a, **kw: ckpt
+        torch.save = lambda obj, path: saved.__setitem__("ckpt", obj)
+        torch.nn.MSELoss = RecMSE
+        R.adapt.STGCN = lambda **kw: orig["stgcn"](**dict(kw, dropout_rate=0.0))
+        R.adapt.load_adaptation_data = lambda coords: _GridDS(d)
+        R.adapt.prepare_model_input = lambda ds, code, emb, normalize=True, stats=None: (feats, stats_)
+        R.adapt.ClimateAwareLRScheduler = RecSched
+        R.adapt.DataLoader = RecLoader
+        stats_ = stats
+        cwd = os.getcwd()
+        try:
+            with tempfile.TemporaryDirectory() as tmp:
+                os.chdir(tmp)
+                torch.manual_seed(0)
+                R.adapt.adaptModel((18, 23, 75, 80), region)
+        finally:
+            os.chdir(cwd)
+            torch.load, torch.save, torch.nn.MSELoss = orig["load"], orig["save"], orig["mse"]
+            R.adapt.STGCN, R.adapt.load_adaptation_data = orig["stgcn"], orig["lda"]
+            R.adapt.prepare_model_input, R.adapt.ClimateAwareLRScheduler = orig["pmi"], orig["sched"]
+            R.adapt.DataLoader = orig["dl"]
+        train, val = loaders[0], loaders[1]
+        n_train, epochs = len(train.dataset), len(saved["sched"].calls)
+        order = np.array(train.record).reshape(epochs, n_train)
+        tag = f"adapt/{region}"
+        out[tag + "/orders"] = order
+        out[tag + "/train_losses"] = np.array(losses[:epochs * n_train]).reshape(epochs, n_train)
+        out[tag + "/val_losses"] = np.array(losses[epochs * n_train:])
+        out[tag + "/sched_calls"] = np.array(saved["sched"].calls)
+        out[tag + "/val_loss"] = np.array(saved["ckpt"]["val_loss"])
+        assert np.array(val.record).tolist() == list(range(len(val.dataset)))
+        for k, v in saved["ckpt"]["hybrid_model_state_dict"].items():
+            if k.startswith(("lstm.", "output_layer.")):
+                out[f"{tag}/adapted/{k}"] = v.numpy().copy()
+            else:  # the frozen GCN stack (no grads, F2) must come back unchanged
+                assert torch.equal(v, torch.from_numpy(params[k])), k
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **out)
+    print("wrote", path)
+
+
+class _Times:
+    def __init__(self, values):
+        self.values = values
+
+    def __len__(self):
+        return len(self.values)
+
+
+class _ValDS(_GridDS):
+    """The xarray surface validateAdapted touches (validate_hybrid_v5.py:137-170): region and
+    time selection, ``valid_time`` timestamps, ``"day_of_year_sin" in ds``."""
+
+    def __init__(self, d, n_times):
+        super().__init__(d)
+        self.valid_time = _Times(np.datetime64("2025-01-01T00") + np.arange(n_times).astype("timedelta64[h]"))
+
+    def sel(self, **kw):
+        return self
+
+    def isel(self, valid_time):
+        out = _ValDS.__new__(_ValDS)
+        out.__dict__.update(self.__dict__)
+        out.valid_time = _Times(self.valid_time.values[valid_time])
+        return out
+
+    def __getitem__(self, key):
+        return self.valid_time
+
+
+def fixture_validate(R, d, name, feat_seed, param_seed, n_times):
+    """validate_hybrid_v5.validateAdapted run UNMODIFIED on synthetic data (:113-371): the 2025
+    NetCDF reads are replaced by a coordinate/time surface, the checkpoint load by an in-memory
+    adapted checkpoint (with normalisation stats), prepare_model_input by the synthetic feature
+    stream of the selected time slice; plots go to a temporary directory. Records the returned
+    denormalised per-variable MSE / MAE and the average (sp excluded)."""
+    import tempfile
+
+    params = synth.init_params(param_seed, d, gcn_bias_scale=0.1)
+    T0 = max(0, n_times // 4)
+    T_sub = min(n_times, T0 + 50) - T0
+    feats = torch.from_numpy(synth.make_features(feat_seed, d.num_nodes, T_sub))
+    rng = np.random.default_rng(param_seed + 1)
+    stats = {"mean": np.array([1.5, -0.8, 285.0, 278.0, 101300.0, 0.0004, 2.1, -1.1, 3.0e5, 0.4, 0.5, -1e-5]),
+             "std": np.abs(rng.normal(size=12)) * np.array([3, 3, 8, 7, 900, 1e-3, 4, 4, 1e5, 0.3, 0.3, 1e-4]) + 1e-3}
+    ckpt = {"config": {"input_channels": d.input_channels, "hidden_channels": d.hidden_channels,
+                       "output_channels": d.output_channels, "window_size": d.window_size,
+                       "forecast_horizon": d.forecast_horizon},
+            "hybrid_config": {"lstm_hidden_size": d.lstm_hidden_size, "lstm_num_layers": d.lstm_num_layers,
+                              "lstm_dropout": 0.2},
+            "hybrid_model_state_dict": {k: torch.from_numpy(v) for k, v in params.items()},
+            "koppen_embed_state_dict": {"embedding.weight": torch.zeros(31, 8)}, "stats": stats}
+    V = R.validate
+    orig = dict(load=torch.load, open=V.xr.open_dataset, merge=V.xr.merge, pmi=V.prepare_model_input)
+    region, coords = "NewYork2025", (40, 45, 285, 290)
+    cwd = os.getcwd()
+    try:
+        with tempfile.TemporaryDirectory() as tmp:
+            os.chdir(tmp)
+            os.makedirs("Out_Data/AdaptedModels")
+            open(f"Out_Data/AdaptedModels/hybrid_v5_adapted_{region}_{coords}.pt", "wb").close()
+            torch.load = lambda *a, **kw: ckpt
+            V.xr.open_dataset = lambda path, *a, **kw: _ValDS(d, n_times)
+            V.xr.merge = lambda dss, *a, **kw: dss[0]
+            V.prepare_model_input = lambda ds, code, emb, normalize=True, stats=None: (feats, stats)
+            res = V.validateAdapted(coords, region)
+    finally:
+        os.chdir(cwd)
+        torch.load, V.xr.open_dataset, V.xr.merge = orig["load"], orig["open"], orig["merge"]
+        V.prepare_model_input = orig["pmi"]
+    out = {"param_seed": np.array(param_seed), "feat_seed": np.array(feat_seed), "n_times": np.array(n_times),
+           "t_sub": np.array(T_sub), "stats_mean": stats["mean"], "stats_std": stats["std"],
+           "average_mse": np.array(res["average_mse"]), "var_names": np.array(list(V.VAR_NAMES[:6]))}
+    for v in V.VAR_NAMES[:6]:
+        out[f"{v}/mse"] = np.array(res[v]["mse"])
+        out[f"{v}/mae"] = np.array(res[v]["mae"])
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **out)
+    print("wrote", path, "average_mse", float(res["average_mse"]))
+
+
+def fixture_stgcn_forward(R, name, dims_list, param_seed, feat_seed):
+    """model.STGCN.forward (model.py:30-52) in eval mode: conv1..4 + ReLU (+ dropout, off in
+    eval), last time block, output_layer, view(N, Hf, C).reshape(-1, C)."""
+    out = {"param_seed": np.array(param_seed), "feat_seed": np.array(feat_seed)}
+    for i, d in enumerate(dims_list):
+        params = synth.init_params(param_seed, d, gcn_bias_scale=0.1)
+        base = R.model.STGCN(in_channels=d.input_channels, hidden_channels=d.hidden_channels,
+                             out_channels=d.output_channels, window_size=d.window_size,
+                             forecast_horizon=d.forecast_horizon, dropout_rate=0.2)
+        base.load_state_dict({k[len("base_stgcn."):]: torch.from_numpy(v) for k, v in params.items()
+                              if k.startswith("base_stgcn.")})
+        base.eval()
+        ei, _, _ = R.graph.build_spatial_graph(grid_ds(d), k_neighbors=4)
+        x, _ = synth.sample_xy(synth.make_features(feat_seed, d.num_nodes, synth.t_total_for(1)), 0)
+        with torch.no_grad():
+            y = base(torch.from_numpy(np.ascontiguousarray(x)), ei)
+        out[f"d{i}/num_nodes"] = np.array(d.num_nodes)
+        out[f"d{i}/hidden_channels"] = np.array(d.hidden_channels)
+        out[f"d{i}/edge_index"] = ei.numpy().astype(np.int64)
+        out[f"d{i}/out"] = y.numpy()
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **out)
+    print("wrote", path)
+
+
 def main():
     ref_dir = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
-    which = sys.argv[2:] or ["cfg1", "maml", "cfg2"]
+    which = sys.argv[2:] or ["cfg1", "maml", "cfg2", "adapt", "stgcn", "validate"]
     R = import_reference(ref_dir)
     torch.manual_seed(0)
     if "cfg1" in which:
@@ -345,6 +585,15 @@ def main():
     if "cfg2" in which:
         fixture_forward_and_inner(R, CONFIG2, "cfg2_ref.npz", feat_seed=1000, param_seed=42,
                                   n_samples=4, inner_epochs=1, n_support=3, tasks=1, full=False)
+    if "adapt" in which:
+        fixture_adapt(R, CONFIG1, "cfg4_adapt.npz", feat_seed=4000, param_seed=17, n_samples=20,
+                      regions=["Thailand", "Moscow", "Delhi"],
+                      sched_losses=[1.4, 1.2, 0.9, 1.3, 0.15, 0.5, 1.1, 0.1, 0.7, 1.05, 0.19, 0.3, 2.0, 0.9, 0.05])
+    if "validate" in which:
+        fixture_validate(R, CONFIG1, "cfg1_validate.npz", feat_seed=4200, param_seed=29, n_times=160)
+        fixture_validate(R, CONFIG2, "cfg2_validate.npz", feat_seed=4300, param_seed=31, n_times=160)
+    if "stgcn" in which:
+        fixture_stgcn_forward(R, "stgcn_forward.npz", [CONFIG1, CONFIG2], param_seed=23, feat_seed=4100)
 
 
 if __name__ == "__main__":

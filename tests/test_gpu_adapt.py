@@ -34,7 +34,7 @@ def test_adaptation_matches_oracle(region, drop, tmp_path):
                 epochs=epochs, device="cuda:0", dropout=drop or (0.0, 0.0), dropout_seed=77)
     torch.manual_seed(123)
     PT = refcpu.to_torch(P)
-    ref_p, ref_losses, ref_lrs, ref_val = refcpu.adapt_reference(
+    ref_p, ref_losses, ref_lrs, ref_val, _ = refcpu.adapt_reference(
         {k: PT[k] for k in tr}, {k: v for k, v in PT.items() if k not in tr}, refcpu.TaskData(feats, ei, d),
         region, epochs, dropout=(77, drop[0], drop[1]) if drop else None)
     assert res.n_train == 16 and res.n_val == 4
@@ -50,3 +50,69 @@ def test_adaptation_matches_oracle(region, drop, tmp_path):
     checkpoint.save(ck, str(tmp_path / "adapted.pt"))
     back = checkpoint.load(str(tmp_path / "adapted.pt"), weights_only=False)  # our own file (numpy stats)
     assert back["adaptation_type"] == "v5_regional_adaptation_adaptive" and back["region_name"] == region
+
+
+def _split(P):
+    tr = {k: v for k, v in P.items() if k.startswith(("lstm.", "output_layer."))}
+    return tr, {k: v for k, v in P.items() if k not in tr}
+
+
+@pytest.mark.parametrize("region", ["Thailand", "Moscow", "Delhi"])
+def test_adaptation_matches_reference_adapt_model(golden_dir, region):
+    """adapt() on the GPU against adapt_hybrid_v5.adaptModel run unmodified on the same
+    synthetic stream (tests/golden/cfg4_adapt.npz; the recorded DataLoader shuffle orders
+    replayed): per-step and per-epoch losses, learning rates, validation MSE, adapted params."""
+    import os
+    z = np.load(os.path.join(golden_dir, "cfg4_adapt.npz"))
+    d = CONFIG1
+    P = synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1)
+    tr, gcn = _split(P)
+    lats, lons = synth.region_grid(n_lat=5, n_lon=5)
+    ei = build_spatial_graph(lats, lons, 4)[0]
+    feats = synth.make_features(int(z["feat_seed"]), d.num_nodes, synth.t_total_for(int(z["n_samples"])))
+    tag = f"adapt/{region}"
+    orders = z[tag + "/orders"]
+    res = adapt(d, feats, ei, {k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, tr, region,
+                epochs=len(orders), device="cuda:0", orders=orders)
+    calls = z[tag + "/sched_calls"]
+    assert rel(res.epoch_losses, calls[:, 0]) < 1e-5
+    np.testing.assert_allclose(res.lrs, [float(z[f"sched/{region}/lr0"])] + list(calls[:-1, 1]), rtol=1e-6)
+    assert abs(res.val_loss - float(z[tag + "/val_loss"])) < 1e-5 * float(z[tag + "/val_loss"])
+    got = params.unpack(res.theta, d, 0)
+    for k in tr:
+        assert rel(got[k].cpu().numpy(), z[f"{tag}/adapted/{k}"]) < 1e-5, k
+
+
+def test_adaptation_n441_matches_oracle():
+    """BASELINE config 4 shapes (N=441, Hc=256, LSTM 4x128, batch-1 steps): 2 epochs over 16
+    shuffled training windows + the 4-window validation, against the oracle. Runs the
+    small-grid split-K forward / BPTT steps and the per-window GCN feature cache (the second
+    epoch reads every window's features from it)."""
+    from weatherforecast_stgcn_maml_amd import _capi
+    from weatherforecast_stgcn_maml_amd.config import CONFIG2
+
+    d = CONFIG2
+    P = synth.init_params(22, d, gcn_bias_scale=0.1)
+    tr, gcn = _split(P)
+    lats, lons = synth.region_grid()
+    ei = build_spatial_graph(lats, lons, 4)[0]
+    feats = synth.make_features(3200, d.num_nodes, synth.t_total_for(20))
+    ctx = _capi.Context(d, 0)
+    ctx.variant_counts(reset=True)
+    torch.manual_seed(5)
+    res = adapt(d, feats, ei, {k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, tr, "Moscow",
+                epochs=2, device="cuda:0", ctx=ctx)
+    vc = ctx.variant_counts()
+    assert vc["fwd_split"] > 0 and vc["bwd_split"] > 0, vc
+    torch.manual_seed(5)
+    PT = refcpu.to_torch(P)
+    tr_t, gcn_t = _split(PT)
+    ref_p, ref_losses, ref_lrs, ref_val, _ = refcpu.adapt_reference(tr_t, gcn_t, refcpu.TaskData(feats, ei, d),
+                                                                    "Moscow", 2)
+    assert res.n_train == 16 and res.n_val == 4
+    np.testing.assert_allclose(res.lrs, ref_lrs, rtol=1e-12)
+    assert rel(res.epoch_losses, ref_losses) < 1e-5
+    got = params.unpack(res.theta, d, 0)
+    for k in tr:
+        assert rel(got[k].cpu().numpy(), ref_p[k].numpy()) < 1e-5, k
+    assert abs(res.val_loss - ref_val) < 1e-5 * ref_val

@@ -232,3 +232,119 @@ def test_alloc_free_and_world1_comm():
     torch.cuda.synchronize()
     assert torch.equal(buf, ref)  # world 1: sum over one rank
     ctx.comm_destroy()
+
+
+# ----------------------------------------------------------------------------- module-API dropout
+def _module(d, P, p_gcn, p_lstm):
+    from weatherforecast_stgcn_maml_amd.hybrid_model import HybridSTGCN_LSTM
+    from weatherforecast_stgcn_maml_amd.model import STGCN
+
+    base = STGCN(d.input_channels, d.hidden_channels, d.output_channels, d.window_size, d.forecast_horizon,
+                 dropout_rate=p_gcn)
+    m = HybridSTGCN_LSTM(base, d.lstm_hidden_size, d.lstm_num_layers, p_lstm, d.output_channels,
+                         d.forecast_horizon, freeze_base=True)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    return m.to("cuda:0")
+
+
+@pytest.mark.parametrize("d", [CONFIG1, CONFIG2])
+def test_train_mode_module_dropout_matches_oracle(d):
+    """HybridSTGCN_LSTM in train() mode with the reference's dropout sites (STGCN dropout after
+    conv1-3, hybrid_model.py:67,70,73; nn.LSTM inter-layer dropout :42-49; head input :108):
+    an unmodified loss.backward() through the autograd shim reproduces the oracle's loss and
+    gradients under the same counter-based masks (seed drawn from the torch RNG per call)."""
+    from weatherforecast_stgcn_maml_amd.hybrid_model import draw_dropout_seed
+
+    P = synth.init_params(41, d, gcn_bias_scale=0.1)
+    m = _module(d, P, 0.2, 0.2).train()
+    ei = grid_edges(d)
+    feats = synth.make_features(4400, d.num_nodes, synth.t_total_for(2))
+    x, y = synth.sample_xy(feats, 1)
+    xg = torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
+    yg = torch.from_numpy(np.ascontiguousarray(y)).to("cuda:0")
+    torch.manual_seed(77)
+    pred = m(xg, torch.from_numpy(ei).to("cuda:0"))
+    loss = torch.nn.MSELoss()(pred, yg)
+    loss.backward()
+    torch.manual_seed(77)
+    seed = draw_dropout_seed()
+    names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
+    PT = refcpu.to_torch(P)
+    Pt = {k: PT[k].clone().requires_grad_(True) for k in names}
+    task = refcpu.TaskData(feats, ei, d)
+    ref_loss, ref_pred = refcpu.batch_loss(Pt, {k: v for k, v in PT.items() if k not in names}, task, [1],
+                                           refcpu.Dropout(seed, 0.2, 0.2, 0, 0))
+    ref_loss.backward()
+    assert rel(pred.detach().cpu().numpy(), ref_pred[0].detach().numpy()) < 1e-5
+    assert abs(float(loss) - float(ref_loss)) < 1e-5 * float(ref_loss)
+    got = {"lstm." + n: p.grad for n, p in m.lstm.named_parameters()}
+    got["output_layer.weight"] = m.output_layer.weight.grad
+    got["output_layer.bias"] = m.output_layer.bias.grad
+    for k in names:
+        assert rel(got[k].cpu().numpy(), Pt[k].grad.numpy()) < 1e-4, k
+    # eval() and a second train-mode call: no dropout / fresh masks
+    m.eval()
+    with torch.no_grad():
+        p_eval = m(xg, torch.from_numpy(ei).to("cuda:0"))
+        p_eval2 = m(xg, torch.from_numpy(ei).to("cuda:0"))
+    assert torch.equal(p_eval, p_eval2)
+    m.train()
+    with torch.no_grad():
+        p2 = m(xg, torch.from_numpy(ei).to("cuda:0"))
+    assert not torch.equal(p2, pred.detach()) and not torch.equal(p2, p_eval)
+
+
+@pytest.mark.parametrize("i", [0, 1])
+def test_stgcn_forward_matches_reference(golden_dir, i):
+    """The drop-in model.STGCN.forward (model.py:30-52: conv x4 + ReLU, last time block,
+    output_layer, view/reshape) against the reference module's own output (eval mode), and in
+    train mode (dropout after each of the four convs) against the oracle's masks."""
+    import os
+    from weatherforecast_stgcn_maml_amd.hybrid_model import draw_dropout_seed
+    from weatherforecast_stgcn_maml_amd.model import STGCN
+
+    z = np.load(os.path.join(golden_dir, "stgcn_forward.npz"))
+    d = CONFIG1 if int(z[f"d{i}/num_nodes"]) == CONFIG1.num_nodes else CONFIG2
+    P = synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1)
+    base = STGCN(d.input_channels, d.hidden_channels, d.output_channels, d.window_size, d.forecast_horizon,
+                 dropout_rate=0.2)
+    base.load_state_dict({k[len("base_stgcn."):]: torch.from_numpy(v) for k, v in P.items()
+                          if k.startswith("base_stgcn.")})
+    base = base.to("cuda:0").eval()
+    x, _ = synth.sample_xy(synth.make_features(int(z["feat_seed"]), d.num_nodes, synth.t_total_for(1)), 0)
+    xg = torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
+    eig = torch.from_numpy(z[f"d{i}/edge_index"]).to("cuda:0")
+    out = base(xg, eig).cpu().numpy()
+    assert out.shape == z[f"d{i}/out"].shape
+    assert rel(out, z[f"d{i}/out"]) < 1e-5
+    base.train()
+    torch.manual_seed(3)
+    out_t = base(xg, eig).cpu()
+    torch.manual_seed(3)
+    drop = refcpu.Dropout(draw_dropout_seed(), 0.2, 0.0, 0, 0)
+    ref = refcpu.stgcn_forward(torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(z[f"d{i}/edge_index"]),
+                               refcpu.to_torch(P), d, drop)
+    assert rel(out_t.numpy(), ref.numpy()) < 1e-5
+    assert rel(out_t.numpy(), out) > 1e-3
+
+
+@pytest.mark.parametrize("name", ["cfg1_validate.npz", "cfg2_validate.npz"])
+def test_evaluate_regional_matches_validate_adapted(golden_dir, name):
+    """evaluate.evaluate_regional (HIP forward of the first 3 windows, sample / node means on
+    the device, denormalised per-variable MSE / MAE) against validate_hybrid_v5.validateAdapted
+    run unmodified on the same synthetic stream (tests/golden/cfg*_validate.npz)."""
+    import os
+    from weatherforecast_stgcn_maml_amd.evaluate import evaluate_regional
+
+    z = np.load(os.path.join(golden_dir, name))
+    d = CONFIG1 if name.startswith("cfg1") else CONFIG2
+    P = synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1)
+    m = _module(d, P, 0.2, 0.2).eval()
+    feats = torch.from_numpy(synth.make_features(int(z["feat_seed"]), d.num_nodes, int(z["t_sub"]))).to("cuda:0")
+    res = evaluate_regional(m, feats, grid_edges(d), {"mean": z["stats_mean"], "std": z["stats_std"]})
+    for v in z["var_names"]:
+        v = str(v)
+        for k in ("mse", "mae"):
+            want = float(z[f"{v}/{k}"])
+            assert abs(res[v][k] - want) <= 1e-4 * abs(want), (v, k, res[v][k], want)
+    assert abs(res["average_mse"] - float(z["average_mse"])) <= 1e-4 * float(z["average_mse"])

@@ -127,3 +127,115 @@ def test_forward_and_inner_cfg2(golden_dir):
         assert rel(ad[k].detach().numpy().reshape(-1)[:64], z[f"t0_adapted_slice/{k}"]) < 1e-5, k
     q, _ = refcpu.batch_loss(ad, Pg, task, [int(z["n_support"])])
     assert abs(float(q) - float(z["t0_query_mse"])) < 1e-5 * float(z["t0_query_mse"])
+
+
+# ----------------------------------------------------------------------------- config 4
+def _adapt_split(P):
+    tr = {k: v for k, v in P.items() if k.startswith(("lstm.", "output_layer."))}
+    return tr, {k: v for k, v in P.items() if k not in tr}
+
+
+def test_climate_scheduler_matches_reference(golden_dir):
+    """ClimateAwareLRScheduler / create_climate_optimizer (adaptive_scheduler.py:7-94), run by
+    the reference itself, against the package's restatement and the oracle's."""
+    from weatherforecast_stgcn_maml_amd.adapt import ClimateAwareLRScheduler, climate_optimizer_config
+
+    z = load(golden_dir, "cfg4_adapt.npz")
+    losses = z["sched_losses"]
+    for region in z["regions"]:
+        region = str(region)
+        lr0, wd = climate_optimizer_config(region)
+        assert lr0 == float(z[f"sched/{region}/lr0"]) and wd == float(z[f"sched/{region}/wd"])
+        s = ClimateAwareLRScheduler(region, lr0)
+        np.testing.assert_allclose([s.step(float(x)) for x in losses], z[f"sched/{region}/lrs"], rtol=1e-12)
+        np.testing.assert_allclose([refcpu.climate_lr(region, i + 1, lr0, float(x)) for i, x in enumerate(losses)],
+                                   z[f"sched/{region}/lrs"], rtol=1e-12)
+
+
+def test_random_sampler_order_matches_dataloader():
+    """adapt.random_sampler_order consumes the global torch RNG exactly as a shuffling
+    DataLoader does (its _base_seed draw, then RandomSampler's seed): same orders epoch after
+    epoch."""
+    from weatherforecast_stgcn_maml_amd.adapt import random_sampler_order
+
+    for seed, n in [(123, 16), (0, 960), (7, 5)]:
+        torch.manual_seed(seed)
+        dl = torch.utils.data.DataLoader(range(n), batch_size=1, shuffle=True)
+        want = [[int(b) for b in dl] for _ in range(3)]
+        torch.manual_seed(seed)
+        got = [random_sampler_order(n).tolist() for _ in range(3)]
+        assert got == want
+
+
+@pytest.mark.parametrize("region", ["Thailand", "Moscow", "Delhi"])
+def test_adapt_oracle_matches_reference_adapt_model(golden_dir, region):
+    """refcpu.adapt_reference against adapt_hybrid_v5.adaptModel run unmodified on the same
+    synthetic stream (15 epochs x 16 shuffled batch-1 steps, Adam + L2, clip, climate LR, the
+    20% validation split): per-step losses, per-epoch learning rates, validation MSE and the
+    adapted LSTM / head parameters."""
+    z = load(golden_dir, "cfg4_adapt.npz")
+    d = CONFIG1
+    P = synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1)
+    tr, gcn = _adapt_split(refcpu.to_torch(P))
+    feats = synth.make_features(int(z["feat_seed"]), d.num_nodes, synth.t_total_for(int(z["n_samples"])))
+    tag = f"adapt/{region}"
+    orders = z[tag + "/orders"]
+    p, ep_losses, lrs, val, steps = refcpu.adapt_reference(tr, gcn, refcpu.TaskData(feats, grid_edges(d), d), region,
+                                                           len(orders), orders=orders)
+    calls = z[tag + "/sched_calls"]
+    assert rel(np.array(steps), z[tag + "/train_losses"]) < 1e-5
+    np.testing.assert_allclose(ep_losses, calls[:, 0], rtol=1e-5)
+    lr0 = float(z[f"sched/{region}/lr0"])
+    np.testing.assert_allclose(lrs, [lr0] + list(calls[:-1, 1]), rtol=1e-6)
+    assert abs(val - float(z[tag + "/val_loss"])) < 1e-5 * float(z[tag + "/val_loss"])
+    for k, v in p.items():
+        assert rel(v.numpy(), z[f"{tag}/adapted/{k}"]) < 1e-5, k
+
+
+def test_stgcn_forward_oracle_matches_reference(golden_dir):
+    """model.STGCN.forward (model.py:30-52, eval) restated: GCN x4 + ReLU, last time block,
+    output_layer, view(N, Hf, C).reshape(-1, C)."""
+    z = load(golden_dir, "stgcn_forward.npz")
+    for i in range(2):
+        d = CONFIG1 if int(z[f"d{i}/num_nodes"]) == CONFIG1.num_nodes else CONFIG2
+        P = refcpu.to_torch(synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1))
+        x, _ = synth.sample_xy(synth.make_features(int(z["feat_seed"]), d.num_nodes, synth.t_total_for(1)), 0)
+        out = refcpu.stgcn_forward(torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(z[f"d{i}/edge_index"]),
+                                   P, d)
+        assert rel(out.numpy(), z[f"d{i}/out"]) < 1e-6
+
+
+# ----------------------------------------------------------------------------- evaluation
+def _validate_inputs(z, d):
+    P = synth.init_params(int(z["param_seed"]), d, gcn_bias_scale=0.1)
+    feats = synth.make_features(int(z["feat_seed"]), d.num_nodes, int(z["t_sub"]))
+    stats = {"mean": z["stats_mean"], "std": z["stats_std"]}
+    return P, feats, stats
+
+
+def check_validate_results(res, z, tol):
+    for v in z["var_names"]:
+        v = str(v)
+        for m in ("mse", "mae"):
+            want = float(z[f"{v}/{m}"])
+            assert abs(res[v][m] - want) <= tol * abs(want), (v, m, res[v][m], want)
+    assert abs(res["average_mse"] - float(z["average_mse"])) <= tol * float(z["average_mse"])
+
+
+@pytest.mark.parametrize("d,name", [(CONFIG1, "cfg1_validate.npz"), (CONFIG2, "cfg2_validate.npz")])
+def test_regional_eval_oracle_matches_validate_adapted(golden_dir, d, name):
+    """refcpu.regional_eval and evaluate.regional_metrics against validateAdapted run unmodified
+    on the same synthetic stream: denormalised per-variable MSE / MAE and the average without sp."""
+    from weatherforecast_stgcn_maml_amd.evaluate import regional_metrics
+
+    z = load(golden_dir, name)
+    P, feats, stats = _validate_inputs(z, d)
+    res = refcpu.regional_eval(refcpu.to_torch(P), feats, grid_edges(d), stats, d)
+    check_validate_results(res, z, 1e-5)
+    # the package's host-side metric step, fed the oracle's sample-averaged arrays
+    ei = torch.from_numpy(grid_edges(d))
+    preds = [refcpu.hybrid_forward(refcpu.to_torch(P), torch.from_numpy(np.ascontiguousarray(
+        synth.sample_xy(feats, i)[0])), ei, d).numpy() for i in range(3)]
+    trues = [synth.sample_xy(feats, i)[1] for i in range(3)]
+    res2 = regional_metrics(np.mean(preds, axis=0), np.mean(trues, axis=0), stats, d.forecast_horizon, d.num_nodes)
+    check_validate_results(res2, z, 1e-5)

@@ -23,6 +23,7 @@ EXPORTS = (
     "smaml_backward", "smaml_gcn_forward", "smaml_lstm_forward", "smaml_lstm_backward", "smaml_head_loss",
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
     "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy", "smaml_variant_counts", "smaml_set_option",
+    "smaml_dropout",
 )
 ABI_VERSION = 4
 
@@ -104,6 +105,7 @@ _SIGS = {
                               PI64, I32], I32),
     "smaml_variant_counts": ([P, PI64, I32, PI32, I32], I32),
     "smaml_set_option": ([P, ctypes.c_char_p, I64], I32),
+    "smaml_dropout": ([P, P, P, I64, F32, ctypes.c_uint32, I32], I32),
 }
 
 
@@ -326,6 +328,9 @@ class Context:
         check(self._L.smaml_variant_counts(self._h, buf, n, ctypes.byref(cnt), 1 if reset else 0))
         assert cnt.value == n, (cnt.value, n)
         return {name: int(buf[i]) for i, name in enumerate(VARIANTS)}
+
+    def dropout(self, stream, x, p, seed, layer):
+        check(self._L.smaml_dropout(self._h, stream, ptr(x), x.numel(), float(p), int(seed) & 0xFFFFFFFF, int(layer)))
 
     def set_option(self, key: str, value: int):
         check(self._L.smaml_set_option(self._h, key.encode(), int(value)))

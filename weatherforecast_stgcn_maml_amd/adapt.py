@@ -68,8 +68,11 @@ class ClimateAwareLRScheduler:
 
 
 def random_sampler_order(n: int) -> torch.Tensor:
-    """The order torch.utils.data.RandomSampler yields for DataLoader(shuffle=True) without an
-    explicit generator: a fresh seed drawn from the global torch RNG, then randperm."""
+    """The order a ``DataLoader(ds, batch_size=1, shuffle=True)`` (adapt_hybrid_v5.py:179; PyG's
+    loader is torch's) yields in one epoch, drawing from the global torch RNG exactly as it does:
+    the iterator first draws its ``_base_seed`` (one int64), then ``RandomSampler`` draws its
+    own seed (one int64) and runs ``randperm`` on a generator seeded with it."""
+    torch.empty((), dtype=torch.int64).random_()  # _BaseDataLoaderIter._base_seed
     seed = int(torch.empty((), dtype=torch.int64).random_().item())
     g = torch.Generator()
     g.manual_seed(seed)
@@ -89,9 +92,11 @@ class AdaptResult:
 def adapt(dims: ModelDims, features, edge_index, gcn: dict, theta: dict, region_name: str, epochs: int = 15,
           max_samples: int = 1200, train_frac: float = 0.8, base_lr: float = 0.0006, device="cuda",
           val_batch: int = 32, ctx: Optional[_capi.Context] = None, dropout=(0.0, 0.0),
-          dropout_seed: int = 0) -> AdaptResult:
+          dropout_seed: int = 0, orders=None) -> AdaptResult:
     """``dropout`` = (STGCN dropout_rate, lstm_dropout) of the train-mode steps (the reference
-    adapts in train mode: (0.2, 0.2)); validation runs without dropout (eval mode)."""
+    adapts in train mode: (0.2, 0.2)); validation runs without dropout (eval mode).
+    ``orders``: optional per-epoch sample permutations of the training windows (default: drawn
+    from the global torch RNG as the reference's shuffling DataLoader draws them)."""
     dev = torch.device(device)
     ctx = ctx or _capi.Context(dims, dev.index or 0)
     ei = edge_index.detach().cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
@@ -117,7 +122,9 @@ def adapt(dims: ModelDims, features, edge_index, gcn: dict, theta: dict, region_
     ctx.set_task_ids([0])
     for _ in range(epochs):
         ctx.set_dropout(dropout[0], dropout[1], dropout_seed)  # masks keyed by the global step index
-        order = random_sampler_order(n_train).numpy().astype(np.int32)
+        ep = len(res.epoch_losses)
+        order = np.asarray(orders[ep] if orders is not None else random_sampler_order(n_train).numpy(), np.int32)
+        assert order.shape == (n_train,), order.shape
         lr_dev = torch.full((n_train,), lr, device=dev, dtype=torch.float32)
         ctx.adapt_steps(stream, th, m, v, step, order.reshape(n_train, 1), lr_dev, (0.9, 0.999), 1e-8, wd,
                         MAX_GRAD_NORM, losses)

@@ -19,6 +19,7 @@ from . import params
 from .config import (GRAD_ACCUMULATION_STEPS, INNER_BATCH_CAP, INNER_EPOCHS_PER_TASK, INNER_LR,
                      MAX_GRAD_NORM, MamlConfig)
 from .dataset import resolve_windows
+from .hybrid_model import draw_dropout_seed
 from .maml import MetaLearner
 
 
@@ -28,15 +29,25 @@ def _learner(hybrid_model, edge_index, device, steps, num_nodes):
                      query_loss_scale=1.0 / GRAD_ACCUMULATION_STEPS)
     ei = edge_index.detach().cpu().numpy() if torch.is_tensor(edge_index) else np.asarray(edge_index)
     # the reference adapts a train()-mode copy (train_hybrid_maml_v5.py:113,159): its dropout
-    # rates apply; masks are keyed off torch's seed for reproducibility
-    drop = (float(hybrid_model.base_stgcn.dropout_rate), float(hybrid_model.dropout.p))
+    # rates apply; every call draws a fresh mask seed from the global torch RNG, as
+    # the reference's nn.Dropout calls draw fresh masks
+    drop = (float(hybrid_model.base_stgcn.dropout.p), float(hybrid_model.dropout.p))
+    seed = draw_dropout_seed() if drop != (0.0, 0.0) else 0
     return MetaLearner(dims, cfg, hybrid_model.named_gcn(), hybrid_model.named_trainable(), ei, device=device,
-                       dropout=drop, dropout_seed=torch.initial_seed() & 0xFFFFFFFF), dims
+                       dropout=drop, dropout_seed=seed), dims
+
+
+def _support_len(windows) -> int:
+    """Samples inner_loop_v4 trains on: the first min(15, len(support_ds)) (:124-127)."""
+    return min(len(windows), INNER_BATCH_CAP)
 
 
 def _run(hybrid_model, task_specs, device):
-    """task_specs: [(features, support_windows, query_window, edge_index)] sharing one graph."""
-    S = min(len(task_specs[0][1]), INNER_BATCH_CAP)
+    """task_specs: [(features, support_windows, query_window, edge_index)] sharing one graph and
+    one support length (so one inner-step count)."""
+    S = _support_len(task_specs[0][1])
+    if any(_support_len(sw) != S for _, sw, _, _ in task_specs):
+        raise ValueError("tasks batched into one pass must have the same support length")
     K = INNER_EPOCHS_PER_TASK * S
     N = task_specs[0][0].shape[1]
     ml, dims = _learner(hybrid_model, task_specs[0][3], device, K, N)
@@ -82,7 +93,9 @@ def meta_update_v4(hybrid_model, koppen_embed, tasks, device, meta_optimizer):
         if qf is not feats:
             raise ValueError("support and query of a task must share one feature stream")
         ei = ds.edge_index.detach().cpu().numpy() if torch.is_tensor(ds.edge_index) else np.asarray(ds.edge_index)
-        groups.setdefault(ei.tobytes(), []).append((feats.to(device, torch.float32).contiguous(), sw, qw[0], ei))
+        # one pass per (graph, support length): tasks in a pass share edge_index and step count
+        key = (ei.tobytes(), _support_len(sw))
+        groups.setdefault(key, []).append((feats.to(device, torch.float32).contiguous(), sw, qw[0], ei))
     meta_loss = 0.0
     for specs in groups.values():
         res, _, _ = _run(hybrid_model, specs, device)

@@ -918,6 +918,10 @@ int smaml_forward(smaml_ctx* c, void* stream, const float* theta, const float* c
   TRY(reserve(c, 1, nsamples));
   set_work(c, 1, nsamples);
   TRY(upload_xtab(c, s, x_host, nsamples));
+  if (c->p_gcn > 0.f || c->p_lstm > 0.f) {  // train-mode module forward: masks of (seed, task id, step 0)
+    TRY(upload_task_ids(c, s, 1));
+    set_step_drop(c, 0);  // kept in c->w.drop for the smaml_backward of these activations
+  }
   TRY(run_forward(c, s, theta, 0, c->xtab));
   Work w = c->w;
   w.pred = pred;
@@ -1226,6 +1230,14 @@ int smaml_backward(smaml_ctx* c, void* stream, const float* theta, const float* 
   HIP_TRY(hipMemsetAsync(grad, 0, (size_t)c->po.P * 4, s));
   c->act_B = -1;  // the BPTT overwrites the saved gates with dG
   TRY(run_backward(c, s, theta, 0, grad));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_dropout(smaml_ctx* c, void* stream, float* x, int64_t n, float p, uint32_t seed, int32_t layer) {
+  if (!c || !x || n < 0 || !(p >= 0.f && p < 1.f) || layer < 0) return fail(SMAML_EINVAL, "bad dropout arguments");
+  TRY(ensure_device(c));
+  if (p > 0.f && n > 0) launch_dropout_inplace((hipStream_t)stream, x, n, p, seed, layer);
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }

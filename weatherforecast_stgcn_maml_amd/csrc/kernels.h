@@ -185,6 +185,9 @@ void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float
 void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
 // dst[z] = drop(src[z]) with the head-input mask ([M][H] rows per task; src == dst allowed)
 void launch_drop_rows(hipStream_t s, const Work& w, int H, const float* src, int64_t src_zstride, float* dst);
+// x[i] = drop(x[i]) in place with the GCN-output masks (kind 1, `layer`, step 0, task 0, sample 0):
+// STGCN.forward's train-mode dropout after conv layer+1 of one sample (model.py:33-42)
+void launch_dropout_inplace(hipStream_t s, float* x, int64_t n, float p, uint32_t seed, int layer);
 // rows the head reads: h_T (or R h_T) of the top layer, or their dropout-masked copies
 const float* head_input(const Dims& d, const Work& w, bool tangent, int64_t* zstride);
 void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,

@@ -578,6 +578,18 @@ void launch_drop_rows(hipStream_t s, const Work& w, int H, const float* src, int
   k_drop_rows<<<dim3(nb, w.Z), NT, 0, s>>>(src, src_zstride, dst, w.M, H, w.drop);
 }
 
+__global__ void k_dropout_inplace(float* x, int64_t n, uint32_t site, uint32_t thr, float sc) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = drop_keep(site, (uint64_t)i, thr) ? x[i] * sc : 0.f;
+}
+
+void launch_dropout_inplace(hipStream_t s, float* x, int64_t n, float p, uint32_t seed, int layer) {
+  const uint32_t thr = (uint32_t)std::min<double>(std::llround((double)p * 16777216.0), 16777216.0);
+  int nb = (int)((n + NT - 1) / NT);
+  if (nb > 4096) nb = 4096;
+  k_dropout_inplace<<<nb, NT, 0, s>>>(x, n, drop_site(seed, 1, 0, layer), thr, 1.f / (1.f - p));
+}
+
 // The head's input rows: h_T of the top layer (z stride T*M*H), or drop(h_T) under dropout.
 const float* head_input(const Dims& d, const Work& w, bool tangent, int64_t* zstride) {
   if (w.drop.lstm()) {

@@ -15,13 +15,18 @@ is ``smaml_backward`` (head, BPTT, weight gradients on the GPU), so unmodified c
 the HIP path. Gradients reach the LSTM and head only (the reference computes the GCN under
 ``no_grad``, F2). One forward/backward pair may be in flight per model shape: a second forward
 before the backward ends the first one's saved activations (the backward then raises).
+
+In ``train()`` mode the forward applies the reference's dropout sites (STGCN ``dropout`` after
+conv1-3 inside ``extract_base_features``, hybrid_model.py:67,70,73; ``nn.LSTM``'s inter-layer
+dropout, :42-49; the head-input dropout, :108) with the library's counter-based masks; every
+call draws a fresh mask seed from the global torch RNG (as ``nn.Dropout`` draws its masks), and
+the backward reuses the forward's masks. ``eval()`` (or p = 0) runs without dropout.
 For whole meta-steps use ``weatherforecast_stgcn_maml_amd.maml`` (run entirely inside the
 library).
 """
 from __future__ import annotations
 
 import math
-import warnings
 
 import torch
 import torch.nn as nn
@@ -31,13 +36,31 @@ from .config import ModelDims
 from .model import _context, _set_graph
 
 
+def draw_dropout_seed() -> int:
+    """One 32-bit mask seed from the global torch RNG (a train-mode forward draws one)."""
+    return int(torch.empty((), dtype=torch.int64).random_().item()) & 0xFFFFFFFF
+
+
+def _forward(lib_ctx, theta, xs, pred, drop, feats=None):
+    """smaml_forward, with train-mode dropout (p_gcn, p_lstm, seed) set around it (the masks are
+    captured by the forward and reused by the following smaml_backward)."""
+    if drop is not None:
+        lib_ctx.set_task_ids([0])
+        lib_ctx.set_dropout(*drop)
+    try:
+        lib_ctx.forward(_capi.stream_ptr(torch), theta, xs, pred, feats)
+    finally:
+        if drop is not None:
+            lib_ctx.set_dropout(0.0, 0.0, 0)
+
+
 class _HybridFn(torch.autograd.Function):
     """pred = HybridSTGCN_LSTM(x) with d pred / d (LSTM, head) from ``smaml_backward``."""
 
     @staticmethod
-    def forward(fctx, x, lib_ctx, dims, theta, names, *tparams):
+    def forward(fctx, x, lib_ctx, dims, theta, names, drop, *tparams):
         pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
-        lib_ctx.forward(_capi.stream_ptr(torch), theta, [x], pred)
+        _forward(lib_ctx, theta, [x], pred, drop)
         fctx.lib_ctx, fctx.dims, fctx.theta, fctx.names = lib_ctx, dims, theta, names
         return pred
 
@@ -46,7 +69,7 @@ class _HybridFn(torch.autograd.Function):
         grad = torch.empty_like(fctx.theta)
         fctx.lib_ctx.backward(_capi.stream_ptr(torch), fctx.theta, gpred.contiguous().float(), grad)
         g = params.unpack(grad, fctx.dims)
-        return (None, None, None, None, None, *[g[n] for n in fctx.names])
+        return (None, None, None, None, None, None, *[g[n] for n in fctx.names])
 
 
 class LSTMParams(nn.Module):
@@ -127,13 +150,17 @@ class HybridSTGCN_LSTM(nn.Module):
             out[f"base_stgcn.conv{k}.lin.weight"] = conv.lin.weight.detach()
         return out
 
+    def _drop(self):
+        """(p_gcn, p_lstm, seed) of a train-mode forward, None in eval mode or at p = 0."""
+        p_gcn = float(self.base_stgcn.dropout.p)
+        p_lstm = float(self.dropout.p)
+        if not self.training or (p_gcn <= 0.0 and p_lstm <= 0.0):
+            return None
+        return (p_gcn, p_lstm, draw_dropout_seed())
+
     def _prepare(self, x, edge_index):
         if x.device.type != "cuda":
             raise _capi.SmamlError(-1, "HybridSTGCN_LSTM.forward runs on a HIP device only")
-        if self.training and (self.dropout.p > 0 or self.base_stgcn.dropout_rate > 0):
-            warnings.warn("the module-level forward/backward applies no dropout (the training drivers "
-                          "MetaLearner / meta_train / adapt and the inner_loop_v4 / meta_update_v4 wrappers "
-                          "do); build the model with dropout 0 for train-mode parity (SURVEY F7)", stacklevel=3)
         T = self.base_stgcn.window_size
         if x.shape[0] % T:
             raise ValueError(f"x has {x.shape[0]} rows, not a multiple of window_size={T}")
@@ -152,7 +179,7 @@ class HybridSTGCN_LSTM(nn.Module):
         x = x.contiguous().float()
         pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
         feats = torch.empty(x.shape[0], dims.hidden_channels, device=x.device)
-        ctx.forward(_capi.stream_ptr(torch), theta, [x], pred, feats)
+        _forward(ctx, theta, [x], pred, self._drop(), feats)
         return feats
 
     def _trainable_params(self):
@@ -165,10 +192,11 @@ class HybridSTGCN_LSTM(nn.Module):
         ctx, dims, theta = self._prepare(x, edge_index)
         x = x.contiguous().float()
         named = self._trainable_params()
+        drop = self._drop()
         if torch.is_grad_enabled() and any(p.requires_grad for _, p in named):
-            return _HybridFn.apply(x, ctx, dims, theta, [n for n, _ in named], *[p for _, p in named])
+            return _HybridFn.apply(x, ctx, dims, theta, [n for n, _ in named], drop, *[p for _, p in named])
         pred = torch.empty(dims.num_nodes * dims.forecast_horizon, dims.output_channels, device=x.device)
-        ctx.forward(_capi.stream_ptr(torch), theta, [x], pred)
+        _forward(ctx, theta, [x], pred, drop)
         return pred
 
     def get_trainable_parameters(self):

@@ -8,7 +8,6 @@ there is no CPU path.
 from __future__ import annotations
 
 import math
-import warnings
 
 import numpy as np
 import torch
@@ -83,9 +82,18 @@ class GCNConv(nn.Module):
         return f"GCNConv({self.in_channels}, {self.out_channels})"
 
 
+def _any_context(device):
+    """A context for device-wide helper launches (e.g. smaml_dropout) on ``device``."""
+    return _context(ModelDims(num_nodes=1, window_size=1, input_channels=4, hidden_channels=4, lstm_hidden_size=32,
+                              lstm_num_layers=1, forecast_horizon=1, output_channels=1), device)
+
+
 class STGCN(nn.Module):
     """model.py:7-52. ``forward`` (not on the hybrid path) returns the last time block's
-    node features through ``output_layer`` as the reference does (model.py:44-52)."""
+    node features through ``output_layer`` as the reference does (model.py:44-52); in
+    ``train()`` mode it applies ``self.dropout`` after each of the four conv + ReLU layers
+    (model.py:33,36,39,42) with the library's counter-based masks, a fresh seed per call drawn
+    from the global torch RNG. Forward only (no autograd through the HIP GCN)."""
 
     def __init__(self, in_channels, hidden_channels, out_channels=12, window_size=6,
                  forecast_horizon=1, dropout_rate=0.3):
@@ -102,12 +110,17 @@ class STGCN(nn.Module):
         self.output_layer = nn.Linear(hidden_channels, out_channels * forecast_horizon)
 
     def forward(self, x, edge_index):
-        if self.training and self.dropout_rate > 0:
-            warnings.warn("HIP STGCN path applies no dropout (SURVEY F7)", stacklevel=2)
+        p = float(self.dropout.p) if self.training else 0.0
+        if p > 0.0:
+            from .hybrid_model import draw_dropout_seed
+            seed = draw_dropout_seed()
+            dctx = _any_context(x.device)
         with torch.no_grad():
             h = x
-            for conv in (self.conv1, self.conv2, self.conv3, self.conv4):
+            for k, conv in enumerate((self.conv1, self.conv2, self.conv3, self.conv4)):
                 h = torch.relu_(conv(h, edge_index))
+                if p > 0.0:
+                    dctx.dropout(_capi.stream_ptr(torch), h, p, seed, k)
             num_nodes = h.shape[0] // self.window_size
             h = h[-num_nodes:]
             out = torch.nn.functional.linear(h, self.output_layer.weight, self.output_layer.bias)
