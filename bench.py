@@ -273,7 +273,9 @@ def main():
             "kind": "port",
             "sample": f"{args.cpu_sample_steps} batch-1 sample-steps (fwd+bwd+clip+SGD) of the reference's "
                       f"per-node nn.LSTM CPU path at N={d.num_nodes}, {t_step:.3f} s each; meta-steps/s = "
-                      f"1/({sample_steps} sample-steps x t)",
+                      f"1/({sample_steps} sample-steps x t); first-order work only (the reference has no "
+                      f"second-order path); the port times 1.04x the reference's own inner step on the "
+                      f"same sample (profiles/r02_cpu_calibration.log)",
         }
         out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
