@@ -1,16 +1,13 @@
 #!/bin/bash
-# Parity tests on the default library, then interleaved A/B benches of library variants.
+# GPU parity tests of the default build, then (only if green) the A/B of library variants on the
+# SO bench (tools/gpu_ab.sh). Chain stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-: > gpurun_out/ab.log
-for round in 1 2; do
-  for v in libsmaml.so ${AB_VARIANTS:-}; do
-    SMAML_LIB=weatherforecast_stgcn_maml_amd/$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-sample-steps 0 > gpurun_out/ab_tmp.log 2>&1 || exit $?
-    echo "$v $(tail -1 gpurun_out/ab_tmp.log)" >> gpurun_out/ab.log
-  done
-done
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py} -x -v --timeout 300 --timeout-method thread \
+  -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+bash tools/gpu_ab.sh

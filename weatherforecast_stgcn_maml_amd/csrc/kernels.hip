@@ -714,92 +714,122 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 }
 
 // Cell backward of one BPTT tile (acc = dh from the fused K = 8H GEMM, head dh_T not yet added):
-// dc, dG (in place over G_t), the cell-state carry and (optionally) the kept dh.
-template <int H, class CfgNN, bool PRE = false>
-__device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, const float* Gz, float* dGz, float* __restrict__ dhz,
-                                         const float* __restrict__ Cz, const float* __restrict__ dHz,
-                                         float* __restrict__ dcz, int m0, int n0, int l, int t, int L, int T, int M) {
+// dc, dG (in place over G_t, or into a separate slab), the cell-state carry and (optionally) the
+// kept dh.
+//
+// The accumulators are first transposed through LDS (the mainloop's staging buffers, idle by
+// then) so that every lane then works on float4 groups of 4 consecutive hidden units of one row:
+// all epilogue memory traffic becomes 16-B loads / stores (4x fewer instructions than the
+// accumulator's column-per-lane layout, whole 128-B lines per 8 lanes) and one address serves 4
+// elements. The item loop is software-pipelined: item k+1's operands (gates, c_t, c_{t-1}, the dc
+// carry, dh_T) are loaded before item k is computed and stored, so loads stay in flight under the
+// math and the stores. Program order keeps the in-place dG over G safe: an item's elements are
+// read before they are written and items never share elements. Uniform conditions (t = 0, the
+// first step) are selects on loads from valid addresses, so no branch splits the loads.
+#ifndef SMAML_EPI_DEPTH
+#define SMAML_EPI_DEPTH 1  // epilogue items in flight per thread (1 or 2; A/B-able at build time)
+#endif
+template <class C>
+constexpr int epi_smem_floats() {
+  return C::SMEM_FLOATS > C::BM * C::BN ? C::SMEM_FLOATS : C::BM * C::BN;
+}
+
+
+template <int H, class CfgNN, bool HEAD, bool CHECK>
+__device__ __forceinline__ void bwd_cell_(const float* smem, const float* Gz, float* dGz, float* __restrict__ dhz,
+                                          const float* __restrict__ Cz, const float* __restrict__ dHz,
+                                          float* __restrict__ dcz, int m0, int n0, int t, int T, int M) {
   constexpr int G4 = 4 * H;
-  const bool first = (t == T - 1);
-  const bool head = first && l == L - 1;
-  const bool full = m0 + CfgNN::BM <= M;
-  const uint32_t tM = (uint32_t)t * (uint32_t)M;
-#pragma unroll
-  for (int i = 0; i < CfgNN::WTM; ++i)
-#pragma unroll
-  for (int jj = 0; jj < CfgNN::WTN; ++jj) {
-    const int j = n0 + acc_col<CfgNN>(jj);
-    const int rb = m0 + acc_row<CfgNN>(i, 0);
-    if (j >= H) continue;
-    if constexpr (PRE) {
-    // operands of 4 rows are loaded before their stores (each (row, unit) is read and then
-    // overwritten by this lane only; the compiler cannot prove the in-place dG stores do not
-    // alias the next rows' loads, so without this it serialises their latency row by row)
-#pragma unroll
-    for (int r0 = 0; r0 < 16; r0 += 4) {
-      float v[4][8];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = rb + racc(r0 + q);
-        const bool ok = full || m < M;
-        const uint32_t row = tM + (uint32_t)m;
-        const uint32_t oh = row * H + j, og = row * G4 + j, oc = (uint32_t)m * H + j;
-        v[q][0] = ok && head ? ldb(dHz, 4u * oc) : 0.f;
-        v[q][1] = ok ? ldb(Gz, 4u * og) : 0.f;
-        v[q][2] = ok ? ldb(Gz, 4u * (og + H)) : 0.f;
-        v[q][3] = ok ? ldb(Gz, 4u * (og + 2 * H)) : 0.f;
-        v[q][4] = ok ? ldb(Gz, 4u * (og + 3 * H)) : 0.f;
-        v[q][5] = ok ? ldb(Cz, 4u * oh) : 0.f;
-        v[q][6] = ok && t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-        v[q][7] = ok && !first ? ldb(dcz, 4u * oc) : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = r0 + q;
-        const int m = rb + racc(r);
-        if (!full && m >= M) continue;
-        const uint32_t row = tM + (uint32_t)m;
-        const uint32_t oh = row * H + j;
-        const uint32_t og = row * G4 + j;
-        const uint32_t oc = (uint32_t)m * H + j;
-        const float dh = acc.v[i][jj][r] + v[q][0];
-        const float gi = v[q][1], gf = v[q][2], gg = v[q][3], go = v[q][4];
-        const float tc = tanhf_(v[q][5]);
-        const float cp = v[q][6];
-        const float dct = v[q][7] + dh * go * (1.f - tc * tc);
-        stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
-        stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
-        stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
-        stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
-        stb(dcz, 4u * (oc), dct * gf);
-        if (dhz) stb(dhz, 4u * (oh), dh);
-      }
+  constexpr int GPR = CfgNN::BN / 4;                          // float4 groups per tile row
+  constexpr int NIT = CfgNN::BM * GPR / CfgNN::NTH;           // items per thread
+  static_assert(NIT * CfgNN::NTH == CfgNN::BM * GPR && NIT % 2 == 0, "epilogue items");
+  const bool first = (t == T - 1), past = t > 0;
+  const int64_t pM = past ? (int64_t)M * H : 0;  // c_{t-1} offset (t = 0: masked)
+  const int64_t tM = (int64_t)t * M;
+  struct V {
+    float4 g[4], c, cp, dc, hd;
+  };
+  auto coords = [&](int k, int& r, int& m, int& j) {
+    const int item = (int)threadIdx.x + CfgNN::NTH * k;
+    r = item / GPR;
+    m = m0 + r;
+    j = n0 + 4 * (item % GPR);
+  };
+  auto load = [&](int k, V& v) {
+    int r, m, j;
+    coords(k, r, m, j);
+    if (CHECK) {  // out-of-range items read a valid element (their results are not stored)
+      m = min(m, M - 1);
+      j = min(j, H - 4);
     }
-    } else {
+    const int64_t row = tM + m;
+    const float* gp = Gz + row * G4 + j;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = rb + racc(r);
-      if (!full && m >= M) continue;
-      const uint32_t row = tM + (uint32_t)m;
-      const uint32_t oh = row * H + j;
-      const uint32_t og = row * G4 + j;
-      const uint32_t oc = (uint32_t)m * H + j;
-      const float dh = acc.v[i][jj][r] + (head ? ldb(dHz, 4u * oc) : 0.f);
-      const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
-      const float c = ldb(Cz, 4u * (oh));
-      const float tc = tanhf_(c);
-      const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-      const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
-      const float dct = dcin + dh * go * (1.f - tc * tc);
-      stb(dGz, 4u * (og), dct * gg * gi * (1.f - gi));
-      stb(dGz, 4u * (og + H), dct * cp * gf * (1.f - gf));
-      stb(dGz, 4u * (og + 2 * H), dct * gi * (1.f - gg * gg));
-      stb(dGz, 4u * (og + 3 * H), dh * tc * go * (1.f - go));
-      stb(dcz, 4u * (oc), dct * gf);
-      if (dhz) stb(dhz, 4u * (oh), dh);
+    for (int g = 0; g < 4; ++g) v.g[g] = ld4(gp + g * H);
+    v.c = ld4(Cz + row * H + j);
+    v.cp = ld4(Cz + row * H - pM + j);
+    v.dc = ld4(dcz + (int64_t)m * H + j);
+    if (HEAD) v.hd = ld4(dHz + (int64_t)m * H + j);
+  };
+  auto step = [&](int k, const V& v) {
+    int r, m, j;
+    coords(k, r, m, j);
+    if (CHECK && (m >= M || j >= H)) return;
+    float4 dh = *reinterpret_cast<const float4*>(smem + r * CfgNN::BN + (j - n0));
+    if (HEAD) dh = make_float4(dh.x + v.hd.x, dh.y + v.hd.y, dh.z + v.hd.z, dh.w + v.hd.w);
+    const float4 cp = sel4(past, v.cp), dc = sel4(!first, v.dc);
+    float4 o[4], odc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gi = f4get(v.g[0], e), gf = f4get(v.g[1], e), gg = f4get(v.g[2], e), go = f4get(v.g[3], e);
+      const float d = f4get(dh, e);
+      const float tc = tanhf_(f4get(v.c, e));
+      const float dct = f4get(dc, e) + d * go * (1.f - tc * tc);
+      const float r0 = dct * gg * gi * (1.f - gi), r1 = dct * f4get(cp, e) * gf * (1.f - gf);
+      const float r2 = dct * gi * (1.f - gg * gg), r3 = d * tc * go * (1.f - go);
+      const float rc = dct * gf;
+      if (e == 0) { o[0].x = r0; o[1].x = r1; o[2].x = r2; o[3].x = r3; odc.x = rc; }
+      if (e == 1) { o[0].y = r0; o[1].y = r1; o[2].y = r2; o[3].y = r3; odc.y = rc; }
+      if (e == 2) { o[0].z = r0; o[1].z = r1; o[2].z = r2; o[3].z = r3; odc.z = rc; }
+      if (e == 3) { o[0].w = r0; o[1].w = r1; o[2].w = r2; o[3].w = r3; odc.w = rc; }
     }
+    const int64_t row = tM + m;
+    float* gp = dGz + row * G4 + j;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) st4(gp + g * H, o[g]);
+    st4(dcz + (int64_t)m * H + j, odc);
+    if (dhz) st4(dhz + row * H + j, dh);
+  };
+  if constexpr (SMAML_EPI_DEPTH >= 2) {  // two items in flight (more registers)
+    V va, vb;
+    load(0, va);
+#pragma unroll 1
+    for (int k = 0; k < NIT; k += 2) {
+      load(k + 1, vb);
+      step(k, va);
+      if (k + 2 < NIT) load(k + 2, va);
+      step(k + 1, vb);
+    }
+  } else {  // one item's 7 x 16-B loads in flight; its stores drain under the next item's loads
+    V v;
+#pragma unroll 1
+    for (int k = 0; k < NIT; ++k) {
+      load(k, v);
+      step(k, v);
     }
   }
+}
+
+template <int H, class CfgNN, bool HEAD>
+__device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, float* smem, const float* Gz, float* dGz,
+                                         float* __restrict__ dhz, const float* __restrict__ Cz,
+                                         const float* __restrict__ dHz, float* __restrict__ dcz, int m0, int n0,
+                                         int t, int T, int M) {
+  acc_to_lds<CfgNN>(acc, smem);
+  if (m0 + CfgNN::BM <= M && n0 + CfgNN::BN <= H)  // all but the last row tile: no bounds checks
+    bwd_cell_<H, CfgNN, HEAD, false>(smem, Gz, dGz, dhz, Cz, dHz, dcz, m0, n0, t, T, M);
+  else
+    bwd_cell_<H, CfgNN, HEAD, true>(smem, Gz, dGz, dhz, Cz, dHz, dcz, m0, n0, t, T, M);
 }
 
 // GsAll: gates in; dGAll: dG out (== GsAll: in place) and the neighbours' dG read by the GEMM;
@@ -812,7 +842,7 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
                                                       const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
                                                       BwdWave wv, int L, int T, int M, Drop dr) {
-  __shared__ float smem[CfgNN::SMEM_FLOATS];
+  __shared__ float smem[epi_smem_floats<CfgNN>()];
   constexpr int G4 = 4 * H;
   const int p = wave_index(wv, (int)blockIdx.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
@@ -850,7 +880,10 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
       if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
   }
-  bwd_cell<H, CfgNN, SMAML_EPI_PRELOAD != 0>(acc, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, l, t, L, T, M);
+  if (l == L - 1 && t == T - 1)  // the head's dh_T enters at the top layer's last step only
+    bwd_cell<H, CfgNN, true>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
+  else
+    bwd_cell<H, CfgNN, false>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
 }
 
 // Split-K BPTT step for small grids (see k_lstm_fwd_part): partial dh over a K-tile range of the
@@ -895,6 +928,7 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell(const float* GsAll
                                                              const float* __restrict__ dHhead,
                                                              float* __restrict__ dcAll, int64_t lsz, BwdWave wv, int L,
                                                              int T, int M, int S, const float* __restrict__ part) {
+  __shared__ float smem[CfgNN::BM * CfgNN::BN];
   constexpr int G4 = 4 * H;
   const int p = wave_index(wv, (int)blockIdx.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
@@ -908,9 +942,15 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell(const float* GsAll
   for (int q = 0; q < S; ++q)
     add_part<CfgNN>(acc, part + (((int64_t)z * (S * ntn) + q * ntn + blockIdx.y) * gridDim.x + blockIdx.x) * PER);
   const int64_t slab = (int64_t)z * T * M;
-  bwd_cell<H, CfgNN, true>(acc, GsAll + (int64_t)l * lsz * 4 + slab * G4, dGAll + (int64_t)l * lsz * 4 + slab * G4,
-                     dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr, CsAll + (int64_t)l * lsz + slab * H,
-                     dHhead + (int64_t)z * M * H, dcAll + ((int64_t)l * gridDim.z + z) * M * H, m0, n0, l, t, L, T, M);
+  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dhz = dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr;
+  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
+  if (l == L - 1 && t == T - 1)
+    bwd_cell<H, CfgNN, true>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
+  else
+    bwd_cell<H, CfgNN, false>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
 }
 
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,

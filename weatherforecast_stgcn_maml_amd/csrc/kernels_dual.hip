@@ -324,6 +324,102 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
 using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
 using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_DUAL_BK>;
 
+// Tangent-only cell backward of a kept step (see kernels.hip bwd_cell_): R(dh) = the GEMM
+// accumulators, transposed through LDS so each lane works on float4 groups of 4 hidden units of
+// one row (16-B loads / stores); the primal cell backward is re-derived from the kept dh. Writes
+// R(dG) in place over R(G) (each item's elements are read before they are written) and both
+// cell-state carries.
+template <int H, class C, bool HEAD, bool CHECK>
+__device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const float* Gz, float* RGz,
+                                                    const float* __restrict__ dhz, const float* __restrict__ Cz,
+                                                    const float* __restrict__ RCz, const float* __restrict__ dHz,
+                                                    const float* __restrict__ RdHz, float* __restrict__ dcz,
+                                                    float* __restrict__ rdcz, int m0, int n0, int t, int T, int M) {
+  constexpr int G4 = 4 * H;
+  constexpr int GPR = C::BN / 4;
+  constexpr int NIT = C::BM * GPR / C::NTH;
+  static_assert(NIT * C::NTH == C::BM * GPR, "epilogue items");
+  const bool first = (t == T - 1), past = t > 0;
+  const int64_t pM = past ? (int64_t)M * H : 0;
+  const int64_t tM = (int64_t)t * M;
+  struct V {
+    float4 dh, g[4], rg[4], c, rc, cp, rcp, dc, rdc, rhd;
+  };
+  auto coords = [&](int k, int& r, int& m, int& j) {
+    const int item = (int)threadIdx.x + C::NTH * k;
+    r = item / GPR;
+    m = m0 + r;
+    j = n0 + 4 * (item % GPR);
+  };
+  auto load = [&](int k, V& v) {
+    int r, m, j;
+    coords(k, r, m, j);
+    if (CHECK) {
+      m = min(m, M - 1);
+      j = min(j, H - 4);
+    }
+    const int64_t row = tM + m;
+    const float* gp = Gz + row * G4 + j;
+    const float* rp = RGz + row * G4 + j;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      v.g[g] = ld4(gp + g * H);
+      v.rg[g] = ld4(rp + g * H);
+    }
+    v.dh = ld4(dhz + row * H + j);
+    v.c = ld4(Cz + row * H + j);
+    v.rc = ld4(RCz + row * H + j);
+    v.cp = ld4(Cz + row * H - pM + j);
+    v.rcp = ld4(RCz + row * H - pM + j);
+    v.dc = ld4(dcz + (int64_t)m * H + j);
+    v.rdc = ld4(rdcz + (int64_t)m * H + j);
+    if (HEAD) v.rhd = ld4(RdHz + (int64_t)m * H + j);
+  };
+  auto step = [&](int k, const V& v) {
+    int r, m, j;
+    coords(k, r, m, j);
+    if (CHECK && (m >= M || j >= H)) return;
+    const float4 acc = *reinterpret_cast<const float4*>(smem + r * C::BN + (j - n0));
+    float4 o[4], odc, ordc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float dh = f4get(v.dh, e);
+      const float rdh = f4get(acc, e) + (HEAD ? f4get(v.rhd, e) : 0.f);
+      const float gi = f4get(v.g[0], e), gf = f4get(v.g[1], e), gg = f4get(v.g[2], e), go = f4get(v.g[3], e);
+      const float ri = f4get(v.rg[0], e), rf = f4get(v.rg[1], e), rgg = f4get(v.rg[2], e), ro = f4get(v.rg[3], e);
+      const float c = f4get(v.c, e), rc = f4get(v.rc, e);
+      const float cp = past ? f4get(v.cp, e) : 0.f, rcp = past ? f4get(v.rcp, e) : 0.f;
+      const float dcin = first ? 0.f : f4get(v.dc, e), rdcin = first ? 0.f : f4get(v.rdc, e);
+      const float tc = tanhf_(c);
+      const float s2 = 1.f - tc * tc;
+      const float rtc = s2 * rc;
+      const float dct = dcin + dh * go * s2;
+      const float rdct = rdcin + rdh * go * s2 + dh * ro * s2 - 2.f * dh * go * tc * rtc;
+      const float si = gi * (1.f - gi), sf = gf * (1.f - gf), so = go * (1.f - go), sg = 1.f - gg * gg;
+      const float o0 = rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri;
+      const float o1 = rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf;
+      const float o2 = rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg;
+      const float o3 = rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro;
+      const float d0 = dct * gf, d1 = rdct * gf + dct * rf;
+      if (e == 0) { o[0].x = o0; o[1].x = o1; o[2].x = o2; o[3].x = o3; odc.x = d0; ordc.x = d1; }
+      if (e == 1) { o[0].y = o0; o[1].y = o1; o[2].y = o2; o[3].y = o3; odc.y = d0; ordc.y = d1; }
+      if (e == 2) { o[0].z = o0; o[1].z = o1; o[2].z = o2; o[3].z = o3; odc.z = d0; ordc.z = d1; }
+      if (e == 3) { o[0].w = o0; o[1].w = o1; o[2].w = o2; o[3].w = o3; odc.w = d0; ordc.w = d1; }
+    }
+    float* rp = RGz + (tM + m) * G4 + j;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) st4(rp + g * H, o[g]);
+    st4(dcz + (int64_t)m * H + j, odc);
+    st4(rdcz + (int64_t)m * H + j, ordc);
+  };
+  V v;
+#pragma unroll 1
+  for (int k = 0; k < NIT; ++k) {
+    load(k, v);
+    step(k, v);
+  }
+}
+
 // Tangent BPTT step, one anti-diagonal per launch (kernels.hip k_lstm_bwd_step; BwdWave):
 //   dh  = A . B,   R(dh) = A2 . B + A . B2   with  A = [dG(l+1,t) | dG(l,t+1)],
 //   A2 = [R dG(l+1,t) | R dG(l,t+1)],  B = [W_ih(l+1) ; W_hh(l)],  B2 = [U_ih(l+1) ; U_hh(l)]
@@ -344,6 +440,7 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                                       const float* __restrict__ U, int64_t tstride, BwdWave wv, int L,
                                                       int T, int M, Drop dr) {
   __shared__ float smem[DualStage<CfgNND>::FLOATS];
+  static_assert(DualStage<CfgNND>::FLOATS >= CfgNND::BM * CfgNND::BN, "epilogue transpose fits the staging LDS");
   constexpr int G4 = 4 * H;
   const int p = wave_index(wv, (int)blockIdx.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
@@ -399,6 +496,19 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   const float* dHz = dHhead + (int64_t)z * M * H;
   const float* RdHz = RdHhead + (int64_t)z * M * H;
   const bool full = m0 + CfgNND::BM <= M;
+  if constexpr (KEPT) {
+    acc_to_lds<CfgNND>(at, smem);
+    const bool nochk = full && n0 + CfgNND::BN <= H;
+#define SMAML_KEPT_EPI(HD, CK)                                                                          \
+  bwd_dual_kept_cell_<H, CfgNND, HD, CK>(smem, Gz, RGz, dhz, Cz, RCz, dHz, RdHz, dcz, rdcz, m0, n0, t, T, M)
+    if (head) {
+      if (nochk) SMAML_KEPT_EPI(true, false); else SMAML_KEPT_EPI(true, true);
+    } else {
+      if (nochk) SMAML_KEPT_EPI(false, false); else SMAML_KEPT_EPI(false, true);
+    }
+#undef SMAML_KEPT_EPI
+    return;
+  }
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
   for (int i = 0; i < CfgNND::WTM; ++i)

@@ -41,12 +41,9 @@
 #define SMAML_WGRAD_THREADS (3072 * 256)  // split-K target: total threads of one weight-gradient launch
                                           // (A/B at config 2: 2048 -> 3072 x 256: wgrad 747 -> 711 ms)
 #endif
-#ifndef SMAML_EPI_PRELOAD
-#define SMAML_EPI_PRELOAD 0  // fused step kernels: issue a row group's epilogue loads before its stores
-                             // (always on in the split-K cell kernels; spills the primal BPTT step)
-#endif
 #ifndef SMAML_EPI_PRELOAD_FWD
-#define SMAML_EPI_PRELOAD_FWD SMAML_EPI_PRELOAD  // same, for the fused forward step kernel
+#define SMAML_EPI_PRELOAD_FWD 1  // fused forward step: load a tile's c_{t-1} before its stores
+                                 // (r01 A/B: 339 -> 335.5 ms per meta-step)
 #endif
 #ifndef SMAML_TN_BK
 #define SMAML_TN_BK 16
@@ -252,16 +249,14 @@ __device__ __forceinline__ float sigmoidf_(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
 __device__ __forceinline__ float tanhf_(float x) {
+  // branchless (both forms, then a select): a per-element branch here splits the epilogues into
+  // exec-masked blocks and serialises their memory operations
   const float a = fabsf(x);
-  float r;
-  if (a < 0.125f) {
-    const float x2 = x * x;
-    r = x * fmaf(x2, fmaf(x2, fmaf(x2, -0.053968254f, 0.13333334f), -0.33333334f), 1.0f);
-  } else {
-    const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * a);
-    r = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e), x);
-  }
-  return r;
+  const float x2 = x * x;
+  const float p = x * fmaf(x2, fmaf(x2, fmaf(x2, -0.053968254f, 0.13333334f), -0.33333334f), 1.0f);
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * a);
+  const float r = copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e), x);
+  return a < 0.125f ? p : r;
 }
 #else
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
@@ -337,6 +332,25 @@ __device__ __forceinline__ void wave_problem(const WV& wv, int bx, int& l, int& 
   lo = wave_sel(wv.lo, p);
   b0 = wave_sel(wv.off, p);
 }
+
+// acc -> smem [BM][BN] (row-major), for epilogues that work on row-contiguous float4 groups
+// instead of the accumulator's column-per-lane layout; ends with a barrier. The caller's mainloop
+// must have retired its LDS reads (gemm_mainloop / gemm_dual_mainloop end with a barrier) and
+// smem must hold BM * BN floats.
+template <class C>
+__device__ __forceinline__ void acc_to_lds(const Acc<C>& acc, float* smem) {
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < C::WTN; ++jj) {
+      const int col = acc_col<C>(jj);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) smem[acc_row<C>(i, r) * C::BN + col] = acc.v[i][jj][r];
+    }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float4 sel4(bool c, float4 a) { return c ? a : f4zero(); }
 
 // Row offset (within the 32-row tile) of accumulator register r: (r&3) + 8*(r>>2).
 __device__ __forceinline__ constexpr int racc(int r) { return (r & 3) + 8 * (r >> 2); }
