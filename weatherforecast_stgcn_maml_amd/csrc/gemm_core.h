@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace smaml {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -76,20 +78,32 @@ struct GemmCfg {
   static constexpr int SMEM_FLOATS = 2 * (A_STAGE + B_STAGE);
 };
 
+// Loaders that fetch a whole operand tile themselves (``kTileFetch``; loaders.h "tile
+// loaders"): the K-tile's segment is chosen once per tile (uniform), rows are clamped instead of
+// zero-filled, so the loads compile to branch-free saddr + vgpr-offset loads.
+template <class L, class = void>
+struct has_tile_fetch : std::false_type {};
+template <class L>
+struct has_tile_fetch<L, std::void_t<decltype(L::kTileFetch)>> : std::true_type {};
+
 // Fetch this thread's share of one operand tile into registers.
 // KC: element (row r, k) ; MC: element (k, row r).  `row0`, `k0` absolute.
 template <int ROWS, int F4, int NTH, bool KC, int BK, class L>
 __device__ __forceinline__ void fetch_tile(const L& ld, int row0, int k0, float4 (&r)[F4]) {
-  const int tid = threadIdx.x;
+  if constexpr (has_tile_fetch<L>::value) {
+    ld.template fetch<ROWS, F4, NTH, KC, BK>(row0, k0, r);
+  } else {
+    const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < F4; ++i) {
-    const int f = tid + NTH * i;
-    if (KC) {
-      const int rr = f / (BK / 4), q = f % (BK / 4);
-      r[i] = ld(row0 + rr, k0 + 4 * q);
-    } else {
-      const int kk = f / (ROWS / 4), q = f % (ROWS / 4);
-      r[i] = ld(k0 + kk, row0 + 4 * q);
+    for (int i = 0; i < F4; ++i) {
+      const int f = tid + NTH * i;
+      if (KC) {
+        const int rr = f / (BK / 4), q = f % (BK / 4);
+        r[i] = ld(row0 + rr, k0 + 4 * q);
+      } else {
+        const int kk = f / (ROWS / 4), q = f % (ROWS / 4);
+        r[i] = ld(k0 + kk, row0 + 4 * q);
+      }
     }
   }
 }

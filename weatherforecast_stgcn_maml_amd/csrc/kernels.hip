@@ -305,8 +305,9 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     LstmFwdA<H, true> la{X + (slab + (int64_t)t * M) * cin, Hp, M, cin, xd};
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   } else {
-    LstmFwdA<H> la{X + (slab + (int64_t)t * M) * cin, Hp, M, cin, XDrop{}};
-    gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+    const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
+    const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
+    gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   }
 
   fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
@@ -423,8 +424,8 @@ __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
   Acc<CfgGate> acc;
   acc.zero();
   if (kbeg < kend) {
-    LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
-    LstmFwdA<H> la{X + (slab + (int64_t)t * M) * cin, Hp, M, cin, XDrop{}};
+    const SegGateBt<2> lb{{th + lo.wih, th + lo.whh}, {cin, H}, H};
+    const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
     gemm_mainloop<CfgGate>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
   store_part<CfgGate>(acc, part_slab<CfgGate>(part, S, (int)blockIdx.y));
@@ -875,8 +876,8 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
         gemm_mainloop<CfgNN>(SegKC{{pn, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
                              SegMC{{th + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, 0, G4, acc, smem);
     } else {
-      SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
-      SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
+      const SegKCt<2> la{{up ? pa : pn, pn}, {G4, G4}, M};
+      const SegMCt<2> lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H};
       if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
   }
@@ -913,8 +914,8 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_part(con
   Acc<CfgNN> acc;
   acc.zero();
   if (kbeg < kend) {
-    SegKC la{{up ? pa : pn, up ? pn : nullptr, nullptr, nullptr}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0, 0, 0}, M};
-    SegMC lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {ns >= 1 ? G4 : 0, ns >= 2 ? G4 : 0}, H};
+    const SegKCt<2> la{{up ? pa : pn, pn}, {G4, G4}, M};
+    const SegMCt<2> lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H};
     gemm_mainloop<CfgNN>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
   // slab of (z, y = split * ntn + tn, x)
@@ -1094,10 +1095,14 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
     } else {
       gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
-  } else if (tn == 0 && with_bias) {
-    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
-    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    // branch-free tile loaders (segment per tile, K tail / shifted rows zero-filled by selects)
+    const MCKt lat{la.p, la.K, la.cols};
+    const WgBt lbt{b.B1, b.B2, b.c1, b.c2, b.K, b.Mshift};
+    if (tn == 0 && with_bias)
+      gemm_mainloop<CfgTN, SMAML_IGLP>(lat, lbt, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    else
+      gemm_mainloop<CfgTN, SMAML_IGLP>(lat, lbt, m0, n0, (int)kbeg, (int)kend, acc, smem);
   }
   const int ncols = lb.c1 + lb.c2;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;

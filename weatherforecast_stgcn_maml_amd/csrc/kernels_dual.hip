@@ -105,7 +105,9 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
     else
-      gemm_mainloop<CfgGateD, SMAML_IGLP>(la, lb, m0, n0, 0, cin + wh, ap, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
+                                          SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, 0,
+                                          cin + wh, ap, smem);
     if (j < H) {
       float bp[4];
 #pragma unroll
@@ -141,7 +143,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else
-      gemm_mainloop<CfgGateD, SMAML_IGLP>(la, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
+                                          SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
+                                                       {cin, wh, wrx, wh}, H},
+                                          m0, n0, 0, cin + wh + wrx + wh, at, smem);
   }
   if (j >= H) return;
   float bu[4];
@@ -488,7 +493,12 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                           SegMC{{th + lo.whh, nullptr}, {G4, 0}, H},
                                           SegMC{{u + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, G4, 0, ap, at, smem);
     } else if (ns) {
-      gemm_dual_mainloop<CfgNND, !KEPT>(la, la2, lb, lb2, m0, n0, ns * G4, 0, ap, at, smem);
+      const float* a0 = up ? dGAll + oa : dGz + on;
+      const float* r0 = up ? RGsAll + oa : RGz + on;
+      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, dGz + on}, {G4, G4}, M}, SegKCt<2>{{r0, RGz + on}, {G4, G4}, M},
+                                        SegMCt<2>{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H},
+                                        SegMCt<2>{{up ? u + wih_up : u + lo.whh, u + lo.whh}, {G4, G4}, H}, m0, n0,
+                                        ns * G4, 0, ap, at, smem);
     }
   }
   const bool first = (t == T - 1);

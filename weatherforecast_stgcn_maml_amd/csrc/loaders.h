@@ -183,6 +183,163 @@ struct WgB {
   }
 };
 
+// ---- tile loaders (gemm_core.h has_tile_fetch) -------------------------------------------
+// Contract: every segment width is a multiple of BK (so a K-tile lies inside one segment, chosen
+// once per tile with scalar code) and the GEMM's K is the sum of the widths (no K tail). Rows /
+// columns past the matrix edge are CLAMPED to the last valid one instead of zero-filled: their
+// products land in accumulator rows / columns the epilogues never store. Offsets are 32-bit
+// byte offsets from a uniform base (global_load ... saddr): every segment slab is < 4 GiB.
+__device__ __forceinline__ float4 ldo(const float* base, uint32_t byteoff) {
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byteoff);
+}
+
+// KC operand [rows][w_s] per segment (row stride = width), k-concatenated.
+template <int NS>
+struct SegKCt {
+  static constexpr bool kTileFetch = true;
+  const float* p[NS];
+  int w[NS];
+  int rows;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch(int row0, int k0, float4 (&r)[F4]) const {
+    static_assert(KC, "SegKCt is a k-contiguous operand");
+    const float* b = p[0];
+    int ws = w[0], kk = k0;
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
+      if (kk >= ws) {
+        kk -= ws;
+        b = p[s];
+        ws = w[s];
+      }
+    b += kk;
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int row = min(row0 + f / (BK / 4), rows - 1);
+      r[i] = ldo(b, 4u * (uint32_t)(row * ws + 4 * (f % (BK / 4))));
+    }
+  }
+};
+
+// MC operand [K_s][cols] per segment (cols contiguous), k-concatenated.
+template <int NS>
+struct SegMCt {
+  static constexpr bool kTileFetch = true;
+  const float* p[NS];
+  int K[NS];
+  int cols;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch(int col0, int k0, float4 (&r)[F4]) const {
+    static_assert(!KC, "SegMCt is an n-contiguous operand");
+    const float* b = p[0];
+    int ks = K[0], kk = k0;
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
+      if (kk >= ks) {
+        kk -= ks;
+        b = p[s];
+        ks = K[s];
+      }
+    b += (int64_t)kk * cols;
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int c = min(col0 + 4 * (f % (ROWS / 4)), cols - 4);
+      r[i] = ldo(b, 4u * (uint32_t)((f / (ROWS / 4)) * cols + c));
+    }
+  }
+};
+
+// LSTM gate-GEMM B operand (SegGateB's row mapping: logical row n = ug*128 + g*32 + jj ->
+// weight row g*H + ug*32 + jj of each [4H][w_s] segment), k-concatenated.
+template <int NS>
+struct SegGateBt {
+  static constexpr bool kTileFetch = true;
+  const float* p[NS];
+  int w[NS];
+  int H;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch(int n0, int k0, float4 (&r)[F4]) const {
+    static_assert(KC, "SegGateBt is a k-contiguous operand");
+    const float* b = p[0];
+    int ws = w[0], kk = k0;
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
+      if (kk >= ws) {
+        kk -= ws;
+        b = p[s];
+        ws = w[s];
+      }
+    b += kk;
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int n = n0 + f / (BK / 4);
+      const int ug = n >> 7, rem = n & 127;
+      const int j = min(ug * 32 + (rem & 31), H - 1);
+      const int row = (rem >> 5) * H + j;
+      r[i] = ldo(b, 4u * (uint32_t)(row * ws + 4 * (f % (BK / 4))));
+    }
+  }
+};
+
+// MC operand [K][cols] (cols contiguous) with zero rows at k >= K (split-K weight gradients: the
+// K tail is real, so it is zero-filled by a select, not clamped).
+struct MCKt {
+  static constexpr bool kTileFetch = true;
+  const float* p;
+  int64_t K;
+  int cols;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch(int col0, int k0, float4 (&r)[F4]) const {
+    static_assert(!KC, "MCKt is an n-contiguous operand");
+    const float* b = p + (int64_t)k0 * cols;
+    const int kmax = (int)min<int64_t>(K - k0, (int64_t)BK) - 1;  // last valid k row of this tile
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int kk = f / (ROWS / 4);
+      const int c = min(col0 + 4 * (f % (ROWS / 4)), cols - 4);
+      const float4 v = ldo(b, 4u * (uint32_t)(min(kk, kmax) * cols + c));
+      r[i] = kk <= kmax ? v : f4zero();
+    }
+  }
+};
+
+// Weight-gradient B operand (WgB) as a tile loader: Bcat[k] = [B1[k] (c1) | B2[k - Mshift] (c2)],
+// zero for k >= K, for B2 rows k < Mshift (h_{-1} = 0) and for a null B1 (no layer-0 tangent). A
+// BN-wide column tile lies inside one of the two blocks (c1 is a multiple of BN).
+struct WgBt {
+  static constexpr bool kTileFetch = true;
+  const float* B1;
+  const float* B2;
+  int c1, c2;
+  int64_t K, Mshift;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch(int col0, int k0, float4 (&r)[F4]) const {
+    static_assert(!KC, "WgBt is an n-contiguous operand");
+    const bool first = col0 < c1;  // uniform: which block this column tile reads
+    const int ld = first ? c1 : c2;
+    const int cbase = first ? col0 : col0 - c1;
+    const int64_t shift = first ? 0 : Mshift;
+    const float* src = first ? B1 : B2;
+    const int64_t kv0 = (int64_t)k0 - shift;  // source row of the tile's first k
+    const int64_t nrows = K - shift;          // valid source rows [0, nrows)
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int kk = f / (ROWS / 4);
+      const int c = min(cbase + 4 * (f % (ROWS / 4)), ld - 4);
+      const int64_t ks = kv0 + kk;
+      const bool ok = src && ks >= 0 && ks < nrows;
+      const int64_t kc = ks < 0 ? 0 : (ks >= nrows ? nrows - 1 : ks);
+      const float4 v = src ? ldo(src + kc * ld, 4u * (uint32_t)c) : f4zero();
+      r[i] = ok ? v : f4zero();
+    }
+  }
+};
+
 // Dropout mask on the x segment of an LSTM layer's input: x = drop(h_{l-1}) of one
 // (task, t) slab; element (m, k) has index base + m*H + k (kernels.h Drop, kind 2).
 struct XDrop {
