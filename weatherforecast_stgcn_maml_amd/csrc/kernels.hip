@@ -114,6 +114,10 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
   const int q0 = m0 - (int)la.rps_div.div((uint32_t)m0) * la.rps;
   if (q0 < la.ell_rows || q0 + CfgGcn::BM > la.rps) {
     gemm_mainloop<CfgGcn, SMAML_IGLP>(la, lb, m0, n0, 0, la.cin, acc, smem);
+  } else if (la.buf && la.cin % CfgGcn::BK == 0) {
+    // layers 2-4 away from the t = 0 rows: plain row-major operands, branch-free tile loaders
+    gemm_mainloop<CfgGcn, SMAML_IGLP>(SegKCt<1>{{la.buf}, {la.cin}, la.R}, SegKCt<1>{{lb.p}, {lb.K}, lb.rows}, m0,
+                                      n0, 0, la.cin, acc, smem);
   } else {
     const GcnPlain lp{la.tab, la.buf, la.rps_div, la.rps, la.cin, la.R};
     gemm_mainloop<CfgGcn, SMAML_IGLP>(lp, lb, m0, n0, 0, la.cin, acc, smem);
@@ -1095,14 +1099,12 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
     } else {
       gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
+  } else if (tn == 0 && with_bias) {
+    // (the branch-free MCKt / WgBt tile loaders measured slower here: wgrad 723 -> 820 ms per
+    // meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log)
+    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
-    // branch-free tile loaders (segment per tile, K tail / shifted rows zero-filled by selects)
-    const MCKt lat{la.p, la.K, la.cols};
-    const WgBt lbt{b.B1, b.B2, b.c1, b.c2, b.K, b.Mshift};
-    if (tn == 0 && with_bias)
-      gemm_mainloop<CfgTN, SMAML_IGLP>(lat, lbt, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
-    else
-      gemm_mainloop<CfgTN, SMAML_IGLP>(lat, lbt, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
   }
   const int ncols = lb.c1 + lb.c2;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;

@@ -187,8 +187,8 @@ struct WgB {
 // Contract: every segment width is a multiple of BK (so a K-tile lies inside one segment, chosen
 // once per tile with scalar code) and the GEMM's K is the sum of the widths (no K tail). Rows /
 // columns past the matrix edge are CLAMPED to the last valid one instead of zero-filled: their
-// products land in accumulator rows / columns the epilogues never store. Offsets are 32-bit
-// byte offsets from a uniform base (global_load ... saddr): every segment slab is < 4 GiB.
+// products land in accumulator rows / columns the epilogues never store. Per-lane offsets are
+// 32-bit byte offsets from a uniform 64-bit tile base (global_load ... saddr).
 __device__ __forceinline__ float4 ldo(const float* base, uint32_t byteoff) {
   return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byteoff);
 }
@@ -212,12 +212,12 @@ struct SegKCt {
         b = p[s];
         ws = w[s];
       }
-    b += kk;
+    b += kk + (int64_t)row0 * ws;  // the tile's first row: 64-bit, uniform
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
       const int f = (int)threadIdx.x + NTH * i;
-      const int row = min(row0 + f / (BK / 4), rows - 1);
-      r[i] = ldo(b, 4u * (uint32_t)(row * ws + 4 * (f % (BK / 4))));
+      const int dr = min(row0 + f / (BK / 4), rows - 1) - row0;
+      r[i] = ldo(b, 4u * (uint32_t)(dr * ws + 4 * (f % (BK / 4))));
     }
   }
 };
@@ -308,8 +308,9 @@ struct MCKt {
 };
 
 // Weight-gradient B operand (WgB) as a tile loader: Bcat[k] = [B1[k] (c1) | B2[k - Mshift] (c2)],
-// zero for k >= K, for B2 rows k < Mshift (h_{-1} = 0) and for a null B1 (no layer-0 tangent). A
-// BN-wide column tile lies inside one of the two blocks (c1 is a multiple of BN).
+// zero for k >= K, for B2 rows k < Mshift (h_{-1} = 0) and for a null B1 (no layer-0 tangent).
+// Requires every BN-wide column tile to lie inside one block (c1 a multiple of BN, or c2 = 0);
+// k_wgrad falls back to WgB otherwise.
 struct WgBt {
   static constexpr bool kTileFetch = true;
   const float* B1;
