@@ -220,7 +220,7 @@ struct smaml_ctx {
   Staging stage;
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
-  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX};
+  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -298,7 +298,10 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   const int64_t seq = (int64_t)zbc * d.N;
   int max_cin = std::max(d.Hc, d.H);
   const int64_t wpart = std::max<int64_t>((int64_t)zc * G * (max_cin + d.H + 1) * SMAML_WGRAD_MAXSPLIT, 1 << 24);
-  const int64_t lblk = (int64_t)zc * ((seq + 127) / 128 + 1);
+  // loss partials per task: head_lblocks(M) for every per-task row count M <= seq
+  const int64_t lblk =
+      (int64_t)zc * (std::max<int64_t>(head_lblocks(d, (int)std::min<int64_t>(seq, SMAML_HEAD_SMALL_M)),
+                                       (seq + 127) / 128) + 1);
   std::vector<std::pair<void**, int64_t>> parts;  // (dst, bytes)
   Work w{};
   parts.push_back({(void**)&w.F, rows * d.Hc * 4});
@@ -526,7 +529,7 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.Z = Z;
   c->w.B = B;
   c->w.M = B * c->d.N;
-  c->w.lblocks = (c->w.M + 127) / 128;
+  c->w.lblocks = head_lblocks(c->d, c->w.M);
   c->w.F = c->F_main;
   c->w.primal_kept = 0;
   c->w.drop = Drop{};  // dropout only inside smaml_meta_step / smaml_adapt_steps (set_step_drop)
@@ -620,6 +623,11 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
   int64_t hz = 0;
   const float* hT = head_input(d, w, false, &hz);  // h_T, or drop(h_T) under dropout
+  if (head_small(d, w.M)) {
+    TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
+          launch_head_wgrad_small(s, d, w, w.dpred, hT, hz, grad, po.P, po.wo, po.bo));
+    return run_bptt(c, s, theta, tstride, grad);
+  }
   timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, hT, hz, d.H, nullptr, 0, 0,
                      w.M, 0, grad, po.P, po.wo, -1, po.bo, -1);
   return run_bptt(c, s, theta, tstride, grad);
@@ -632,7 +640,11 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   const ParamOff& po = c->po;
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
-  // BPTT as reverse anti-diagonals; layer l's weight gradient as soon as its t = 0 step is done
+  // BPTT as reverse anti-diagonals; layer l's weight gradient as soon as its t = 0 step is done,
+  // or, for small grids (batch-1 adaptation), all layers' in one launch after the sweep
+  const bool grouped = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows;
+  WgradPlan plans[MAX_LAYERS];
+  double gfl = 0.0;
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
     const double fl = bwd_wave(d, w, po, e, 0, false, wv);
@@ -641,10 +653,21 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     if (e < d.T - 1 || l < 0) continue;
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
+    if (grouped) {
+      WgradPlan& p = plans[l];
+      plan_wgrad(w, w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
+                 w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true,
+                 false, p);
+      p.drop = w.drop;
+      p.drop_layer = l - 1;
+      gfl += 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H);
+      continue;
+    }
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
                        w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
                        lo.bhh, true, false, l - 1);
   }
+  if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1047,13 +1070,15 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     TRY(run_backward(c, s, c->fast, P, c->grad));
     use_primal(c, SET_MAIN);
     float* V = c->grad;
+    if (steps > 0)
+      TIMED(c, s, C_MISC, 0, launch_dot(s, c->so_grad + (int64_t)(steps - 1) * Z * P, V, P, Z, c->w.sqpart));
     for (int k = steps - 1; k >= 0; --k) {
       const float* th = c->so_theta + (int64_t)k * Z * P;
       const float* gk = c->so_grad + (int64_t)k * Z * P;
       const float* const* xt = c->xtab + (int64_t)k * Z * B;
       TIMED(c, s, C_MISC, 0,
-            launch_so_dir(s, V, gk, P, Z, c->w.sqpart, c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z,
-                          max_norm, c->so_u));
+            launch_so_dir_only(s, V, gk, P, Z, c->w.sqpart, c->so_norm + (int64_t)k * Z,
+                               c->so_coef + (int64_t)k * Z, max_norm, c->so_u));
       c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
       const int slot = steps - 1 - k;
       use_primal(c, slot < nkeep ? slot : SET_MAIN);
@@ -1062,7 +1087,11 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
-      TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
+      if (k > 0)  // v_k = v_{k+1} - lr H_k w_k, and step k-1's dot g_{k-1} . v_k in the same pass
+        TIMED(c, s, C_MISC, 0,
+              launch_axpy_dot(s, V, c->so_hu, -inner_lr, c->so_grad + (int64_t)(k - 1) * Z * P, P, Z, c->w.sqpart));
+      else
+        TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
       c->w.primal_kept = 0;
     }
     use_primal(c, SET_MAIN);
@@ -1191,6 +1220,10 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bwdd_big_min = (int)std::min<int64_t>(value, 1 << 30);
   } else if (k == "split_max" && value >= 1) {
     c->kn.split_max = (int)std::min<int64_t>(value, 64);
+  } else if (k == "wgrad_group_max_rows" && value >= 0) {
+    c->kn.wgrad_group_max_rows = (int)std::min<int64_t>(value, 1 << 30);
+  } else if (k == "wgrad_group_wgs" && value >= 1) {
+    c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {
     c->keep_max = (int)std::min<int64_t>(value, 1 << 20);
     c->keep_tried_K = -1;  // re-plan the kept slots on the next second-order meta-step

@@ -244,6 +244,56 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
   gemm_mainloop<C, IG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
 }
 
+// Chunked mainloop for short K ranges (the split-K steps of small grids): with one wave per SIMD
+// and a handful of K-tiles per workgroup, the double-buffered loop above pays one global-load
+// latency per K-tile. Here NCH K-tiles are fetched per round trip (registers), staged into NCH
+// LDS slots and then consumed, and chunk c+1's loads are in flight under chunk c's MFMAs.
+// LDS: NCH * (A_STAGE + B_STAGE) floats (chunked_smem_floats).
+template <class C, int NCH>
+constexpr int chunked_smem_floats() {
+  return NCH * (C::A_STAGE + C::B_STAGE);
+}
+template <class C, int NCH, class LA, class LB>
+__device__ __forceinline__ void gemm_mainloop_chunked(const LA& la, const LB& lb, int m0, int n0, int kbeg,
+                                                      int kend, Acc<C>& acc, float* smem) {
+  constexpr int BKc = C::BK;
+  float* As = smem;
+  float* Bs = smem + NCH * C::A_STAGE;
+  const int nkt = (kend - kbeg + BKc - 1) / BKc;
+  if (nkt <= 0) return;
+  float4 ra[NCH][C::A_F4], rb[NCH][C::B_F4];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (c0 + i < nkt) {
+        fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (c0 + i) * BKc, ra[i]);
+        fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg + (c0 + i) * BKc, rb[i]);
+      }
+  };
+  fetch(0);
+  NoHook hook;
+  for (int c0 = 0; c0 < nkt; c0 += NCH) {
+    if (c0 > 0) __syncthreads();  // the previous chunk's MFMAs have read their slots
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (c0 + i < nkt) {
+        store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, BKc>(As + i * C::A_STAGE, ra[i]);
+        store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(Bs + i * C::B_STAGE, rb[i]);
+      }
+    __syncthreads();
+    if (c0 + NCH < nkt) fetch(c0 + NCH);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (c0 + i < nkt) mma_tile<C>(As + i * C::A_STAGE, Bs + i * C::B_STAGE, acc, hook);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  }
+}
+
 }  // namespace smaml
 
 namespace smaml {

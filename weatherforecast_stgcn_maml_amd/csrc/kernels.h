@@ -106,7 +106,15 @@ struct Knobs {
   int bwd_big_min;   // BPTT launches with >= this many 64x128 tiles use them (else 64x64 / split-K)
   int bwdd_big_min;  // same, tangent BPTT
   int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
+  int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
+  int wgrad_group_wgs;       // workgroups that grouped launch aims for
 };
+#ifndef SMAML_WGRAD_GROUP_ROWS
+#define SMAML_WGRAD_GROUP_ROWS 2048
+#endif
+#ifndef SMAML_WGRAD_GROUP_WGS
+#define SMAML_WGRAD_GROUP_WGS 256
+#endif
 
 // Activations of one forward pass for Z tasks x B samples (M = B*N sequences per task).
 struct Work {
@@ -183,6 +191,15 @@ void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* 
 void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float* hT, const float* theta,
                         const ParamOff& po, const float* const* ytab, float* pred, float* dpred, float dscale);
 void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out);
+#ifndef SMAML_HEAD_SMALL_M
+#define SMAML_HEAD_SMALL_M 2048  // rows per task up to which the head runs as a SIMT kernel
+#endif
+#define SMAML_HEAD_MAX_H 128  // (SIMT head: H <= this, H * 8 threads per weight-gradient workgroup)
+bool head_small(const Dims& d, int M);
+int head_lblocks(const Dims& d, int M);  // loss partials per task written by the head launch
+// head weight gradient (dWo, dbo) for head_small() sizes; overwrites
+void launch_head_wgrad_small(hipStream_t s, const Dims& d, const Work& w, const float* dpred, const float* hT,
+                             int64_t hz, float* grad, int64_t P, int64_t wo, int64_t bo);
 // dst[z] = drop(src[z]) with the head-input mask ([M][H] rows per task; src == dst allowed)
 void launch_drop_rows(hipStream_t s, const Work& w, int H, const float* src, int64_t src_zstride, float* dst);
 // x[i] = drop(x[i]) in place with the GCN-output masks (kind 1, `layer`, step 0, task 0, sample 0):
@@ -223,6 +240,14 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
                 int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                 int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,
                 WgradPlan& p);
+// Several plans (same Z) in one GEMM launch + one reduce launch; their nsplit / kchunk / part are
+// re-planned for about target_wgs workgroups in total (partial slabs must fit w.wpart).
+struct WgMulti {
+  int n;
+  int blk[MAX_LAYERS], rblk[MAX_LAYERS];
+  WgradPlan p[MAX_LAYERS];
+};
+void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs);
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
 void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part);
@@ -249,5 +274,12 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
 void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,
                    const float* coefs, float max_norm, float* U);
 void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha);
+// the second-order sweep's bookkeeping in two launches per inner step: dot partials g . v
+// (launch_dot for the first step, then fused into the previous step's v update), then u
+void launch_dot(hipStream_t s, const float* G, const float* V, int64_t P, int Z, double* part);
+void launch_axpy_dot(hipStream_t s, float* V, const float* X, float alpha, const float* Gn, int64_t P, int Z,
+                     double* part);
+void launch_so_dir_only(hipStream_t s, const float* V, const float* G, int64_t P, int Z, const double* part,
+                        const float* norms, const float* coefs, float max_norm, float* U);
 
 }  // namespace smaml

@@ -404,11 +404,32 @@ __device__ __forceinline__ void split_range(int K, int S, int split, int bk, int
   kend = min(K, kbeg + per * bk);
 }
 
+#ifndef SMAML_FWD_PART_NCH
+#define SMAML_FWD_PART_NCH 3  // K-tiles per load round trip in the split-K gate step (0: double-buffered loop)
+#endif
+#ifndef SMAML_BWD_PART_NCH
+#define SMAML_BWD_PART_NCH 8  // same, split-K BPTT step
+#endif
+template <class C, int NCH>
+constexpr int part_smem_floats() {
+  return NCH > 0 && chunked_smem_floats<C, (NCH > 0 ? NCH : 1)>() > C::SMEM_FLOATS
+             ? chunked_smem_floats<C, (NCH > 0 ? NCH : 1)>()
+             : C::SMEM_FLOATS;
+}
+template <class C, int NCH, class LA, class LB>
+__device__ __forceinline__ void part_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
+                                              Acc<C>& acc, float* smem) {
+  if constexpr (NCH > 0)
+    gemm_mainloop_chunked<C, NCH>(la, lb, m0, n0, kbeg, kend, acc, smem);
+  else
+    gemm_mainloop<C>(la, lb, m0, n0, kbeg, kend, acc, smem);
+}
+
 template <int H>
 __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
     const float* __restrict__ F, const float* __restrict__ HsAll, int64_t lsz, const float* __restrict__ theta,
     int64_t tstride, FwdWave wv, int T, int M, int S, float* __restrict__ part) {
-  __shared__ float smem[CfgGate::SMEM_FLOATS];
+  __shared__ float smem[part_smem_floats<CfgGate, SMAML_FWD_PART_NCH>()];
   int l, t, b0;
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
@@ -430,7 +451,7 @@ __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
   if (kbeg < kend) {
     const SegGateBt<2> lb{{th + lo.wih, th + lo.whh}, {cin, H}, H};
     const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
-    gemm_mainloop<CfgGate>(la, lb, m0, n0, kbeg, kend, acc, smem);
+    part_mainloop<CfgGate, SMAML_FWD_PART_NCH>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
   store_part<CfgGate>(acc, part_slab<CfgGate>(part, S, (int)blockIdx.y));
 }
@@ -458,6 +479,79 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restric
               CsAll + (int64_t)l * lsz + slab * H, HsAll + (int64_t)l * lsz + slab * H, tm * CfgGate::BM, ug, t, M);
 }
 
+// The same cell step spread over 4x the threads: blockIdx.y = q picks accumulator registers
+// 4q..4q+3 (4 rows) of every gate, so each thread's S x 4 partial loads are independent and
+// in flight together, then 4 rows' c_{t-1} loads. Sums the partials in the same order as
+// k_lstm_fwd_cell (bitwise identical results).
+template <int H>
+__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell_q(float* __restrict__ HsAll, float* __restrict__ CsAll,
+                                                                 float* __restrict__ GsAll, int64_t lsz,
+                                                                 const float* __restrict__ theta, int64_t tstride,
+                                                                 FwdWave wv, int T, int M, int S,
+                                                                 const float* __restrict__ part) {
+  static_assert(CfgGate::WTM == 1 && CfgGate::WTN == 4, "one 32-row tile of 4 gates per wave");
+  constexpr int PER = CfgGate::WTM * CfgGate::WTN * 16 * CfgGate::NTH;
+  constexpr int UPB = CfgGate::WAVES_N;
+  int l, t, b0;
+  LayerOff lo;
+  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  int tm, ug;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+    return;
+  const int q = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
+  const float* base = part + ((int64_t)z * gridDim.x + blockIdx.x) * S * PER + 4 * (q * CfgGate::NTH + tid);
+  float4 a[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) a[g] = f4zero();
+  for (int sp = 0; sp < S; ++sp)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 v = ld4(base + (int64_t)sp * PER + 4 * (g * 4 * CfgGate::NTH));
+      a[g] = make_float4(a[g].x + v.x, a[g].y + v.y, a[g].z + v.z, a[g].w + v.w);
+    }
+  const float* th = theta + (int64_t)z * tstride;
+  const int j = (ug * UPB + (tid >> 6) % UPB) * 32 + (tid & 31);
+  if (j >= H) return;
+  float bsum[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bsum[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
+  const int64_t slab = (int64_t)z * T * M;
+  float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * (4 * H);
+  float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* Hz = HsAll + (int64_t)l * lsz + slab * H;
+  const int rb = tm * CfgGate::BM + acc_row<CfgGate>(0, 0) + 8 * q;  // row of register 4q
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
+  float cpv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int m = rb + e;
+    cpv[e] = (t > 0 && m < M) ? ldb(Cz, 4u * ((tM - (uint32_t)M + (uint32_t)m) * H + j)) : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int m = rb + e;
+    if (m >= M) continue;
+    const uint32_t row = tM + (uint32_t)m;
+    const uint32_t oh = row * H + j;
+    const uint32_t og = row * (4 * H) + j;
+    const float gi = sigmoidf_(f4get(a[0], e) + bsum[0]);
+    const float gf = sigmoidf_(f4get(a[1], e) + bsum[1]);
+    const float gg = tanhf_(f4get(a[2], e) + bsum[2]);
+    const float go = sigmoidf_(f4get(a[3], e) + bsum[3]);
+    const float c = gf * cpv[e] + gi * gg;
+    const float h = go * tanhf_(c);
+    stb(Gz, 4u * (og), gi);
+    stb(Gz, 4u * (og + H), gf);
+    stb(Gz, 4u * (og + 2 * H), gg);
+    stb(Gz, 4u * (og + 3 * H), go);
+    stb(Cz, 4u * (oh), c);
+    stb(Hz, 4u * (oh), h);
+  }
+}
+#ifndef SMAML_FWD_CELL_Q
+#define SMAML_FWD_CELL_Q 1  // split-K gate step's cell kernel over 4x the threads (0: k_lstm_fwd_cell)
+#endif
+
 #ifndef SMAML_SPLIT_WGS
 #define SMAML_SPLIT_WGS 256  // split while the launch stays within this many workgroups
 #endif
@@ -478,7 +572,7 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   const int ntm = (w.M + CfgGate::BM - 1) / CfgGate::BM;
   const int ngrp = (d.H + 32 * CfgGate::WAVES_N - 1) / (32 * CfgGate::WAVES_N);
   FwdWave wv{};
-  const double fl = fwd_wave(d, w, po, diag, (ntm + 7) / 8 * 8 * ngrp, false, wv);
+  const double fl = fwd_wave(d, w, po, diag, gate_blocks(ntm, ngrp), false, wv);
   if (flops) *flops = fl;
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
@@ -499,8 +593,14 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
       dim3 gp(grid.x, S, grid.z);
       SMAML_DISPATCH_H(d.H, k_lstm_fwd_part<HT><<<gp, CfgGate::NTH, 0, s>>>(w.F, w.Hs, lsz, theta, tstride, wv,
                                                                               d.T, w.M, S, w.wpart));
-      SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell<HT><<<grid, CfgGate::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
-                                                                               wv, d.T, w.M, S, w.wpart));
+      if (SMAML_FWD_CELL_Q) {
+        dim3 gq(grid.x, 4, grid.z);
+        SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell_q<HT><<<gq, CfgGate::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
+                                                                                 wv, d.T, w.M, S, w.wpart));
+      } else {
+        SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell<HT><<<grid, CfgGate::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta,
+                                                                                 tstride, wv, d.T, w.M, S, w.wpart));
+      }
       return;
     }
   }
@@ -606,6 +706,107 @@ const float* head_input(const Dims& d, const Work& w, bool tangent, int64_t* zst
   return (tangent ? w.RHs : w.Hs) + (int64_t)(d.L - 1) * lsz + (int64_t)(d.T - 1) * w.M * d.H;
 }
 
+// Small-M head (batch-1 adaptation: M = 441 rows): the MFMA tile kernel above gets ceil(M/128)
+// workgroups and a serial epilogue. Here one workgroup per row m (one thread per output column):
+// h_T[m] is staged in LDS, each thread streams its Wo row (L2-resident) with all loads in flight.
+// Loss partial per row (head_lblocks = M), summed in row order by k_loss_final.
+__global__ __launch_bounds__(128) void k_head_loss_small(const float* __restrict__ hT_base, int64_t hT_zstride,
+                                                         const float* __restrict__ theta, int64_t tstride, int64_t wo,
+                                                         int64_t bo, const float* const* __restrict__ xtab,
+                                                         float* __restrict__ pred, float* __restrict__ dpred,
+                                                         float* __restrict__ lpart, int lblocks, int M, int H, int HfC,
+                                                         int N, int Hf, int C, int yrow0, int yld, int B, float dscale) {
+  __shared__ float hs[SMAML_HEAD_MAX_H];
+  __shared__ float red[2];
+  const int z = blockIdx.z, m = blockIdx.x, cc = threadIdx.x;
+  const float* th = theta + (int64_t)z * tstride;
+  const float* h = hT_base + (int64_t)z * hT_zstride + (int64_t)m * H;
+  for (int k = cc; k < H; k += blockDim.x) hs[k] = h[k];
+  __syncthreads();
+  float lsum = 0.f;
+  if (cc < HfC) {
+    const float* wr = th + wo + (int64_t)cc * H;
+    float4 acc = f4zero();
+#pragma unroll 8
+    for (int k = 0; k < H; k += 4) {
+      const float4 wv = ld4(wr + k);
+      const float4 hv = *reinterpret_cast<const float4*>(hs + k);
+      acc = make_float4(fmaf(wv.x, hv.x, acc.x), fmaf(wv.y, hv.y, acc.y), fmaf(wv.z, hv.z, acc.z),
+                        fmaf(wv.w, hv.w, acc.w));
+    }
+    const float p = ((acc.x + acc.y) + (acc.z + acc.w)) + th[bo + cc];
+    const int64_t o = ((int64_t)z * M + m) * HfC + cc;
+    if (pred) pred[o] = p;
+    if (xtab) {
+      const int sm = m / N, n = m - sm * N;
+      const int hh = cc / C, c = cc - hh * C;
+      const int rr = n * Hf + hh;  // F4 pairing (see k_head_loss)
+      const int hp = rr / N, np = rr - hp * N;
+      const float df = p - xtab[z * B + sm][((int64_t)(yrow0 + hp) * N + np) * yld + c];
+      lsum = df * df;
+      if (dpred) dpred[o] = dscale * df;
+    }
+  }
+  if (lpart) {
+    // fixed-order block sum over the (<= 2) waves
+    float v = lsum;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) lpart[(int64_t)z * lblocks + m] = blockDim.x > 64 ? red[0] + red[1] : red[0];
+  }
+}
+
+bool head_small(const Dims& d, int M) {
+  return M <= SMAML_HEAD_SMALL_M && d.HfC <= 128 && d.H % 4 == 0 && d.H <= SMAML_HEAD_MAX_H;
+}
+int head_lblocks(const Dims& d, int M) { return head_small(d, M) ? M : (M + CfgNT::BM - 1) / CfgNT::BM; }
+static int head_small_threads(const Dims& d) { return d.HfC > 64 ? 128 : 64; }
+
+// dWo[c][j] = sum_m dpred[m][c] h_T[m][j], dbo[c] = sum_m dpred[m][c] for small M: one workgroup
+// per output row c, HW row groups x H units; each row group sums its contiguous share of the rows
+// in order, then the groups are added in a fixed order through LDS (deterministic).
+constexpr int HWG = 8;  // row groups
+__global__ __launch_bounds__(1024) void k_head_wgrad_small(const float* __restrict__ dpred, int64_t dp_zstride,
+                                                         const float* __restrict__ hT, int64_t hz, int M, int H,
+                                                         int HfC, float* __restrict__ grad, int64_t P, int64_t wo,
+                                                         int64_t bo) {
+  __shared__ float red[HWG][SMAML_HEAD_MAX_H + 1];
+  const int c = blockIdx.x, z = blockIdx.y, j = threadIdx.x % H, rg = threadIdx.x / H;
+  const float* dp = dpred + (int64_t)z * dp_zstride + c;
+  const float* h = hT + (int64_t)z * hz + j;
+  const int per = (M + HWG - 1) / HWG, mb = rg * per, me = min(M, mb + per);
+  float a = 0.f, b = 0.f;
+#pragma unroll 8
+  for (int m = mb; m < me; ++m) {
+    const float d0 = dp[(int64_t)m * HfC];
+    a = fmaf(d0, h[(int64_t)m * H], a);
+    b += d0;
+  }
+  red[rg][j] = a;
+  if (j == 0) red[rg][H] = b;
+  __syncthreads();
+  if (rg == 0) {
+    float s = 0.f, sb = 0.f;
+#pragma unroll
+    for (int g = 0; g < HWG; ++g) s += red[g][j];
+    float* gz = grad + (int64_t)z * P;
+    gz[wo + (int64_t)c * H + j] = s;
+    if (j == 0) {
+#pragma unroll
+      for (int g = 0; g < HWG; ++g) sb += red[g][H];
+      gz[bo + c] = sb;
+    }
+  }
+}
+
+void launch_head_wgrad_small(hipStream_t s, const Dims& d, const Work& w, const float* dpred, const float* hT,
+                             int64_t hz, float* grad, int64_t P, int64_t wo, int64_t bo) {
+  k_head_wgrad_small<<<dim3(d.HfC, w.Z), HWG * d.H, 0, s>>>(dpred, (int64_t)w.M * d.HfC, hT, hz, w.M, d.H, d.HfC,
+                                                           grad, P, wo, bo);
+}
+
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                       const ParamOff& po, const float* const* xtab, float dscale, bool want_loss) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
@@ -613,6 +814,12 @@ void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* 
   if (w.drop.lstm()) launch_drop_rows(s, w, d.H, top + (int64_t)(d.T - 1) * w.M * d.H, (int64_t)d.T * w.M * d.H, w.hTd);
   int64_t hz = 0;
   const float* hT = head_input(d, w, false, &hz);
+  if (head_small(d, w.M)) {
+    k_head_loss_small<<<dim3(w.M, 1, w.Z), head_small_threads(d), 0, s>>>(
+        hT, hz, theta, tstride, po.wo, po.bo, want_loss ? xtab : nullptr, w.pred, want_loss ? w.dpred : nullptr,
+        want_loss ? w.lpart : nullptr, w.lblocks, w.M, d.H, d.HfC, d.N, d.Hf, d.C, d.T + 1, d.Cin0, w.B, dscale);
+    return;
+  }
   dim3 grid((w.M + CfgNT::BM - 1) / CfgNT::BM, 1, w.Z);
   // targets from the feature stream: rows T+1 .. T+Hf after the window start, first C channels (F5)
   k_head_loss<<<grid, NT, 0, s>>>(hT, hz, theta, tstride, po.wo, po.bo,
@@ -624,6 +831,12 @@ void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* 
 void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float* hT, const float* theta,
                         const ParamOff& po, const float* const* ytab, float* pred, float* dpred, float dscale) {
   // explicit targets: ytab[s] -> y [Hf*N][C] in the reference's layout (dataset.py:40-48)
+  if (head_small(d, w.M)) {
+    k_head_loss_small<<<dim3(w.M, 1, 1), head_small_threads(d), 0, s>>>(
+        hT, 0, theta, 0, po.wo, po.bo, ytab, pred, ytab ? dpred : nullptr, ytab ? w.lpart : nullptr, w.lblocks, w.M,
+        d.H, d.HfC, d.N, d.Hf, d.C, 0, d.C, w.B, dscale);
+    return;
+  }
   dim3 grid((w.M + CfgNT::BM - 1) / CfgNT::BM, 1, 1);
   k_head_loss<<<grid, NT, 0, s>>>(hT, 0, theta, 0, po.wo, po.bo, ytab, pred, ytab ? dpred : nullptr,
                                   ytab ? w.lpart : nullptr, w.lblocks, w.M, d.H, d.HfC, d.N, d.Hf, d.C, 0, d.C,
@@ -898,7 +1111,7 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_part(con
                                                                             const float* __restrict__ theta,
                                                                             int64_t tstride, BwdWave wv, int L, int T,
                                                                             int M, int S, float* __restrict__ part) {
-  __shared__ float smem[CfgNN::SMEM_FLOATS];
+  __shared__ float smem[part_smem_floats<CfgNN, SMAML_BWD_PART_NCH>()];
   constexpr int G4 = 4 * H;
   const int p = wave_index(wv, (int)blockIdx.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
@@ -920,7 +1133,7 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_part(con
   if (kbeg < kend) {
     const SegKCt<2> la{{up ? pa : pn, pn}, {G4, G4}, M};
     const SegMCt<2> lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H};
-    gemm_mainloop<CfgNN>(la, lb, m0, n0, kbeg, kend, acc, smem);
+    part_mainloop<CfgNN, SMAML_BWD_PART_NCH>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
   // slab of (z, y = split * ntn + tn, x)
   constexpr int PER = CfgNN::WTM * CfgNN::WTN * 16 * CfgNN::NTH;
@@ -1066,15 +1279,15 @@ struct WgBDrop {
   }
 };
 
+// One weight-gradient workgroup: block L of a launch over ((ngroups + 7) / 8 * 8 * ntile) blocks.
 template <bool DROP>
-__global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
-                                              WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
-                                              int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
-                                              int ldp, int with_bias, Drop dr, int drop_layer) {
-  __shared__ float smem[CfgTN::SMEM_FLOATS];
+__device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
+                                            int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn, int ntile,
+                                            int nsplit, int ngroups, float* __restrict__ part, int ldp, int with_bias,
+                                            const Drop& dr, int drop_layer, float* smem) {
   // XCD-aware: the ntile output tiles of one (split, task) group stream the same K rows of
   // A and B, so they are placed on one XCD (blocks 8 apart) to share its L2. Speed only.
-  const int L = blockIdx.x, j = L >> 3;
+  const int j = L >> 3;
   const int g = (j / ntile) * 8 + (L & 7), tile = j - (j / ntile) * ntile;
   if (g >= ngroups) return;
   const int z = g / nsplit, split = g - z * nsplit;
@@ -1111,23 +1324,59 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < CfgTN::WTM; ++i)
 #pragma unroll
-    for (int j = 0; j < CfgTN::WTN; ++j) {
-      const int c = n0 + acc_col<CfgTN>(j);
+    for (int jj = 0; jj < CfgTN::WTN; ++jj) {
+      const int c = n0 + acc_col<CfgTN>(jj);
       if (c >= ncols) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + acc_row<CfgTN>(i, r);
-        if (row < Mrows) P[(int64_t)row * ldp + c] = acc.v[i][j][r];
+        if (row < Mrows) P[(int64_t)row * ldp + c] = acc.v[i][jj][r];
       }
     }
   if (tn == 0) hook.store(P, m0, Mrows, ldp, ncols, with_bias != 0);
 }
 
-__global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int Mrows, int ldp, int c1, int c2,
-                               float* __restrict__ grad, int64_t P, int64_t off_w1, int64_t off_w2,
-                               int64_t off_b1, int64_t off_b2, int accumulate) {
-  const int z = blockIdx.y;
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+template <bool DROP>
+__global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
+                                              WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
+                                              int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
+                                              int ldp, int with_bias, Drop dr, int drop_layer) {
+  __shared__ float smem[CfgTN::SMEM_FLOATS];
+  wgrad_block<DROP>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, nsplit,
+                    ngroups, part, ldp, with_bias, dr, drop_layer, smem);
+}
+
+// Several weight gradients in ONE launch (the LSTM layers of a small-grid backward: at batch 1 each
+// layer alone fills too little of the chip and its K loop is short). Problem q owns blocks
+// [blk[q], blk[q+1]) and partial slabs from part + poff[q].
+template <bool DROP>
+__global__ __launch_bounds__(CfgTN::NTH) void k_wgrad_multi(WgMulti mp, Drop dr) {
+  __shared__ float smem[CfgTN::SMEM_FLOATS];
+  int q = 0;
+  for (int i = 1; i < mp.n; ++i)
+    if ((int)blockIdx.x >= mp.blk[i]) q = i;
+  const WgradPlan& p = mp.p[q];
+  WgB lb;
+  lb.B1 = p.B1;
+  lb.B2 = p.B2;
+  lb.c1 = p.c1;
+  lb.c2 = p.c2;
+  lb.K = p.K;
+  lb.Mshift = p.Mshift;
+  if (DROP && p.drop_layer >= 0)
+    wgrad_block<true>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
+                      p.kchunk, p.ntn, p.ntm * p.ntn, p.nsplit, p.nsplit * p.Z, p.part, p.ldp, p.with_bias ? 1 : 0,
+                      dr, p.drop_layer, smem);
+  else
+    wgrad_block<false>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
+                       p.kchunk, p.ntn, p.ntm * p.ntn, p.nsplit, p.nsplit * p.Z, p.part, p.ldp, p.with_bias ? 1 : 0,
+                       dr, -1, smem);
+}
+
+__device__ __forceinline__ void wgrad_reduce_elem(const float* __restrict__ part, int nsplit, int Mrows, int ldp,
+                                                  int c1, int c2, float* __restrict__ grad, int64_t P, int64_t off_w1,
+                                                  int64_t off_w2, int64_t off_b1, int64_t off_b2, int accumulate,
+                                                  int z, int64_t e) {
   const int64_t total = (int64_t)Mrows * ldp;
   if (e >= total) return;
   const float* p = part + (int64_t)z * nsplit * total + e;
@@ -1147,6 +1396,24 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int M
     return;
   }
   *dst = accumulate ? *dst + v : v;
+}
+
+__global__ void k_wgrad_reduce(const float* __restrict__ part, int nsplit, int Mrows, int ldp, int c1, int c2,
+                               float* __restrict__ grad, int64_t P, int64_t off_w1, int64_t off_w2,
+                               int64_t off_b1, int64_t off_b2, int accumulate) {
+  wgrad_reduce_elem(part, nsplit, Mrows, ldp, c1, c2, grad, P, off_w1, off_w2, off_b1, off_b2, accumulate,
+                    (int)blockIdx.y, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// Problem q's reduce owns blocks [rblk[q], rblk[q+1]) of the x dimension.
+__global__ void k_wgrad_reduce_multi(WgMulti mp) {
+  int q = 0;
+  for (int i = 1; i < mp.n; ++i)
+    if ((int)blockIdx.x >= mp.rblk[i]) q = i;
+  const WgradPlan& p = mp.p[q];
+  wgrad_reduce_elem(p.part, p.nsplit, p.Mrows, p.ldp, p.c1, p.c2, p.grad, p.P, p.off_w1, p.off_w2, p.off_b1, p.off_b2,
+                    p.accumulate ? 1 : 0, (int)blockIdx.y,
+                    ((int64_t)blockIdx.x - mp.rblk[q]) * blockDim.x + threadIdx.x);
 }
 
 void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
@@ -1235,6 +1502,42 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
              off_b1, off_b2, with_bias, accumulate, p);
   launch_wgrad_gemm(s, p);
   launch_wgrad_reduce(s, p);
+}
+
+// All problems share Z; each gets nsplit = (target workgroups / all tiles) slices of its K range
+// (at least 8 K-tiles each), the partial slabs laid out one problem after another in w.wpart.
+void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs) {
+  int64_t tiles = 0;
+  for (int q = 0; q < n; ++q) tiles += (int64_t)ps[q].ntm * ps[q].ntn * ps[q].Z;
+  int64_t floats = 0;
+  for (int q = 0; q < n; ++q) floats += (int64_t)ps[q].Z * ps[q].Mrows * ps[q].ldp;
+  WgMulti mp{};
+  mp.n = n;
+  int blk = 0, rblk = 0;
+  int64_t off = 0;
+  for (int q = 0; q < n; ++q) {
+    WgradPlan& p = ps[q];
+    const int64_t ktiles = (p.K + CfgTN::BK - 1) / CfgTN::BK;
+    int64_t ns = std::max<int64_t>(1, target_wgs / std::max<int64_t>(1, tiles));
+    if (ns >= 8 && p.Z == 1) ns = ns / 8 * 8;  // whole octets of groups: no padding blocks past target_wgs
+    ns = std::min<int64_t>(ns, std::max<int64_t>(1, ktiles / 8));
+    ns = std::min<int64_t>(ns, std::max<int64_t>(1, w.wpart_floats / std::max<int64_t>(1, floats)));
+    p.kchunk = ((ktiles + ns - 1) / ns) * CfgTN::BK;
+    p.nsplit = (int)((p.K + p.kchunk - 1) / p.kchunk);
+    p.part = w.wpart + off;
+    off += (int64_t)p.nsplit * p.Z * p.Mrows * p.ldp;
+    mp.p[q] = p;
+    mp.blk[q] = blk;
+    blk += ((p.nsplit * p.Z + 7) / 8) * 8 * p.ntm * p.ntn;
+    mp.rblk[q] = rblk;
+    rblk += (int)(((int64_t)p.Mrows * p.ldp + 255) / 256);
+  }
+  const bool drop = w.drop.lstm();
+  if (drop)
+    k_wgrad_multi<true><<<blk, CfgTN::NTH, 0, s>>>(mp, w.drop);
+  else
+    k_wgrad_multi<false><<<blk, CfgTN::NTH, 0, s>>>(mp, w.drop);
+  k_wgrad_reduce_multi<<<dim3(rblk, ps[0].Z), 256, 0, s>>>(mp);
 }
 
 // ====================================================================================

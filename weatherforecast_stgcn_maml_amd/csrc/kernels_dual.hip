@@ -185,7 +185,7 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   const int ntm = (w.M + CfgGateD::BM - 1) / CfgGateD::BM;
   const int ngrp = (d.H + 32 * CfgGateD::WAVES_N - 1) / (32 * CfgGateD::WAVES_N);
   FwdWave wv{};
-  const double fl = fwd_wave(d, w, po, diag, (ntm + 7) / 8 * 8 * ngrp, true, wv);
+  const double fl = fwd_wave(d, w, po, diag, gate_blocks(ntm, ngrp), true, wv);
   if (flops) *flops = fl;
   if (wv.n == 0) return;
   dim3 grid(wv.off[wv.n], 1, w.Z);
@@ -655,6 +655,51 @@ __global__ void k_so_dir(const float* __restrict__ V, const float* __restrict__ 
 __global__ void k_axpy(float* __restrict__ V, const float* __restrict__ X, int64_t n, float alpha) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     V[i] = fmaf(alpha, X[i], V[i]);
+}
+
+// v += alpha * x, fused with the next inner step's dot partials g_next . v (same fixed partition
+// and order as k_dot): one pass over v instead of two launches.
+__global__ void k_axpy_dot(float* __restrict__ V, const float* __restrict__ X, float alpha,
+                           const float* __restrict__ Gn, int64_t P, double* __restrict__ part) {
+  __shared__ double red[NT / 64];
+  const int z = blockIdx.y;
+  float* vz = V + (int64_t)z * P;
+  const float* xz = X + (int64_t)z * P;
+  const float* gz = Gn + (int64_t)z * P;
+  const int64_t per = (P + SQB - 1) / SQB;
+  const int64_t beg = (int64_t)blockIdx.x * per, end = beg + per < P ? beg + per : P;
+  double acc = 0.0;
+  for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
+    const float v = fmaf(alpha, xz[i], vz[i]);
+    vz[i] = v;
+    acc += (double)gz[i] * (double)v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sum = 0.0;
+    for (int i = 0; i < NT / 64; ++i) sum += red[i];
+    part[(int64_t)z * SQB + blockIdx.x] = sum;
+  }
+}
+
+void launch_dot(hipStream_t s, const float* G, const float* V, int64_t P, int Z, double* part) {
+  k_dot<<<dim3(SQB, Z), NT, 0, s>>>(G, V, P, part);
+}
+
+void launch_axpy_dot(hipStream_t s, float* V, const float* X, float alpha, const float* Gn, int64_t P, int Z,
+                     double* part) {
+  k_axpy_dot<<<dim3(SQB, Z), NT, 0, s>>>(V, X, alpha, Gn, P, part);
+}
+
+// dot partials already in `part` (launch_dot / launch_axpy_dot)
+void launch_so_dir_only(hipStream_t s, const float* V, const float* G, int64_t P, int Z, const double* part,
+                        const float* norms, const float* coefs, float max_norm, float* U) {
+  int nb = (int)((P + NT - 1) / NT);
+  if (nb > 1024) nb = 1024;
+  k_so_dir<<<dim3(nb, Z), NT, 0, s>>>(V, G, P, part, norms, coefs, max_norm, U);
 }
 
 void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,

@@ -449,9 +449,17 @@ __device__ __forceinline__ void stb(float* base, uint32_t byteoff, float v) {
 
 // XCD-aware tile mapping for the gate GEMMs: the 4 unit-group workgroups of one row tile
 // are dispatched 8 apart (same XCD under round-robin placement: L2 sharing of the A rows)
-// and within 32 consecutive blocks. Grid: gridDim.x = ceil(ntm/8)*8 * ngrp (ngrp = 4H/128).
+// and within 32 consecutive blocks. Grid: gridDim.x = gate_blocks(ntm, ngrp) per problem
+// (ngrp = 4H/128). Below 8 row tiles (batch-1 steps) the padded layout would leave whole XCDs
+// idle (only blocks with blockIdx % 8 < ntm do work), so there the tiles are packed: tm fastest.
 // Speed-only: a different placement changes nothing but speed. Returns false for padding.
+__host__ __device__ inline int gate_blocks(int ntm, int ngrp) { return ntm < 8 ? ntm * ngrp : (ntm + 7) / 8 * 8 * ngrp; }
 __device__ __forceinline__ bool gate_tile(int L, int ntm, int ngrp, int& tm, int& ug) {
+  if (ntm < 8) {
+    ug = L / ntm;
+    tm = L - ug * ntm;
+    return ug < ngrp;
+  }
   const int per = 8 * ngrp;
   const int q = L / per, rem = L - q * per;
   ug = rem >> 3;
