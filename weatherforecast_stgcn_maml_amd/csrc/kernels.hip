@@ -281,12 +281,13 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
                                               int M, const Drop& dr, float* smem) {
   int l, t, b0;
   LayerOff lo;
-  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  const Blk bk = xcd_block();
+  wave_problem(wv, bk.x, l, t, lo, b0);
   const float* X = l == 0 ? F : HsAll + (int64_t)(l - 1) * lsz;
   float* Hs = HsAll + (int64_t)l * lsz;
   float* Cs = CsAll + (int64_t)l * lsz;
   float* Gs = GsAll + (int64_t)l * lsz * 4;
-  const int z = blockIdx.z;
+  const int z = bk.z;
   const float* th = theta + (int64_t)z * tstride;
   const int cin = lo.cin;
   const int64_t slab = (int64_t)z * T * M;
@@ -297,7 +298,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
   LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
   int tm, ug;
   constexpr int UPB = CfgGate::WAVES_N;  // 32-unit groups per workgroup
-  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+  if (!gate_tile(bk.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
     return;
   const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
@@ -426,7 +427,7 @@ __device__ __forceinline__ void part_mainloop(const LA& la, const LB& lb, int m0
 }
 
 template <int H>
-__global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
+__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
     const float* __restrict__ F, const float* __restrict__ HsAll, int64_t lsz, const float* __restrict__ theta,
     int64_t tstride, FwdWave wv, int T, int M, int S, float* __restrict__ part) {
   __shared__ float smem[part_smem_floats<CfgGate, SMAML_FWD_PART_NCH>()];
@@ -939,11 +940,14 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 // then) so that every lane then works on float4 groups of 4 consecutive hidden units of one row:
 // all epilogue memory traffic becomes 16-B loads / stores (4x fewer instructions than the
 // accumulator's column-per-lane layout, whole 128-B lines per 8 lanes) and one address serves 4
-// elements. The item loop is software-pipelined: item k+1's operands (gates, c_t, c_{t-1}, the dc
-// carry, dh_T) are loaded before item k is computed and stored, so loads stay in flight under the
-// math and the stores. Program order keeps the in-place dG over G safe: an item's elements are
+// elements. Each item's 7 loads (gates, c_t, c_{t-1}, the dc carry, dh_T) are in flight together;
+// SMAML_EPI_DEPTH 2 also loads item k+1 before item k is computed (more registers: slower as
+// measured). Program order keeps the in-place dG over G safe: an item's elements are
 // read before they are written and items never share elements. Uniform conditions (t = 0, the
 // first step) are selects on loads from valid addresses, so no branch splits the loads.
+#ifndef SMAML_DIAG_BWD
+#define SMAML_DIAG_BWD 0  // timing diagnostics only (wrong results): 1 = BPTT step without its epilogue,
+#endif                    // 2 = without its GEMM
 #ifndef SMAML_EPI_DEPTH
 #define SMAML_EPI_DEPTH 1  // epilogue items in flight per thread (1 or 2; A/B-able at build time)
 #endif
@@ -1062,12 +1066,13 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
                                                       BwdWave wv, int L, int T, int M, Drop dr) {
   __shared__ float smem[epi_smem_floats<CfgNN>()];
   constexpr int G4 = 4 * H;
-  const int p = wave_index(wv, (int)blockIdx.x);
+  const Blk bk = xcd_block();
+  const int p = wave_index(wv, bk.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
-  const int z = blockIdx.z;
-  const int m0 = ((int)blockIdx.x - b0) * CfgNN::BM, n0 = blockIdx.y * CfgNN::BN;
+  const int z = bk.z;
+  const int m0 = (bk.x - b0) * CfgNN::BM, n0 = bk.y * CfgNN::BN;
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in
@@ -1095,8 +1100,13 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
     } else {
       const SegKCt<2> la{{up ? pa : pn, pn}, {G4, G4}, M};
       const SegMCt<2> lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H};
-      if (ns) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
+      if (ns && SMAML_DIAG_BWD != 2) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
+  }
+  if (SMAML_DIAG_BWD == 1) {  // timing diagnostic: GEMM phase only (keep the result live)
+    acc_to_lds<CfgNN>(acc, smem);
+    if (t < 0) dGz[threadIdx.x] = smem[threadIdx.x];
+    return;
   }
   if (l == L - 1 && t == T - 1)  // the head's dh_T enters at the top layer's last step only
     bwd_cell<H, CfgNN, true>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
@@ -1107,7 +1117,7 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
 // Split-K BPTT step for small grids (see k_lstm_fwd_part): partial dh over a K-tile range of the
 // fused [above | next] GEMM, then k_lstm_bwd_cell sums the partials in order and runs bwd_cell.
 template <int H, class CfgNN>
-__global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_part(const float* dGAll, int64_t lsz,
+__global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_part(const float* dGAll, int64_t lsz,
                                                                             const float* __restrict__ theta,
                                                                             int64_t tstride, BwdWave wv, int L, int T,
                                                                             int M, int S, float* __restrict__ part) {

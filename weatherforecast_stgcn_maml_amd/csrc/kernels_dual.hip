@@ -53,7 +53,8 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   constexpr int G4 = 4 * H;
   int l, t, b0;
   LayerOff lo;
-  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  const Blk bk = xcd_block();
+  wave_problem(wv, bk.x, l, t, lo, b0);
   const float* X = l == 0 ? F : HsAll + (int64_t)(l - 1) * lsz;
   const float* RX = l == 0 ? nullptr : RHsAll + (int64_t)(l - 1) * lsz;
   float* Hs = HsAll + (int64_t)l * lsz;
@@ -62,7 +63,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   float* RHs = RHsAll + (int64_t)l * lsz;
   float* RCs = RCsAll + (int64_t)l * lsz;
   float* RGs = RGsAll + (int64_t)l * lsz * 4;
-  const int z = blockIdx.z;
+  const int z = bk.z;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
   const int cin = lo.cin;
@@ -80,8 +81,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   const int wh = hp ? H : 0;
   int tm, ug;
   constexpr int UPB = CfgGateD::WAVES_N;  // 32-unit groups per workgroup
-  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm,
-                 ug))
+  if (!gate_tile(bk.x - b0, (M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
     return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
   XDrop xd{};
@@ -326,6 +326,9 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
 }
 
 // ====================================================================================
+#ifndef SMAML_DIAG_BWDD
+#define SMAML_DIAG_BWDD 0  // timing diagnostics only (wrong results): 1 = kept tangent BPTT without its
+#endif                     // epilogue, 2 = without its GEMM
 using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
 using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_DUAL_BK>;
 
@@ -447,12 +450,13 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   __shared__ float smem[DualStage<CfgNND>::FLOATS];
   static_assert(DualStage<CfgNND>::FLOATS >= CfgNND::BM * CfgNND::BN, "epilogue transpose fits the staging LDS");
   constexpr int G4 = 4 * H;
-  const int p = wave_index(wv, (int)blockIdx.x);
+  const Blk bk = xcd_block();
+  const int p = wave_index(wv, bk.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
-  const int z = blockIdx.z;
-  const int m0 = ((int)blockIdx.x - b0) * CfgNND::BM, n0 = blockIdx.y * CfgNND::BN;
+  const int z = bk.z;
+  const int m0 = (bk.x - b0) * CfgNND::BM, n0 = bk.y * CfgNND::BN;
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
@@ -492,7 +496,7 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                           SegKC{{RGz + on, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
                                           SegMC{{th + lo.whh, nullptr}, {G4, 0}, H},
                                           SegMC{{u + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, G4, 0, ap, at, smem);
-    } else if (ns) {
+    } else if (ns && SMAML_DIAG_BWDD != 2) {
       const float* a0 = up ? dGAll + oa : dGz + on;
       const float* r0 = up ? RGsAll + oa : RGz + on;
       gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, dGz + on}, {G4, G4}, M}, SegKCt<2>{{r0, RGz + on}, {G4, G4}, M},
@@ -508,6 +512,10 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   const bool full = m0 + CfgNND::BM <= M;
   if constexpr (KEPT) {
     acc_to_lds<CfgNND>(at, smem);
+    if (SMAML_DIAG_BWDD == 1) {  // timing diagnostic: GEMM phase only (keep the result live)
+      if (t < 0) RGz[threadIdx.x] = smem[threadIdx.x];
+      return;
+    }
     const bool nochk = full && n0 + CfgNND::BN <= H;
 #define SMAML_KEPT_EPI(HD, CK)                                                                          \
   bwd_dual_kept_cell_<H, CfgNND, HD, CK>(smem, Gz, RGz, dhz, Cz, RCz, dHz, RdHz, dcz, rdcz, m0, n0, t, T, M)

@@ -471,6 +471,31 @@ __device__ __forceinline__ bool gate_tile(int ntm, int ngrp, int& tm, int& ug) {
   return gate_tile((int)blockIdx.x, ntm, ngrp, tm, ug);
 }
 
+#ifndef SMAML_XCD_REMAP
+#define SMAML_XCD_REMAP 0  // LSTM step kernels: XCD-contiguous workgroup order (0 = hardware order).
+#endif                     // Measured slower at config 2 (2494 -> 2557 ms per meta-step: BPTT +13,
+                           // tangent BPTT +35, forward +12 ms; profiles/r02_ab_xcd_remap.log).
+// Workgroup coordinates after an XCD-contiguous remap. The hardware places linear workgroup id L
+// on XCD L % 8 (round robin), so in hardware order every XCD runs tiles of every (task, layer)
+// problem and each XCD's 4 MB L2 must hold all of their weight operands (the BPTT's B is the
+// whole 1024 x 128 weight slice per tile: 0.5 MB, 1 MB with the tangent's): it thrashes and the
+// operand streams from HBM. Here logical ids are dealt so that XCD k runs one contiguous range of
+// the (z, y, x) order, x fastest: a few (task, layer) problems per XCD. Bijective for any count
+// (q = n / 8 ids on each XCD, one more on the first n % 8). Speed only.
+struct Blk {
+  int x, y, z;
+};
+__device__ __forceinline__ Blk xcd_block() {
+  if (!SMAML_XCD_REMAP) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int n = gx * gy * (int)gridDim.z;
+  const int L = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+  const int q = n >> 3, r = n & 7, xcd = L & 7;
+  const int lg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+  const int rest = lg / gx;
+  return {lg - rest * gx, rest % gy, rest / gy};
+}
+
 // Wavefront problems (kernels.h FwdWave / BwdWave): the problem owning block bx, and a field
 // of it, selected with scalar compares (no dynamic indexing into the by-value kernel argument).
 template <class WV>
