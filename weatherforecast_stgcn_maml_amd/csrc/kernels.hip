@@ -1181,6 +1181,76 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell(const float* GsAll
     bwd_cell<H, CfgNN, false>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
 }
 
+// The split-K BPTT step's cell kernel over 4x the threads (cf. k_lstm_fwd_cell_q): blockIdx.y =
+// tn * 4 + q, each thread sums its accumulator registers 4q..4q+3 over the S partials (same order
+// as k_lstm_bwd_cell) and runs the cell backward on those 4 rows of its column directly (no LDS
+// transpose): all loads of a thread in flight together. Same expressions as bwd_cell_.
+template <int H, class CfgNN>
+__global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell_q(const float* GsAll, float* dGAll,
+                                                               float* __restrict__ dhAll, const float* __restrict__ CsAll,
+                                                               const float* __restrict__ dHhead,
+                                                               float* __restrict__ dcAll, int64_t lsz, BwdWave wv, int L,
+                                                               int T, int M, int S, const float* __restrict__ part) {
+  static_assert(CfgNN::WTM == 1 && CfgNN::WTN == 1, "one 32 x 32 accumulator tile per wave");
+  constexpr int G4 = 4 * H;
+  constexpr int PER = 16 * CfgNN::NTH;
+  const int p = wave_index(wv, (int)blockIdx.x);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const int z = blockIdx.z, tn = blockIdx.y >> 2, q = blockIdx.y & 3;
+  const int ntn = gridDim.y >> 2;
+  const int m0 = ((int)blockIdx.x - b0) * CfgNN::BM, n0 = tn * CfgNN::BN;
+  const int tid = threadIdx.x;
+  float4 a = f4zero();
+  for (int sp = 0; sp < S; ++sp) {
+    const float4 v =
+        ld4(part + (((int64_t)z * (S * ntn) + sp * ntn + tn) * gridDim.x + blockIdx.x) * PER + 4 * (q * CfgNN::NTH + tid));
+    a = make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
+  }
+  const int64_t slab = (int64_t)z * T * M;
+  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dhz = dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr;
+  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
+  const float* dHz = dHhead + (int64_t)z * M * H;
+  const bool first = (t == T - 1), past = t > 0, head = first && l == L - 1;
+  const int j = n0 + acc_col<CfgNN>(0);
+  const int rb = m0 + acc_row<CfgNN>(0, 0) + 8 * q;  // row of register 4q
+  const int jc = min(j, H - 1);
+  float g[4][4], c[4], cp[4], dc[4], hd[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // all loads first (clamped rows: valid addresses)
+    const int m = min(rb + e, M - 1);
+    const int64_t row = (int64_t)t * M + m;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[e][k] = Gz[row * G4 + k * H + jc];
+    c[e] = Cz[row * H + jc];
+    cp[e] = past ? Cz[row * H - (int64_t)M * H + jc] : 0.f;
+    dc[e] = first ? 0.f : dcz[(int64_t)m * H + jc];
+    hd[e] = head ? dHz[(int64_t)m * H + jc] : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int m = rb + e;
+    if (m >= M || j >= H) continue;
+    const float d = f4get(a, e) + hd[e];
+    const float gi = g[e][0], gf = g[e][1], gg = g[e][2], go = g[e][3];
+    const float tc = tanhf_(c[e]);
+    const float dct = dc[e] + d * go * (1.f - tc * tc);
+    const int64_t row = (int64_t)t * M + m;
+    float* gp = dGz + row * G4 + j;
+    gp[0] = dct * gg * gi * (1.f - gi);
+    gp[H] = dct * cp[e] * gf * (1.f - gf);
+    gp[2 * H] = dct * gi * (1.f - gg * gg);
+    gp[3 * H] = d * tc * go * (1.f - go);
+    dcz[(int64_t)m * H + j] = dct * gf;
+    if (dhz) dhz[row * H + j] = d;
+  }
+}
+#ifndef SMAML_BWD_CELL_Q
+#define SMAML_BWD_CELL_Q 1  // split-K BPTT step's cell kernel over 4x the threads (0: k_lstm_bwd_cell)
+#endif
+
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
                           const ParamOff& po) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
@@ -1212,8 +1282,14 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
         dim3 gp(grid.x, S * ntns, w.Z);
         SMAML_DISPATCH_H(d.H, (k_lstm_bwd_part<HT, CfgNNs><<<gp, CfgNNs::NTH, 0, s>>>(w.dG, lsz, theta, tstride, wv,
                                                                                        d.L, d.T, w.M, S, w.wpart)));
-        SMAML_DISPATCH_H(d.H, (k_lstm_bwd_cell<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
-                                  w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, wv, d.L, d.T, w.M, S, w.wpart)));
+        if (SMAML_BWD_CELL_Q) {
+          dim3 gq(grid.x, 4 * ntns, w.Z);
+          SMAML_DISPATCH_H(d.H, (k_lstm_bwd_cell_q<HT, CfgNNs><<<gq, CfgNNs::NTH, 0, s>>>(
+                                    w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, wv, d.L, d.T, w.M, S, w.wpart)));
+        } else {
+          SMAML_DISPATCH_H(d.H, (k_lstm_bwd_cell<HT, CfgNNs><<<grid, CfgNNs::NTH, 0, s>>>(
+                                    w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, wv, d.L, d.T, w.M, S, w.wpart)));
+        }
         return;
       }
     }
