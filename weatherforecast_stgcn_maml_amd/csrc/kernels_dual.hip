@@ -41,6 +41,68 @@ __device__ __forceinline__ float block_sum_f(float v, float* red) {
 // KEPT: the primal of this step (gates, c, h) is already in Hs / Cs / Gs (kept from the inner
 // step for the second-order sweep): only the tangent pass runs.
 // DROP: layers >= 1 read x = drop(h_{l-1}) and R x = drop(R h_{l-1}) (the same mask).
+// Tangent cell epilogue of one gate tile: R(gates), R(c), R(h) from the tangent accumulators and
+// the primal gates / cell this lane has (just) written or kept. Rows are handled SMAML_FWDD_EPI_RB
+// at a time with all their loads issued before their stores (a row at a time serialised one
+// memory round trip per row: 16 per tile); the t = 0 case loads a valid address and selects 0, and
+// the row bound is checked only in the last row tile (CHECK), so the batch's loads never branch.
+#ifndef SMAML_FWDD_EPI_RB
+#define SMAML_FWDD_EPI_RB 4
+#endif
+template <int H, bool CHECK>
+__device__ __forceinline__ void fwd_dual_tangent_epi(const Acc<CfgGateD>& at, const float (&bu)[4],
+                                                     const float* __restrict__ Gz, float* __restrict__ RGz,
+                                                     const float* __restrict__ Cz, float* __restrict__ RCz,
+                                                     float* __restrict__ RHz, int rb, int j, uint32_t tM, int M,
+                                                     int t) {
+  constexpr int G4 = 4 * H;
+  constexpr int RB = SMAML_FWDD_EPI_RB;
+  static_assert(16 % RB == 0, "row batch");
+  const bool past = t > 0;
+  const uint32_t pM = past ? (uint32_t)M * H : 0u;
+#pragma unroll
+  for (int r0 = 0; r0 < 16; r0 += RB) {
+    float gi[RB], gf[RB], gg[RB], go[RB], c[RB], cp[RB], rcp[RB];
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      int m = rb + racc(r0 + q);
+      if (CHECK) m = min(m, M - 1);
+      const uint32_t row = tM + (uint32_t)m;
+      const uint32_t oh = row * H + j;
+      const uint32_t og = row * G4 + j;
+      gi[q] = ldb(Gz, 4u * (og));
+      gf[q] = ldb(Gz, 4u * (og + H));
+      gg[q] = ldb(Gz, 4u * (og + 2 * H));
+      go[q] = ldb(Gz, 4u * (og + 3 * H));
+      c[q] = ldb(Cz, 4u * (oh));
+      cp[q] = ldb(Cz, 4u * (oh - pM));
+      rcp[q] = ldb(RCz, 4u * (oh - pM));
+    }
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      const int r = r0 + q;
+      const int m = rb + racc(r);
+      if (CHECK && m >= M) continue;
+      const uint32_t row = tM + (uint32_t)m;
+      const uint32_t oh = row * H + j;
+      const uint32_t og = row * G4 + j;
+      const float ri = gi[q] * (1.f - gi[q]) * (at.v[0][0][r] + bu[0]);
+      const float rf = gf[q] * (1.f - gf[q]) * (at.v[0][1][r] + bu[1]);
+      const float rg = (1.f - gg[q] * gg[q]) * (at.v[0][2][r] + bu[2]);
+      const float ro = go[q] * (1.f - go[q]) * (at.v[0][3][r] + bu[3]);
+      const float cpv = past ? cp[q] : 0.f, rcpv = past ? rcp[q] : 0.f;
+      const float rc = rf * cpv + gf[q] * rcpv + ri * gg[q] + gi[q] * rg;
+      const float tc = tanhf_(c[q]);
+      stb(RGz, 4u * (og), ri);
+      stb(RGz, 4u * (og + H), rf);
+      stb(RGz, 4u * (og + 2 * H), rg);
+      stb(RGz, 4u * (og + 3 * H), ro);
+      stb(RCz, 4u * (oh), rc);
+      stb(RHz, 4u * (oh), ro * tc + go[q] * (1.f - tc * tc) * rc);
+    }
+  }
+}
+
 template <int H, bool KEPT, bool DROP>
 __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
                                                       float* __restrict__ HsAll, float* __restrict__ CsAll,
@@ -152,31 +214,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   float bu[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bu[g] = u[lo.bih + g * H + j] + u[lo.bhh + g * H + j];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = rb + racc(r);
-    if (!full && m >= M) continue;
-    const uint32_t row = tM + (uint32_t)m;
-    const uint32_t oh = row * H + j;
-    const uint32_t og = row * G4 + j;
-    const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H));
-    const float gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
-    const float c = ldb(Cz, 4u * (oh));
-    const float ri = gi * (1.f - gi) * (at.v[0][0][r] + bu[0]);
-    const float rf = gf * (1.f - gf) * (at.v[0][1][r] + bu[1]);
-    const float rg = (1.f - gg * gg) * (at.v[0][2][r] + bu[2]);
-    const float ro = go * (1.f - go) * (at.v[0][3][r] + bu[3]);
-    const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-    const float rcp = t > 0 ? ldb(RCz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-    const float rc = rf * cp + gf * rcp + ri * gg + gi * rg;
-    const float tc = tanhf_(c);
-    stb(RGz, 4u * (og), ri);
-    stb(RGz, 4u * (og + H), rf);
-    stb(RGz, 4u * (og + 2 * H), rg);
-    stb(RGz, 4u * (og + 3 * H), ro);
-    stb(RCz, 4u * (oh), rc);
-    stb(RHz, 4u * (oh), ro * tc + go * (1.f - tc * tc) * rc);
-  }
+  if (full)
+    fwd_dual_tangent_epi<H, false>(at, bu, Gz, RGz, Cz, RCz, RHz, rb, j, tM, M, t);
+  else
+    fwd_dual_tangent_epi<H, true>(at, bu, Gz, RGz, Cz, RCz, RHz, rb, j, tM, M, t);
 }
 
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
