@@ -1,0 +1,171 @@
+// Microbenchmark: the BPTT GEMM shape (M = 221 x 64 rows x 15 tasks, N = H = 128, K = 8H = 1024)
+// on the fp32 MFMA core with the B operand (the weights) k-major ("MC", read with 4 ds_read_b32 per
+// fragment: the kernels' current layout) vs row-major k-contiguous ("KC", one ds_read_b128 per
+// fragment; padded LDS rows). GEMM only, result stored once. Prints TFLOP/s (HIP events).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include "kernels.h"
+#include "loaders.h"
+using namespace smaml;
+
+// Variant core: all LDS fragments of the K-tile first, then the K-tile's MFMAs (one wait).
+template <class C>
+__device__ __forceinline__ void mma_tile_all(const float* as, const float* bs, Acc<C>& acc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+  const int arow = wm * (C::WTM * 32) + (lane & 31);
+  const int brow = wn * (C::WTN * 32) + (lane & 31);
+  const int h = lane >> 5;
+  constexpr int Q = C::BK / 8;
+  float4 a[Q][C::WTM], b[Q][C::WTN];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) a[q][i] = frag4<C::A_KC, C::LDA, C::BK>(as, arow + 32 * i, h, q);
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) b[q][j] = frag4<C::B_KC, C::LDB, C::BK>(bs, brow + 32 * j, h, q);
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::WTN; ++j)
+          acc.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[q][i], e), f4get(b[q][j], e), acc.v[i][j], 0, 0, 0);
+}
+template <class C, class LA, class LB>
+__device__ __forceinline__ void mainloop_all(const LA& la, const LB& lb, int m0, int n0, int K, Acc<C>& acc, float* smem) {
+  float* As = smem;
+  float* Bs = smem + 2 * C::A_STAGE;
+  const int nkt = K / C::BK;
+  float4 ra[C::A_F4], rb[C::B_F4];
+  fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, C::BK>(la, m0, 0, ra);
+  fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, 0, rb);
+  store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, C::BK>(As, ra);
+  store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, C::BK>(Bs, rb);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, C::BK>(la, m0, (kt + 1) * C::BK, ra);
+      fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, (kt + 1) * C::BK, rb);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    mma_tile_all<C>(As + cur * C::A_STAGE, Bs + cur * C::B_STAGE, acc);
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+      store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, C::BK>(As + (cur ^ 1) * C::A_STAGE, ra);
+      store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, C::BK>(Bs + (cur ^ 1) * C::B_STAGE, rb);
+    }
+    __syncthreads();
+  }
+}
+template <class C>
+__global__ __launch_bounds__(C::NTH) void k_all(const float* A, const float* B, float* O, int M, int N, int K) {
+  __shared__ float smem[C::SMEM_FLOATS];
+  const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
+  Acc<C> acc;
+  acc.zero();
+  RowMajorKC la{A, M, K};
+  RowMajorMC lb{B, K, N};
+  mainloop_all<C>(la, lb, m0, n0, K, acc, smem);
+  const int c = n0 + acc_col<C>(0);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += acc.v[i][j][r];
+  O[(int64_t)blockIdx.x * C::NTH + threadIdx.x] = s + c;
+}
+template <class C>
+void run_all(const char* name, const float* A, const float* B, float* O, int M, int N, int K) {
+  dim3 grid(M / C::BM, N / C::BN);
+  for (int i = 0; i < 3; ++i) k_all<C><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) k_all<C><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  const double tf = 2.0 * M * N * K * reps / (ms * 1e-3) / 1e12;
+  printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
+}
+
+template <class C, bool MC>
+__global__ __launch_bounds__(C::NTH) void k_b(const float* A, const float* B, float* O, int M, int N, int K) {
+  __shared__ float smem[C::SMEM_FLOATS];
+  const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
+  Acc<C> acc;
+  acc.zero();
+  RowMajorKC la{A, M, K};
+  if constexpr (MC) {
+    RowMajorMC lb{B, K, N};
+    gemm_mainloop<C>(la, lb, m0, n0, 0, K, acc, smem);
+  } else {
+    RowMajorKC lb{B, N, K};
+    gemm_mainloop<C>(la, lb, m0, n0, 0, K, acc, smem);
+  }
+  const int c = n0 + acc_col<C>(0);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += acc.v[i][j][r];
+  O[(int64_t)blockIdx.x * C::NTH + threadIdx.x] = s + c;
+}
+
+template <class C, bool MC>
+void run(const char* name, const float* A, const float* B, float* O, int M, int N, int K) {
+  dim3 grid(M / C::BM, N / C::BN);
+  for (int i = 0; i < 3; ++i) k_b<C, MC><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) k_b<C, MC><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  const double tf = 2.0 * M * N * K * reps / (ms * 1e-3) / 1e12;
+  printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
+}
+
+int main() {
+  const int M = 64 * 221 * 15, N = 128, K = 1024;
+  const int Mmax = 64 * 128 * 40;  // the largest row count run below (4 rounds)
+  float *A, *B, *O;
+  hipMalloc(&A, (size_t)Mmax * K * 4);
+  hipMalloc(&B, (size_t)N * K * 4);
+  hipMalloc(&O, (size_t)Mmax * 256 * 4);
+  std::vector<float> h((size_t)Mmax * K);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+  hipMemcpy(A, h.data(), (size_t)Mmax * K * 4, hipMemcpyHostToDevice);
+  hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice);
+  for (int rep = 0; rep < 2; ++rep) {
+    run<GemmCfg<64, 128, 2, 2, true, false, 16>, true>("64x128 w2x2 BK16  B MC (current)", A, B, O, M, N, K);
+    run_all<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  MC frags-first", A, B, O, M, N, K);
+    run<GemmCfg<128, 128, 4, 2, true, false, 16>, true>("128x128 w4x2 BK16 B MC", A, B, O, M, N, K);
+  }
+  // workgroup-round quantization: 5 resident 64x128 workgroups per CU -> 1280 per round
+  for (int rounds10 : {10, 20, 25, 26, 30, 35, 40}) {
+    const int Mr = 64 * 128 * rounds10;  // rounds10 / 10 rounds of 1280 workgroups
+    char name[64];
+    snprintf(name, sizeof name, "64x128 current, %.1f rounds", rounds10 / 10.0);
+    run<GemmCfg<64, 128, 2, 2, true, false, 16>, true>(name, A, B, O, Mr, N, K);
+  }
+  return 0;
+}
