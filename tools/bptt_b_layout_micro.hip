@@ -160,6 +160,12 @@ int main() {
     run_all<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  MC frags-first", A, B, O, M, N, K);
     run<GemmCfg<128, 128, 4, 2, true, false, 16>, true>("128x128 w4x2 BK16 B MC", A, B, O, M, N, K);
   }
+  for (int rep = 0; rep < 2; ++rep) {  // larger wave tiles (64 x 128 per wave = 8 MFMA blocks, as k_wgrad)
+    run<GemmCfg<256, 128, 4, 1, true, false, 16>, true>("256x128 w4x1 BK16 B MC", A, B, O, M, N, K);
+    run<GemmCfg<512, 128, 8, 1, true, false, 16>, true>("512x128 w8x1 BK16 B MC", A, B, O, M, N, K);
+    run<GemmCfg<256, 128, 4, 1, true, true, 16>, false>("256x128 w4x1 BK16 B KC", A, B, O, M, N, K);
+    run<GemmCfg<128, 128, 2, 1, true, false, 16>, true>("128x128 w2x1 BK16 B MC", A, B, O, M, N, K);
+  }
   // workgroup-round quantization: 5 resident 64x128 workgroups per CU -> 1280 per round
   for (int rounds10 : {10, 20, 25, 26, 30, 35, 40}) {
     const int Mr = 64 * 128 * rounds10;  // rounds10 / 10 rounds of 1280 workgroups
