@@ -514,6 +514,31 @@ def test_second_order_bench_tiles_b32(keep):
     _check_meta_step(res, ml, ref, d, names, 1, cfg.inner_steps)
 
 
+def test_second_order_bench_tiles_b32_dropout():
+    """The bench-size tiles with train-mode dropout (0.2 / 0.2: the masked loaders and the
+    dropout variants of the 64x128 BPTT and tangent BPTT kernels) against the oracle's restated
+    masks: 1 task x B=32 x K=1, second order."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=1, batch=32, order=2)
+    P = synth.init_params(15, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(1750, d.num_nodes, stream_len_for(cfg, d))]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=None, dropout=(0.2, 0.2), dropout_seed=9)
+    ml.set_tasks(feats, task_ids=[4])
+    ml.ctx.variant_counts(reset=True)
+    res = ml.meta_step()
+    vc = ml.ctx.variant_counts()
+    assert vc["fwd_drop"] > 0 and vc["bwd_big"] > 0 and vc["bwd_dual_big"] + vc["bwd_dual_big_kept"] > 0, vc
+    seed = (9 * 1000003 + 1) & 0xFFFFFFFF  # MetaLearner's seed of its first meta-step
+    PT = refcpu.to_torch(P)
+    ref = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
+                           [refcpu.TaskData(f, ei, d) for f in feats], list(ml.default_windows()[-1, 0]),
+                           cfg.inner_steps, cfg.batch, cfg.inner_steps * cfg.batch, cfg.inner_lr, cfg.max_norm,
+                           cfg.order, dropout=(seed, 0.2, 0.2), task_ids=[4])
+    _check_meta_step(res, ml, ref, d, names, 1, cfg.inner_steps)
+
+
 @pytest.mark.parametrize("tiles", ["big", "small", "split"])
 @pytest.mark.parametrize("keep", [-1, 0])
 def test_second_order_tile_variants_task_groups(tiles, keep):
