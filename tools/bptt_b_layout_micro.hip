@@ -64,6 +64,126 @@ __device__ __forceinline__ void mainloop_all(const LA& la, const LB& lb, int m0,
     __syncthreads();
   }
 }
+// Variant core: 3-stage LDS ring. Tile k+1 is in LDS one barrier before tile k's MFMAs start, so
+// its fragments are read into a second register set under tile k's MFMAs; the global loads of
+// tile k+3 are in flight under them as well. One barrier per K-tile.
+template <class C>
+struct Frags {
+  float4 a[C::BK / 8][C::WTM], b[C::BK / 8][C::WTN];
+};
+template <class C>
+__device__ __forceinline__ void read_frags(const float* as, const float* bs, Frags<C>& f) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+  const int arow = wm * (C::WTM * 32) + (lane & 31);
+  const int brow = wn * (C::WTN * 32) + (lane & 31);
+  const int h = lane >> 5;
+#pragma unroll
+  for (int q = 0; q < C::BK / 8; ++q) {
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) f.a[q][i] = frag4<C::A_KC, C::LDA, C::BK>(as, arow + 32 * i, h, q);
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) f.b[q][j] = frag4<C::B_KC, C::LDB, C::BK>(bs, brow + 32 * j, h, q);
+  }
+}
+template <class C>
+__device__ __forceinline__ void mma_frags(const Frags<C>& f, Acc<C>& acc) {
+#pragma unroll
+  for (int q = 0; q < C::BK / 8; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::WTN; ++j)
+          acc.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(f.a[q][i], e), f4get(f.b[q][j], e), acc.v[i][j], 0, 0, 0);
+}
+template <class C, class LA, class LB>
+__device__ __forceinline__ void mainloop_ring3(const LA& la, const LB& lb, int m0, int n0, int K, Acc<C>& acc,
+                                               float* smem) {
+  float* As = smem;
+  float* Bs = smem + 3 * C::A_STAGE;
+  const int nkt = K / C::BK;
+  float4 ra[C::A_F4], rb[C::B_F4];
+  auto fetch = [&](int kt) {
+    fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, C::BK>(la, m0, kt * C::BK, ra);
+    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, kt * C::BK, rb);
+  };
+  auto store = [&](int st) {
+    store_tile<C::BM, C::LDA, C::A_F4, C::NTH, C::A_KC, C::BK>(As + st * C::A_STAGE, ra);
+    store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, C::BK>(Bs + st * C::B_STAGE, rb);
+  };
+  fetch(0);
+  store(0);
+  if (nkt > 1) {
+    fetch(1);
+    store(1);
+  }
+  __syncthreads();
+  Frags<C> f0, f1;
+  read_frags<C>(As, Bs, f0);
+  if (nkt > 2) fetch(2);
+  for (int kt = 0; kt < nkt; kt += 2) {
+    // even step: MFMAs on f0 (tile kt), fragments of tile kt+1 into f1
+    if (kt + 1 < nkt) read_frags<C>(As + ((kt + 1) % 3) * C::A_STAGE, Bs + ((kt + 1) % 3) * C::B_STAGE, f1);
+    __builtin_amdgcn_s_setprio(1);
+    mma_frags<C>(f0, acc);
+    __builtin_amdgcn_s_setprio(0);
+    if (kt + 2 < nkt) {
+      store((kt + 2) % 3);
+      if (kt + 3 < nkt) fetch(kt + 3);
+    }
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    // odd step: MFMAs on f1 (tile kt+1), fragments of tile kt+2 into f0
+    if (kt + 2 < nkt) read_frags<C>(As + ((kt + 2) % 3) * C::A_STAGE, Bs + ((kt + 2) % 3) * C::B_STAGE, f0);
+    __builtin_amdgcn_s_setprio(1);
+    mma_frags<C>(f1, acc);
+    __builtin_amdgcn_s_setprio(0);
+    if (kt + 3 < nkt) {
+      store((kt + 3) % 3);
+      if (kt + 4 < nkt) fetch(kt + 4);
+    }
+    __syncthreads();
+  }
+}
+template <class C>
+__global__ __launch_bounds__(C::NTH) void k_ring(const float* A, const float* B, float* O, int M, int N, int K) {
+  __shared__ float smem[3 * (C::A_STAGE + C::B_STAGE)];
+  const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
+  Acc<C> acc;
+  acc.zero();
+  RowMajorKC la{A, M, K};
+  RowMajorMC lb{B, K, N};
+  mainloop_ring3<C>(la, lb, m0, n0, K, acc, smem);
+  const int c = n0 + acc_col<C>(0);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += acc.v[i][j][r];
+  O[(int64_t)blockIdx.x * C::NTH + threadIdx.x] = s + c;
+}
+template <class C>
+void run_ring(const char* name, const float* A, const float* B, float* O, int M, int N, int K) {
+  dim3 grid(M / C::BM, N / C::BN);
+  for (int i = 0; i < 3; ++i) k_ring<C><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) k_ring<C><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  const double tf = 2.0 * M * N * K * reps / (ms * 1e-3) / 1e12;
+  printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
+}
+
 template <class C>
 __global__ __launch_bounds__(C::NTH) void k_all(const float* A, const float* B, float* O, int M, int N, int K) {
   __shared__ float smem[C::SMEM_FLOATS];
@@ -155,6 +275,12 @@ int main() {
   for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
   hipMemcpy(A, h.data(), (size_t)Mmax * K * 4, hipMemcpyHostToDevice);
   hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice);
+  for (int rep = 0; rep < 3; ++rep) {
+    run_ring<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  ring3", A, B, O, M, N, K);
+    run_ring<GemmCfg<64, 128, 2, 2, true, false, 32>>("64x128 w2x2 BK32  ring3", A, B, O, M, N, K);
+    run_ring<GemmCfg<128, 128, 4, 1, true, false, 16>>("128x128 w4x1 BK16 ring3", A, B, O, M, N, K);
+    run<GemmCfg<64, 128, 2, 2, true, false, 16>, true>("64x128 w2x2 BK16  B MC (current)", A, B, O, M, N, K);
+  }
   for (int rep = 0; rep < 2; ++rep) {
     run<GemmCfg<64, 128, 2, 2, true, false, 16>, true>("64x128 w2x2 BK16  B MC (current)", A, B, O, M, N, K);
     run_all<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  MC frags-first", A, B, O, M, N, K);
