@@ -1365,6 +1365,97 @@ struct WgBDrop {
   }
 };
 
+// ---- weight-gradient mainloop with direct-to-LDS loads -----------------------------------
+// k_wgrad runs ONE 8-wave workgroup per CU (207 VGPRs, 512 x 128 tile), where register staging
+// leaves the MFMA pipe waiting on each K-tile's loads. Here every operand tile goes global -> LDS
+// with global_load_lds_dwordx4 (no staging VGPRs, no ds_write), into a 3-stage ring, and the wait
+// before each raw barrier is counted (vmcnt(5): the next tile's 5 loads per wave stay in flight
+// across it). Operands outside the matrix (rows >= K, the shifted h_{t-1} rows before Mshift)
+// load from a zero line. A glds wave-instruction writes 1 KB contiguously in lane order: A rows
+// (512 floats = 2 KB) keep their padded LDS stride (two instructions per row), B rows (128
+// floats) are unpadded (one instruction = 2 rows). Same products in the same order as the
+// register-staged loop: bitwise-identical partial sums (tools/wgrad_glds_micro.hip).
+#ifndef SMAML_WGRAD_GLDS
+#define SMAML_WGRAD_GLDS 1
+#endif
+#ifndef SMAML_WGRAD_GLDS_IGLP
+#define SMAML_WGRAD_GLDS_IGLP -1
+#endif
+__device__ float g_zero_line[256];  // zero-initialised module global: the source of zero rows
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+__device__ __forceinline__ void glds16(const float* g, float* l) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)l, 16, 0, 0);
+}
+struct CfgTNg : CfgTN {  // unpadded B rows
+  static constexpr int LDB = CfgTN::BN;
+  static constexpr int B_STAGE = CfgTN::BK * CfgTN::BN;
+};
+constexpr int WG_GLDS_SMEM = 3 * (CfgTNg::A_STAGE + CfgTNg::B_STAGE);
+constexpr bool kWgradGldsShape = CfgTN::BM == 512 && CfgTN::BN == 128 && CfgTN::BK == 16 && CfgTN::NTH == 512 &&
+                                 !CfgTN::A_KC && !CfgTN::B_KC;
+constexpr int WG_SMEM = (SMAML_WGRAD_GLDS && kWgradGldsShape && WG_GLDS_SMEM > CfgTN::SMEM_FLOATS) ? WG_GLDS_SMEM
+                                                                                                    : CfgTN::SMEM_FLOATS;
+
+// K-tile at row k0 into one stage: per wave 4 A half-rows + 1 B instruction (2 rows).
+__device__ __forceinline__ void wg_issue(const float* A, int64_t K, const WgB& b, int n0, int64_t k0, float* As,
+                                         float* Bs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int row = 2 * w + r;
+    const int64_t k = k0 + row;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const float* src = k < K ? A + k * CfgTN::BM + half * 256 + 4 * lane : g_zero_line + 4 * (lane & 31);
+      glds16(src, As + row * CfgTN::LDA + half * 256);
+    }
+  }
+  const int row = 2 * w + (lane >> 5), col = 4 * (lane & 31);
+  const int64_t k = k0 + row;
+  const float* src;
+  if (n0 < b.c1) {
+    src = k < K ? b.B1 + k * b.c1 + n0 + col : g_zero_line + col;
+  } else {
+    const int64_t k2 = k - b.Mshift;
+    src = (k < K && k2 >= 0) ? b.B2 + k2 * b.c2 + (n0 - b.c1) + col : g_zero_line + col;
+  }
+  glds16(src, Bs + 2 * w * CfgTN::BN);
+}
+
+template <class Hook>
+__device__ __forceinline__ void wgrad_glds_loop(const float* A, int64_t K, const WgB& b, int n0, int64_t kbeg,
+                                                int64_t kend, Acc<CfgTN>& acc, float* smem, Hook& hook) {
+  float* As = smem;
+  float* Bs = smem + 3 * CfgTNg::A_STAGE;
+  const int nkt = (int)((kend - kbeg + CfgTN::BK - 1) / CfgTN::BK);
+  if (nkt <= 0) return;
+  wg_issue(A, K, b, n0, kbeg, As, Bs);
+  if (nkt > 1) wg_issue(A, K, b, n0, kbeg + CfgTN::BK, As + CfgTNg::A_STAGE, Bs + CfgTNg::B_STAGE);
+  Acc<CfgTNg>& accg = reinterpret_cast<Acc<CfgTNg>&>(acc);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // this tile landed; the next one may not have
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");  // every wave's share landed; stage (kt+2)%3 is free
+    const int st = kt % 3;
+    if (kt + 2 < nkt) {
+      const int s2 = (kt + 2) % 3;
+      wg_issue(A, K, b, n0, kbeg + (int64_t)(kt + 2) * CfgTN::BK, As + s2 * CfgTNg::A_STAGE,
+               Bs + s2 * CfgTNg::B_STAGE);
+    }
+    hook(As + st * CfgTNg::A_STAGE, kt);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+    mma_tile<CfgTNg, SMAML_WGRAD_GLDS_IGLP>(As + st * CfgTNg::A_STAGE, Bs + st * CfgTNg::B_STAGE, accg, hook);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  }
+}
+
 // One weight-gradient workgroup: block L of a launch over ((ngroups + 7) / 8 * 8 * ntile) blocks.
 template <bool DROP>
 __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
@@ -1398,6 +1489,15 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
     } else {
       gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
+  } else if (SMAML_WGRAD_GLDS && kWgradGldsShape && Mrows == CfgTN::BM && lb.c1 % CfgTN::BN == 0 &&
+             lb.c2 % CfgTN::BN == 0) {
+    const float* Az = A + (int64_t)z * a_zstride;
+    if (tn == 0 && with_bias) {
+      wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, hook);
+    } else {
+      NoHook nh;
+      wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, nh);
+    }
   } else if (tn == 0 && with_bias) {
     // (the branch-free MCKt / WgBt tile loaders measured slower here: wgrad 723 -> 820 ms per
     // meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log)
@@ -1427,7 +1527,7 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
                                               int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
                                               int ldp, int with_bias, Drop dr, int drop_layer) {
-  __shared__ float smem[CfgTN::SMEM_FLOATS];
+  __shared__ float smem[WG_SMEM];
   wgrad_block<DROP>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, nsplit,
                     ngroups, part, ldp, with_bias, dr, drop_layer, smem);
 }
@@ -1437,7 +1537,7 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ 
 // [blk[q], blk[q+1]) and partial slabs from part + poff[q].
 template <bool DROP>
 __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad_multi(WgMulti mp, Drop dr) {
-  __shared__ float smem[CfgTN::SMEM_FLOATS];
+  __shared__ float smem[WG_SMEM];
   int q = 0;
   for (int i = 1; i < mp.n; ++i)
     if ((int)blockIdx.x >= mp.blk[i]) q = i;
