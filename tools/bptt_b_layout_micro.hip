@@ -184,6 +184,112 @@ void run_ring(const char* name, const float* A, const float* B, float* O, int M,
   printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
 }
 
+// Variant core: direct-to-LDS loads (global_load_lds_dwordx4) into a 3-stage ring with a counted
+// vmcnt across raw barriers, for the 64 x 128 BPTT tile (4 waves). A (k-contiguous rows of 16
+// floats) is stored unpadded with the 16-B chunks XOR-swizzled by (row >> 1) & 3 through the
+// SOURCE address (a glds wave-instruction writes lane-linear LDS); B rows (128 floats) unpadded.
+typedef __attribute__((address_space(3))) void lds_void_m;
+typedef __attribute__((address_space(1))) const void gbl_void_m;
+__device__ __forceinline__ void glds16m(const float* g, float* l) {
+  __builtin_amdgcn_global_load_lds((gbl_void_m*)g, (lds_void_m*)l, 16, 0, 0);
+}
+__device__ __forceinline__ void bptt_issue(const float* A, const float* B, int lda, int ldb, int m0, int n0, int k0,
+                                           float* As, float* Bs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  {  // A: wave w -> rows 16w .. 16w+15 (lane: row 16w + lane/4, LDS chunk lane%4)
+    const int row = 16 * w + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 1) & 3);
+    glds16m(A + (int64_t)(m0 + row) * lda + k0 + 4 * lc, As + 16 * w * 16);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // B: wave w -> k-rows 4w + 2i, +1
+    const int kr = 4 * w + 2 * i + (lane >> 5);
+    glds16m(B + (int64_t)(k0 + kr) * ldb + n0 + 4 * (lane & 31), Bs + (4 * w + 2 * i) * 128);
+  }
+}
+template <class C>
+__device__ __forceinline__ void bptt_mma(const float* as, const float* bs, Acc<C>& acc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+  const int arow = wm * (C::WTM * 32) + (lane & 31);
+  const int brow = wn * (C::WTN * 32) + (lane & 31);
+  const int h = lane >> 5;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    float4 a[C::WTM], b[C::WTN];
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) {
+      const int row = arow + 32 * i, pc = (2 * h + q) ^ ((row >> 1) & 3);
+      a[i] = *reinterpret_cast<const float4*>(as + row * 16 + 4 * pc);
+    }
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) {
+      const float* p = bs + (8 * h + 4 * q) * 128 + brow + 32 * j;
+      b[j] = make_float4(p[0], p[128], p[256], p[384]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::WTN; ++j)
+          acc.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b[j], e), acc.v[i][j], 0, 0, 0);
+  }
+}
+template <class C>
+__global__ __launch_bounds__(C::NTH) void k_gldsb(const float* A, const float* B, float* O, int M, int N, int K) {
+  static_assert(C::BM == 64 && C::BN == 128 && C::NTH == 256 && C::BK == 16, "BPTT tile");
+  __shared__ float smem[3 * (64 * 16 + 16 * 128)];
+  float* As = smem;
+  float* Bs = smem + 3 * 64 * 16;
+  const int m0 = blockIdx.x * C::BM, n0 = blockIdx.y * C::BN;
+  Acc<C> acc;
+  acc.zero();
+  const int nkt = K / 16;
+  bptt_issue(A, B, K, N, m0, n0, 0, As, Bs);
+  bptt_issue(A, B, K, N, m0, n0, 16, As + 1024, Bs + 2048);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    const int st = kt % 3;
+    if (kt + 2 < nkt) {
+      const int s2 = (kt + 2) % 3;
+      bptt_issue(A, B, K, N, m0, n0, (kt + 2) * 16, As + s2 * 1024, Bs + s2 * 2048);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    bptt_mma<C>(As + st * 1024, Bs + st * 2048, acc);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  const int c = n0 + acc_col<C>(0);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += acc.v[i][j][r];
+  O[(int64_t)blockIdx.x * C::NTH + threadIdx.x] = s + c;
+}
+template <class C>
+void run_gldsb(const char* name, const float* A, const float* B, float* O, int M, int N, int K) {
+  dim3 grid(M / C::BM, N / C::BN);
+  for (int i = 0; i < 3; ++i) k_gldsb<C><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) k_gldsb<C><<<grid, C::NTH>>>(A, B, O, M, N, K);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  const double tf = 2.0 * M * N * K * reps / (ms * 1e-3) / 1e12;
+  printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
+}
+
 template <class C>
 __global__ __launch_bounds__(C::NTH) void k_all(const float* A, const float* B, float* O, int M, int N, int K) {
   __shared__ float smem[C::SMEM_FLOATS];
@@ -275,6 +381,10 @@ int main() {
   for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
   hipMemcpy(A, h.data(), (size_t)Mmax * K * 4, hipMemcpyHostToDevice);
   hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice);
+  for (int rep = 0; rep < 3; ++rep) {
+    run_gldsb<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  glds ring3", A, B, O, M, N, K);
+    run<GemmCfg<64, 128, 2, 2, true, false, 16>, true>("64x128 w2x2 BK16  B MC (current)", A, B, O, M, N, K);
+  }
   for (int rep = 0; rep < 3; ++rep) {
     run_ring<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  ring3", A, B, O, M, N, K);
     run_ring<GemmCfg<64, 128, 2, 2, true, false, 32>>("64x128 w2x2 BK32  ring3", A, B, O, M, N, K);
