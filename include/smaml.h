@@ -248,7 +248,10 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  64x128 tiles use them (else 64x64 or split-K tiles);
  *   "split_max":                   split-K ways of small-grid LSTM steps (1 = off);
  *   "keep":                        cap on second-order inner steps whose primal is kept
- *                                  (-1 = the SMAML_KEEP environment variable / all that fit). */
+ *                                  (-1 = the SMAML_KEEP environment variable / all that fit);
+ *   "wgrad_group_max_rows":        a backward with tasks x rows <= this runs all LSTM weight
+ *                                  gradients as one launch after the BPTT (batch-1 adaptation);
+ *   "wgrad_group_wgs":             workgroups that grouped launch aims for. */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus
