@@ -251,7 +251,9 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  (-1 = the SMAML_KEEP environment variable / all that fit);
  *   "wgrad_group_max_rows":        a backward with tasks x rows <= this runs all LSTM weight
  *                                  gradients as one launch after the BPTT (batch-1 adaptation);
- *   "wgrad_group_wgs":             workgroups that grouped launch aims for. */
+ *   "wgrad_group_wgs":             workgroups that grouped launch aims for;
+ *   "bwd_pair":                    1 = big-tile BPTT launches deal row tiles so that the two
+ *                                  readers of each dG cell run on one XCD together (0 = off). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -290,6 +290,89 @@ void run_gldsb(const char* name, const float* A, const float* B, float* O, int M
   printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
 }
 
+// 256 x 128 tile, 8 waves of 32 x 128 (8 x 1), direct-to-LDS 3-stage ring (72 KB: two
+// workgroups per CU): A rows swizzled as in k_gldsb, B rows unpadded.
+__device__ __forceinline__ void bptt_issue256(const float* A, const float* B, int lda, int ldb, int m0, int n0, int k0,
+                                              float* As, float* Bs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // A: 16 instructions of 16 rows; wave w -> row blocks 2w, 2w+1
+    const int rb = 2 * w + i;
+    const int row = 16 * rb + (lane >> 2), pc = lane & 3, lc = pc ^ ((row >> 1) & 3);
+    glds16m(A + (int64_t)(m0 + row) * lda + k0 + 4 * lc, As + rb * 256);
+  }
+  const int kr = 2 * w + (lane >> 5);  // B: 8 instructions of 2 rows; wave w -> rows 2w, 2w+1
+  glds16m(B + (int64_t)(k0 + kr) * ldb + n0 + 4 * (lane & 31), Bs + 2 * w * 128);
+}
+__global__ __launch_bounds__(512) void k_gldsb256(const float* A, const float* B, float* O, int M, int N, int K) {
+  using C = GemmCfg<256, 128, 8, 1, true, false, 16>;
+  __shared__ float smem[3 * (256 * 16 + 16 * 128)];
+  float* As = smem;
+  float* Bs = smem + 3 * 256 * 16;
+  const int m0 = blockIdx.x * 256, n0 = blockIdx.y * 128;
+  Acc<C> acc;
+  acc.zero();
+  const int nkt = K / 16;
+  bptt_issue256(A, B, K, N, m0, n0, 0, As, Bs);
+  bptt_issue256(A, B, K, N, m0, n0, 16, As + 4096, Bs + 2048);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int arow = wave * 32 + (lane & 31), h = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    const int st = kt % 3;
+    if (kt + 2 < nkt) {
+      const int s2 = (kt + 2) % 3;
+      bptt_issue256(A, B, K, N, m0, n0, (kt + 2) * 16, As + s2 * 4096, Bs + s2 * 2048);
+    }
+    const float* as = As + st * 4096;
+    const float* bs = Bs + st * 2048;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int pc = (2 * h + q) ^ ((arow >> 1) & 3);
+      const float4 a = *reinterpret_cast<const float4*>(as + arow * 16 + 4 * pc);
+      float4 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* p = bs + (8 * h + 4 * q) * 128 + 32 * j + (lane & 31);
+        b[j] = make_float4(p[0], p[128], p[256], p[384]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc.v[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a, e), f4get(b[j], e), acc.v[0][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sum += acc.v[0][j][r];
+  O[(int64_t)blockIdx.x * 512 + threadIdx.x] = sum;
+}
+void run_gldsb256(const char* name, const float* A, const float* B, float* O, int M, int N, int K) {
+  dim3 grid(M / 256, N / 128);
+  for (int i = 0; i < 3; ++i) k_gldsb256<<<grid, 512>>>(A, B, O, M, N, K);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) k_gldsb256<<<grid, 512>>>(A, B, O, M, N, K);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  const double tf = 2.0 * M * N * K * reps / (ms * 1e-3) / 1e12;
+  printf("%-36s %8.1f us  %6.1f TF/s\n", name, ms * 1e3 / reps, tf);
+}
+
 template <class C>
 __global__ __launch_bounds__(C::NTH) void k_all(const float* A, const float* B, float* O, int M, int N, int K) {
   __shared__ float smem[C::SMEM_FLOATS];
@@ -382,6 +465,8 @@ int main() {
   hipMemcpy(A, h.data(), (size_t)Mmax * K * 4, hipMemcpyHostToDevice);
   hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice);
   for (int rep = 0; rep < 3; ++rep) {
+    run_gldsb256("256x128 w8x1 BK16 glds ring3", A, B, O, M, N, K);
+    run_gldsb256("256x128 w8x1 glds, 2.0 rounds", A, B, O, 256 * 256 * 2 * 2, N, K);
     run_gldsb<GemmCfg<64, 128, 2, 2, true, false, 16>>("64x128 w2x2 BK16  glds ring3", A, B, O, M, N, K);
     run<GemmCfg<64, 128, 2, 2, true, false, 16>, true>("64x128 w2x2 BK16  B MC (current)", A, B, O, M, N, K);
   }

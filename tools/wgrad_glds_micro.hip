@@ -17,17 +17,28 @@ struct CfgG : CfgR {  // unpadded B rows (a glds wave-instruction writes 2 rows 
   static constexpr int LDB = 128;
   static constexpr int B_STAGE = 16 * 128;
 };
+struct CfgG4 : CfgG {  // unpadded A rows too (the 4-stage ring needs all 160 KB)
+  static constexpr int LDA = 512;
+  static constexpr int A_STAGE = 16 * 512;
+};
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_void;
 
-constexpr int KCH = 3328;  // K rows per workgroup (a k_wgrad split)
-constexpr int SLICES = 64;
+#ifndef KCH_
+#define KCH_ 3328
+#endif
+#ifndef SLICES_
+#define SLICES_ 64
+#endif
+constexpr int KCH = KCH_;  // K rows per workgroup (a k_wgrad split)
+constexpr int SLICES = SLICES_;  // distinct K slices (1536 = every workgroup its own, as in k_wgrad)
 
 __device__ __forceinline__ void glds16(const float* g, float* l) {
   __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)l, 16, 0, 0);
 }
 
 // tile kt of this workgroup's slice into stage st: 5 glds per wave (4 x A half-rows, 1 x B 2 rows)
+template <int LDA_ = CfgG::LDA>
 __device__ __forceinline__ void issue_tile(const float* A, const float* B, int k0, float* As, float* Bs) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -35,7 +46,7 @@ __device__ __forceinline__ void issue_tile(const float* A, const float* B, int k
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int row = 2 * w + r;
-      glds16(A + (int64_t)(k0 + row) * 512 + half * 256 + 4 * lane, As + row * CfgG::LDA + half * 256);
+      glds16(A + (int64_t)(k0 + row) * 512 + half * 256 + 4 * lane, As + row * LDA_ + half * 256);
     }
   const int brow = 2 * w + (lane >> 5);
   glds16(B + (int64_t)(k0 + brow) * 128 + 4 * (lane & 31), Bs + 2 * w * 128);
@@ -78,6 +89,47 @@ __global__ __launch_bounds__(512) void k_glds(const float* A0, const float* B0, 
         O[((int64_t)blockIdx.x * 512 + acc_row<CfgG>(i, r)) * 128 + acc_col<CfgG>(j)] = acc.v[i][j][r];
 }
 
+// 4-stage ring (160 KB: the whole LDS), three tiles in flight
+__global__ __launch_bounds__(512) void k_glds4(const float* A0, const float* B0, float* O) {
+  __shared__ float smem[4 * (CfgG4::A_STAGE + CfgG4::B_STAGE)];
+  float* As = smem;
+  float* Bs = smem + 4 * CfgG4::A_STAGE;
+  const int sl = blockIdx.x % SLICES;
+  const float* A = A0 + (int64_t)sl * KCH * 512;
+  const float* B = B0 + (int64_t)sl * KCH * 128;
+  Acc<CfgG4> acc;
+  acc.zero();
+  NoHook hook;
+  constexpr int nkt = KCH / 16;
+  issue_tile<512>(A, B, 0, As, Bs);
+  issue_tile<512>(A, B, 16, As + CfgG4::A_STAGE, Bs + CfgG4::B_STAGE);
+  issue_tile<512>(A, B, 32, As + 2 * CfgG4::A_STAGE, Bs + 2 * CfgG4::B_STAGE);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 2 < nkt)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (kt + 1 < nkt)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int st = kt & 3;
+    if (kt + 3 < nkt) {
+      const int s3 = (kt + 3) & 3;
+      issue_tile<512>(A, B, (kt + 3) * 16, As + s3 * CfgG4::A_STAGE, Bs + s3 * CfgG4::B_STAGE);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    mma_tile<CfgG4>(As + st * CfgG4::A_STAGE, Bs + st * CfgG4::B_STAGE, acc, hook);
+    __builtin_amdgcn_s_setprio(0);
+  }
+#pragma unroll
+  for (int i = 0; i < CfgG4::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < CfgG4::WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        O[((int64_t)blockIdx.x * 512 + acc_row<CfgG4>(i, r)) * 128 + acc_col<CfgG4>(j)] = acc.v[i][j][r];
+}
+
 __global__ __launch_bounds__(512) void k_reg(const float* A0, const float* B0, float* O) {
   __shared__ float smem[CfgR::SMEM_FLOATS];
   const int sl = blockIdx.x % SLICES;
@@ -93,6 +145,11 @@ __global__ __launch_bounds__(512) void k_reg(const float* A0, const float* B0, f
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         O[((int64_t)blockIdx.x * 512 + acc_row<CfgR>(i, r)) * 128 + acc_col<CfgR>(j)] = acc.v[i][j][r];
+}
+
+__global__ void k_fill(float* p, size_t n, size_t off) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = (float)(((i + off) * 2654435761u) % 1000) / 1000.f - 0.5f;
 }
 
 template <class K>
@@ -116,14 +173,14 @@ int main() {
   if (hipMalloc(&A, na * 4) || hipMalloc(&B, nb * 4)) return 1;
   const int wgs = 256 * 6;
   if (hipMalloc(&O1, (size_t)wgs * 512 * 128 * 4) || hipMalloc(&O2, (size_t)wgs * 512 * 128 * 4)) return 1;
-  std::vector<float> h(na);
-  for (size_t i = 0; i < na; ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
-  hipMemcpy(A, h.data(), na * 4, hipMemcpyHostToDevice);
-  hipMemcpy(B, h.data() + 12345, nb * 4, hipMemcpyHostToDevice);
+  k_fill<<<4096, 256>>>(A, na, 0);
+  k_fill<<<4096, 256>>>(B, nb, 12345);
   const double fl = 2.0 * 512 * 128 * KCH * wgs;
   for (int rep = 0; rep < 3; ++rep) {
     const float tr = timeit(k_reg, wgs, A, B, O1);
     const float tg = timeit(k_glds, wgs, A, B, O2);
+    const float t4 = timeit(k_glds4, wgs, A, B, O1);
+    printf("glds4 %8.1f us %6.1f TF/s\n", t4 * 1e3, fl / (t4 * 1e-3) / 1e12);
     printf("reg  %8.1f us %6.1f TF/s | glds %8.1f us %6.1f TF/s\n", tr * 1e3, fl / (tr * 1e-3) / 1e12, tg * 1e3,
            fl / (tg * 1e-3) / 1e12);
   }

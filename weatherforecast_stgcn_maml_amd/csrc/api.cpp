@@ -220,7 +220,8 @@ struct smaml_ctx {
   Staging stage;
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
-  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS};
+  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
+            SMAML_BWD_PAIR};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -827,6 +828,7 @@ int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out) {
   c->go.total = tot;
   if (const char* e = std::getenv("SMAML_BWD_BIG_MIN")) c->kn.bwd_big_min = std::atoi(e);
   if (const char* e = std::getenv("SMAML_BWDD_BIG_MIN")) c->kn.bwdd_big_min = std::atoi(e);
+  if (const char* e = std::getenv("SMAML_BWD_PAIR")) c->kn.bwd_pair = std::atoi(e) != 0;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
     delete c;
@@ -1222,6 +1224,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.split_max = (int)std::min<int64_t>(value, 64);
   } else if (k == "wgrad_group_max_rows" && value >= 0) {
     c->kn.wgrad_group_max_rows = (int)std::min<int64_t>(value, 1 << 30);
+  } else if (k == "bwd_pair" && (value == 0 || value == 1)) {
+    c->kn.bwd_pair = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {

@@ -108,7 +108,11 @@ struct Knobs {
   int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
   int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
   int wgrad_group_wgs;       // workgroups that grouped launch aims for
+  int bwd_pair;              // big-tile BPTT launches in the paired block order (bwd_block)
 };
+#ifndef SMAML_BWD_PAIR
+#define SMAML_BWD_PAIR 0
+#endif
 #ifndef SMAML_WGRAD_GROUP_ROWS
 #define SMAML_WGRAD_GROUP_ROWS 2048
 #endif
@@ -172,6 +176,7 @@ struct BwdWave {
   int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
   LayerOff lo[MAX_LAYERS];
   int64_t wih_up[MAX_LAYERS];  // W_ih offset of layer l+1 (unused at the top layer)
+  int pair;  // 1: paired block order (bwd_block; off[] spaced by a multiple of 8 row tiles)
 };
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv);

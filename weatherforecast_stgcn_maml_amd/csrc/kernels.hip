@@ -1067,12 +1067,14 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
   __shared__ float smem[epi_smem_floats<CfgNN>()];
   constexpr int G4 = 4 * H;
   const Blk bk = xcd_block();
-  const int p = wave_index(wv, bk.x);
-  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  int mb;
+  const int p = bwd_block(wv, bk.x, mb);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int z = bk.z;
-  const int m0 = (bk.x - b0) * CfgNN::BM, n0 = bk.y * CfgNN::BN;
+  const int m0 = mb * CfgNN::BM, n0 = bk.y * CfgNN::BN;
+  if (m0 >= M) return;  // padding tile of the paired order
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in
@@ -1098,8 +1100,12 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
         gemm_mainloop<CfgNN>(SegKC{{pn, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
                              SegMC{{th + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, 0, G4, acc, smem);
     } else {
-      const SegKCt<2> la{{up ? pa : pn, pn}, {G4, G4}, M};
-      const SegMCt<2> lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H};
+      // paired order: odd layers take the recurrent segment first, so both readers of a shared
+      // dG cell (bwd_block) stream it in the same half of their K loops
+      const bool sw = wv.pair && (l & 1) && up && nx;
+      const SegKCt<2> la{{sw ? pn : (up ? pa : pn), sw ? pa : pn}, {G4, G4}, M};
+      const SegMCt<2> lb{{sw ? th + lo.whh : (up ? th + wih_up : th + lo.whh), sw ? th + wih_up : th + lo.whh},
+                         {G4, G4}, H};
       if (ns && SMAML_DIAG_BWD != 2) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
   }
@@ -1258,11 +1264,16 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
   const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
+  const bool pair = w.kn.bwd_pair && !w.drop.lstm();
 #define SMAML_BWD_STEP(CFG, D_)                                                                               \
   SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
                             w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
   if ((int64_t)wv.n * ntm * ntn * w.Z >= w.kn.bwd_big_min) {
     count_variant(w, V_BWD_BIG);
+    if (pair) {
+      bwd_wave(d, w, po, e, (ntm + 7) / 8 * 8, false, wv);
+      wv.pair = 1;
+    }
     dim3 grid(wv.off[wv.n], ntn, w.Z);
     if (w.drop.lstm()) {
       SMAML_BWD_STEP(CfgBwd, true);

@@ -492,12 +492,14 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   static_assert(DualStage<CfgNND>::FLOATS >= CfgNND::BM * CfgNND::BN, "epilogue transpose fits the staging LDS");
   constexpr int G4 = 4 * H;
   const Blk bk = xcd_block();
-  const int p = wave_index(wv, bk.x);
-  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  int mb;
+  const int p = bwd_block(wv, bk.x, mb);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int z = bk.z;
-  const int m0 = (bk.x - b0) * CfgNND::BM, n0 = bk.y * CfgNND::BN;
+  const int m0 = mb * CfgNND::BM, n0 = bk.y * CfgNND::BN;
+  if (m0 >= M) return;  // padding tile of the paired order
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
@@ -538,12 +540,16 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                           SegMC{{th + lo.whh, nullptr}, {G4, 0}, H},
                                           SegMC{{u + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, G4, 0, ap, at, smem);
     } else if (ns && SMAML_DIAG_BWDD != 2) {
-      const float* a0 = up ? dGAll + oa : dGz + on;
-      const float* r0 = up ? RGsAll + oa : RGz + on;
-      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, dGz + on}, {G4, G4}, M}, SegKCt<2>{{r0, RGz + on}, {G4, G4}, M},
-                                        SegMCt<2>{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H},
-                                        SegMCt<2>{{up ? u + wih_up : u + lo.whh, u + lo.whh}, {G4, G4}, H}, m0, n0,
-                                        ns * G4, 0, ap, at, smem);
+      // paired order (k_lstm_bwd_step): odd layers take the recurrent segment first
+      const bool sw = wv.pair && (l & 1) && up && nx;
+      const float* a0 = up && !sw ? dGAll + oa : dGz + on;
+      const float* r0 = up && !sw ? RGsAll + oa : RGz + on;
+      const float* a1 = sw ? dGAll + oa : dGz + on;
+      const float* r1 = sw ? RGsAll + oa : RGz + on;
+      const int64_t w0o = up && !sw ? wih_up : lo.whh, w1o = sw ? wih_up : lo.whh;
+      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, a1}, {G4, G4}, M}, SegKCt<2>{{r0, r1}, {G4, G4}, M},
+                                        SegMCt<2>{{th + w0o, th + w1o}, {G4, G4}, H},
+                                        SegMCt<2>{{u + w0o, u + w1o}, {G4, G4}, H}, m0, n0, ns * G4, 0, ap, at, smem);
     }
   }
   const bool first = (t == T - 1);
@@ -641,6 +647,10 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   const bool kept = w.primal_kept != 0;
   if ((int64_t)wv.n * ntm * ntn * w.Z >= w.kn.bwdd_big_min) {
     count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
+    if (w.kn.bwd_pair && !w.drop.lstm()) {
+      bwd_wave(d, w, po, e, (ntm + 7) / 8 * 8, true, wv);
+      wv.pair = 1;
+    }
     if (kept)
       bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
     else

@@ -515,6 +515,23 @@ __device__ __forceinline__ T wave_sel(const T (&a)[N], int p) {
     if (q == p) v = a[q];
   return v;
 }
+// BPTT diagonal block -> (problem p, row tile mb). Problems p and p+1 (layers l and l-1) share one
+// operand cell: dG(l, t+1) is p's recurrent segment and p+1's layer-above segment. In the paired
+// order (wv.pair) blocks are dealt 8 row tiles of each problem in turn, so row tile mb of p and of
+// p+1 are 8 linear ids apart -- same XCD (round robin), dispatched together -- and the second
+// reader of each shared dG row finds it in that XCD's L2. (Off: problem-major, as launched.)
+template <class WV>
+__device__ __forceinline__ int bwd_block(const WV& wv, int bx, int& mb) {
+  if (wv.pair) {
+    const int per = 8 * wv.n, g = bx / per, r = bx - g * per;
+    mb = g * 8 + (r & 7);
+    return r >> 3;
+  }
+  const int p = wave_index(wv, bx);
+  mb = bx - wave_sel(wv.off, p);
+  return p;
+}
+
 template <class WV, class LO>
 __device__ __forceinline__ void wave_problem(const WV& wv, int bx, int& l, int& t, LO& lo, int& b0) {
   const int p = wave_index(wv, bx);
