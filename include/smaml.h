@@ -52,6 +52,10 @@ typedef struct smaml_dims {
 
 const char* smaml_last_error(void);
 int32_t smaml_abi_version(void);
+/* Build description: the product form of each GEMM family (bf16x6 = each f32 operand split into
+ * three bf16 pieces, six piece products on v_mfma_f32_32x32x16_bf16 accumulated in f32; or the
+ * f32 MFMA). Host-only, no GPU needed. */
+const char* smaml_build_info(void);
 
 /* ---- host-only helpers (no GPU needed) ------------------------------------------ */
 

@@ -1,0 +1,80 @@
+"""f32 accuracy of the HIP path against a float64 restatement.
+
+Every contraction on the hot path runs as f32-accurate products on the bf16 MFMA pipe
+(gemm_core.h ``SMAML_X6``: each f32 operand split into three bf16 pieces, the six leading
+piece products accumulated in f32) or, in the ``SMAML_X6=0`` build, on
+``v_mfma_f32_32x32x2_f32``. Either way the claim is f32 arithmetic, so the test prices the GPU
+result's error against float64 (the oracle run in f64 on the same inputs) next to the error of
+the reference's own precision (the oracle in f32 on the CPU, MKL) and requires the GPU to be no
+less accurate than that, up to a small factor for summation-order noise.
+
+Workload: BASELINE config-2 shapes (N=441, Hc=256, LSTM 4x128), one task, B=2, K=2 inner steps,
+second order, clip active and inactive: forward, BPTT, weight gradients, the tangent sweep.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import refcpu
+from weatherforecast_stgcn_maml_amd import params, synth
+from weatherforecast_stgcn_maml_amd.config import CONFIG2, MamlConfig
+from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
+from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+FACTOR = 3.0  # GPU error vs f64 may be at most this times the CPU-f32 error vs f64 (+ a floor)
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 0.02])
+def test_f32_accuracy_against_float64(max_norm):
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=2, order=2, max_norm=max_norm)
+    P = synth.init_params(21, d, gcn_bias_scale=0.1)
+    names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
+    theta = {k: P[k] for k in names}
+    gcn = {k: v for k, v in P.items() if k not in names}
+    side = int(round(d.num_nodes ** 0.5))
+    lats, lons = synth.region_grid(n_lat=side, n_lon=side)
+    ei = build_spatial_graph(lats, lons, 4)[0]
+    feats = synth.make_features(1300, d.num_nodes, stream_len_for(cfg, d))
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml.set_tasks([feats])
+    fast = torch.zeros(1, ml.theta.numel(), device=DEV)
+    res = ml.meta_step(fast_out=fast)
+    torch.cuda.synchronize()
+    q = list(ml.default_windows()[-1, 0])
+    S = cfg.inner_steps * cfg.batch
+
+    def oracle(dtype):
+        PT = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dtype) for k, v in P.items()}
+        task = refcpu.TaskData(feats.astype(np.float64 if dtype == torch.float64 else np.float32), ei, d)
+        return refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
+                                [task], q, cfg.inner_steps, cfg.batch, S, cfg.inner_lr, cfg.max_norm, 2)
+
+    r64, r32 = oracle(torch.float64), oracle(torch.float32)
+    mg = params.unpack(ml.meta_grad, d, 0)
+    ad = params.unpack(fast[0], d, 0)
+    rows = []
+    for k in names:
+        e_gpu = rel(mg[k].cpu().numpy(), r64["meta_grad"][k].numpy())
+        e_cpu = rel(r32["meta_grad"][k].numpy(), r64["meta_grad"][k].numpy())
+        rows.append(("meta_grad/" + k, e_gpu, e_cpu))
+        e_gpu = rel(ad[k].cpu().numpy(), r64["adapted"][0][k].numpy())
+        e_cpu = rel(r32["adapted"][0][k].numpy(), r64["adapted"][0][k].numpy())
+        rows.append(("adapted/" + k, e_gpu, e_cpu))
+    ql = float(res.losses.cpu().numpy()[-1, 0])
+    rows.append(("query_mse", abs(ql - r64["query_losses"][0]) / r64["query_losses"][0],
+                 abs(r32["query_losses"][0] - r64["query_losses"][0]) / r64["query_losses"][0]))
+    worst = max(rows, key=lambda r: r[1] / max(r[2], 1e-7))
+    print(f"\nmax_norm={max_norm}: worst GPU/CPU-f32 error ratio {worst[0]}: gpu {worst[1]:.3e} cpu {worst[2]:.3e}; "
+          f"mean gpu {np.mean([r[1] for r in rows]):.3e} cpu {np.mean([r[2] for r in rows]):.3e}")
+    for name, e_gpu, e_cpu in rows:
+        assert e_gpu <= FACTOR * e_cpu + 1e-7, (name, e_gpu, e_cpu)

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("SMAML_LIB") or os.path.join(HERE, "libsmaml.so")
 
 # every function include/smaml.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = (
-    "smaml_last_error", "smaml_abi_version", "smaml_param_layout", "smaml_graph_ell",
+    "smaml_last_error", "smaml_abi_version", "smaml_build_info", "smaml_param_layout", "smaml_graph_ell",
     "smaml_create", "smaml_destroy", "smaml_set_graph", "smaml_set_gcn_params", "smaml_reserve",
     "smaml_workspace_bytes", "smaml_so_kept_steps", "smaml_set_dropout", "smaml_set_task_ids", "smaml_gcn_conv", "smaml_forward", "smaml_set_tasks",
     "smaml_meta_step", "smaml_adamw_step", "smaml_adapt_steps", "smaml_timing", "smaml_timing_collect",
@@ -70,6 +70,7 @@ PDIMS = ctypes.POINTER(Dims)
 _SIGS = {
     "smaml_last_error": ([], ctypes.c_char_p),
     "smaml_abi_version": ([], I32),
+    "smaml_build_info": ([], ctypes.c_char_p),
     "smaml_param_layout": ([PDIMS, I32, PI64, PI64, I32, PI32, PI64], I32),
     "smaml_graph_ell": ([PI64, I64, I32, PI32, PF32], I32),
     "smaml_create": ([PDIMS, I32, ctypes.POINTER(P)], I32),
@@ -126,6 +127,17 @@ def lib():
                 fn.restype = res
             _lib = L
     return _lib
+
+
+def build_info() -> str:
+    """The library's product form per GEMM family (smaml_build_info)."""
+    return lib().smaml_build_info().decode()
+
+
+def x6_families() -> dict:
+    """{family: True if its products run as bf16x6 on the bf16 MFMA pipe} from build_info()."""
+    tail = build_info().split(":", 1)[1]
+    return {k: v == "1" for k, v in (kv.split("=") for kv in tail.split())}
 
 
 def check(rc):

@@ -755,6 +755,8 @@ const char* smaml_last_error(void) { return g_err.c_str(); }
 
 int32_t smaml_abi_version(void) { return 4; }
 
+const char* smaml_build_info(void) { return smaml::products_info(); }
+
 int smaml_param_layout(const smaml_dims* dims, int32_t which, int64_t* offsets, int64_t* sizes, int32_t cap,
                        int32_t* count, int64_t* total) {
   TRY(check_dims(dims));

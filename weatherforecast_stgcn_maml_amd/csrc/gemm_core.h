@@ -34,6 +34,9 @@ constexpr int BK = 32;  // default K-tile (GemmCfg's BK_ parameter)
 #endif                // (IG template argument; A/B: fwd_dual -7, wgrad -7, GCN -2 ms; the primal
                       // gate / BPTT / dual-BPTT loops are slower with it and keep the default order)
 constexpr int NT = 256;  // threads per workgroup of the 4-wave configurations
+#ifndef SMAML_X6
+#define SMAML_X6 1  // default product form of GemmCfg: 1 = bf16x6 (f32-accurate, see mfma_x6), 0 = f32 MFMA
+#endif
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
@@ -53,9 +56,30 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
   return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
 }
 
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32>
+// bf16-piece LDS image of one operand tile for the staged split (GemmCfg X6_ = 2): three planes
+// (x0, x1, x2), each bf16. KC operands: [rows][BK] per plane, 16-B chunks XOR-swizzled by row so the
+// ds_read_b128 fragment reads are conflict-free; MC operands: [BK][rows] per plane with a row
+// stride of 2*rows + 64 B (== 64 or 192 mod 256), read transposed by ds_read_b64_tr_b16.
+template <int ROWS, bool KC, int BK>
+struct X6Img {
+  static constexpr int NCH = BK / 8;                       // 16-B chunks per KC row
+  static constexpr int RS = KC ? 2 * BK : 2 * ROWS + 64;   // bytes per image row
+  static constexpr int PLANE = KC ? ROWS * RS : BK * RS;   // bytes per plane
+  static constexpr int BYTES = 3 * PLANE;
+  static_assert(!KC || NCH == 2 || NCH == 4 || NCH == 8, "KC staged split: BK 16, 32 or 64");
+  static_assert(KC || ROWS % 64 == 0, "MC staged split: rows multiple of 64");
+  __device__ static __forceinline__ int swz(int r) {
+    return NCH == 2 ? (r >> 3) & 1 : NCH == 4 ? (r >> 2) & 3 : (r >> 1) & 7;
+  }
+};
+
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32, int X6_ = SMAML_X6>
 struct GemmCfg {
   static constexpr int BK = BK_;
+  // products: 0 = v_mfma_f32_32x32x2_f32; 1 = bf16x6 with the split on the MFMA fragments (mma_tile);
+  // 2 = bf16x6 with the split done once per element at the LDS store (gemm_mainloop, "staged")
+  static constexpr bool X6 = X6_ != 0;
+  static constexpr bool X6S = X6_ == 2;
   static_assert(BK % 16 == 0, "BK multiple of 16");
   static constexpr int BM = BM_;
   static constexpr int BN = BN_;
@@ -75,7 +99,10 @@ struct GemmCfg {
   static constexpr int A_F4 = BM * BK / 4 / NTH;
   static constexpr int B_F4 = BN * BK / 4 / NTH;
   static_assert(A_F4 * 4 * NTH == BM * BK && B_F4 * 4 * NTH == BN * BK, "tile/threads");
-  static constexpr int SMEM_FLOATS = 2 * (A_STAGE + B_STAGE);
+  using AImg = X6Img<BM, A_KC, BK>;
+  using BImg = X6Img<BN, B_KC, BK>;
+  static constexpr int X6S_STAGE = AImg::BYTES + BImg::BYTES;  // bytes per staged-split stage
+  static constexpr int SMEM_FLOATS = (X6S && X6S_STAGE / 2 > A_STAGE + B_STAGE) ? X6S_STAGE / 2 : 2 * (A_STAGE + B_STAGE);
 };
 
 // Loaders that fetch a whole operand tile themselves (``kTileFetch``; loaders.h "tile
@@ -167,6 +194,58 @@ struct NoHook {
   __device__ __forceinline__ void afrag(int, const float4&) {}
 };
 
+// ---- fp32 products on the bf16 MFMA pipe (SMAML_X6) ---------------------------------------
+// x = x0 + x1 + x2 with each piece a bf16 (x0 = RNE(x), x1 = RNE(x - x0), x2 = RNE(x - x0 - x1);
+// the differences are exact in f32), so |x - x0 - x1 - x2| <= 2^-27 |x|. The product
+// a.b = sum_{i+j<=2} a_i.b_j + O(2^-26 |a||b|) needs six v_mfma_f32_32x32x16_bf16 (each a_i.b_j
+// is exact in f32; accumulation in f32 as in the f32 MFMA): an f32-accurate product at
+// 6 x 32 = 192 SIMD cycles per 32x32x16 step against 8 x 64 = 512 for v_mfma_f32_32x32x2_f32.
+// The fragment layout is the f32 one: for a 16-k step lane half h holds k = 8h .. 8h+7 of its row
+// in frag4(q = 2s) and frag4(q = 2s + 1), exactly the bf16 MFMA operand layout (8 consecutive k per
+// lane half), so the LDS images, loaders and hooks are unchanged; the split runs on the fragments.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+  bf16x8_t p0, p1, p2;
+};
+
+__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){x, y}, bf16x2_t));
+}
+
+__device__ __forceinline__ Split3 split3(const float4& lo, const float4& hi) {
+  const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u32x4_t q0, q1, q2;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float a = x[2 * e], b = x[2 * e + 1];
+    uint32_t u = pk_bf16(a, b);
+    q0[e] = u;
+    a -= __builtin_bit_cast(float, u << 16);
+    b -= __builtin_bit_cast(float, u & 0xffff0000u);
+    u = pk_bf16(a, b);
+    q1[e] = u;
+    a -= __builtin_bit_cast(float, u << 16);
+    b -= __builtin_bit_cast(float, u & 0xffff0000u);
+    q2[e] = pk_bf16(a, b);
+  }
+  return Split3{__builtin_bit_cast(bf16x8_t, q0), __builtin_bit_cast(bf16x8_t, q1), __builtin_bit_cast(bf16x8_t, q2)};
+}
+
+// acc += a . b over one 16-k step, smallest terms first.
+__device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p2, b.p0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p1, b.p1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b.p2, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p1, b.p0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b.p1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p0, b.p0, acc, 0, 0, 0);
+  return acc;
+}
+
 template <class C, int IG = -1, class Hook = NoHook>
 __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C>& acc, Hook& hook) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -175,6 +254,28 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
   const int brow = wn * (C::WTN * 32) + (lane & 31);
   const int h = lane >> 5;
   if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
+  if constexpr (C::X6) {
+#pragma unroll
+  for (int s = 0; s < C::BK / 16; ++s) {
+    Split3 a[C::WTM];
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) {
+      const float4 lo = frag4<C::A_KC, C::LDA, C::BK>(as, arow + 32 * i, h, 2 * s);
+      const float4 hi = frag4<C::A_KC, C::LDA, C::BK>(as, arow + 32 * i, h, 2 * s + 1);
+      hook.afrag(i, lo);
+      hook.afrag(i, hi);
+      a[i] = split3(lo, hi);
+    }
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) {
+      const Split3 b = split3(frag4<C::B_KC, C::LDB, C::BK>(bs, brow + 32 * j, h, 2 * s),
+                              frag4<C::B_KC, C::LDB, C::BK>(bs, brow + 32 * j, h, 2 * s + 1));
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i) acc.v[i][j] = mfma_x6(a[i], b, acc.v[i][j]);
+    }
+  }
+  return;
+  }
 #pragma unroll
   for (int q = 0; q < C::BK / 8; ++q) {
     float4 a[C::WTM], b[C::WTN];
@@ -194,11 +295,163 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
   }
 }
 
+// ---- staged split (GemmCfg X6_ = 2) ----------------------------------------------------------
+// The thread that fetched a float4 of an operand splits it once (split3 on 4 values) and writes the
+// three bf16 pieces into the planes of the tile's X6Img; the MFMA phase reads bf16 fragments
+// directly (KC: one ds_read_b128 per plane; MC: two ds_read_b64_tr_b16 per plane), so the split
+// costs 5.5 VALU per element per workgroup instead of per wave that reads the fragment.
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split4(const float4& v, uint2& p0, uint2& p1, uint2& p2) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t q0[2], q1[2], q2[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    float a = x[2 * e], b = x[2 * e + 1];
+    uint32_t u = pk_bf16(a, b);
+    q0[e] = u;
+    a -= __builtin_bit_cast(float, u << 16);
+    b -= __builtin_bit_cast(float, u & 0xffff0000u);
+    u = pk_bf16(a, b);
+    q1[e] = u;
+    a -= __builtin_bit_cast(float, u << 16);
+    b -= __builtin_bit_cast(float, u & 0xffff0000u);
+    q2[e] = pk_bf16(a, b);
+  }
+  p0 = make_uint2(q0[0], q0[1]);
+  p1 = make_uint2(q1[0], q1[1]);
+  p2 = make_uint2(q2[0], q2[1]);
+}
+
+// Split this thread's staged float4s of one operand tile into the image at `img` (byte base).
+template <int ROWS, int F4, int NTH, bool KC, int BK>
+__device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) {
+  using I = X6Img<ROWS, KC, BK>;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < F4; ++i) {
+    const int f = tid + NTH * i;
+    int off;
+    if (KC) {
+      const int rr = f / (BK / 4), q = f % (BK / 4);
+      off = rr * I::RS + 16 * ((q >> 1) ^ I::swz(rr)) + 8 * (q & 1);
+    } else {
+      const int kk = f / (ROWS / 4), q = f % (ROWS / 4);
+      off = kk * I::RS + 8 * q;
+    }
+    uint2 p0, p1, p2;
+    split4(r[i], p0, p1, p2);
+    *reinterpret_cast<uint2*>(img + off) = p0;
+    *reinterpret_cast<uint2*>(img + I::PLANE + off) = p1;
+    *reinterpret_cast<uint2*>(img + 2 * I::PLANE + off) = p2;
+  }
+}
+
+// The three pieces of the 32-row fragment at tile row `row` (this lane's row = row + (lane & 31)
+// for KC; the fragment's first row for MC), MFMA step s (k = 16s + 8h .. 16s + 8h + 7).
+template <int ROWS, bool KC, int BK>
+__device__ __forceinline__ Split3 frag_x6(const char* img, int row, int s) {
+  using I = X6Img<ROWS, KC, BK>;
+  const int lane = threadIdx.x & 63;
+  Split3 f;
+  if (KC) {
+    const int r = row + (lane & 31), h = lane >> 5;
+    const int off = r * I::RS + 16 * ((2 * s + h) ^ I::swz(r));
+    f.p0 = *reinterpret_cast<const bf16x8_t*>(img + off);
+    f.p1 = *reinterpret_cast<const bf16x8_t*>(img + I::PLANE + off);
+    f.p2 = *reinterpret_cast<const bf16x8_t*>(img + 2 * I::PLANE + off);
+  } else {
+    // ds_read_b64_tr_b16: per 16-lane group g, lane 4q+p addresses image row kb+q, columns
+    // c0+4p..c0+4p+3; lane i receives column c0+i of rows kb..kb+3 (element q = row kb+q).
+    const int g = lane >> 4, i = lane & 15;
+    const int h = g >> 1;
+    const int col = row + 16 * (g & 1) + 4 * (i & 3);
+    const int off = (16 * s + 8 * h + (i >> 2)) * I::RS + 2 * col;
+    typedef __attribute__((address_space(3))) bf16x4_t* lp;
+    auto rd = [&](int o) {
+      const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp)(img + o));
+      const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp)(img + o + 4 * I::RS));
+      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    f.p0 = rd(off);
+    f.p1 = rd(I::PLANE + off);
+    f.p2 = rd(2 * I::PLANE + off);
+  }
+  return f;
+}
+
+template <class C, int IG = -1>
+__device__ __forceinline__ void mma_tile_x6s(const char* as, const char* bs, Acc<C>& acc) {
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+  if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
+#pragma unroll
+  for (int s = 0; s < C::BK / 16; ++s) {
+    Split3 a[C::WTM];
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, C::BK>(as, wm * (C::WTM * 32) + 32 * i, s);
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) {
+      const Split3 b = frag_x6<C::BN, C::B_KC, C::BK>(bs, wn * (C::WTN * 32) + 32 * j, s);
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i) acc.v[i][j] = mfma_x6(a[i], b, acc.v[i][j]);
+    }
+  }
+}
+
+// Hooks may see the staged A float4s before the split (stage_a); see ColSumHook (kernels.hip).
+template <class H, class = void>
+struct has_stage_a : std::false_type {};
+template <class H>
+struct has_stage_a<H, std::void_t<decltype(&H::template stage_a<1>)>> : std::true_type {};
+
+template <class C, int IG, class LA, class LB, class Hook>
+__device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
+                                                  Acc<C>& acc, float* smem, Hook& hook) {
+  constexpr int BKc = C::BK;
+  constexpr int SA = C::AImg::BYTES;
+  char* st0 = reinterpret_cast<char*>(smem);
+  const int nkt = (kend - kbeg + BKc - 1) / BKc;
+  if (nkt <= 0) return;
+  float4 ra[C::A_F4], rb[C::B_F4];
+  auto store = [&](char* st) {
+    if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra);
+    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
+    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(st + SA, rb);
+  };
+  fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg, ra);
+  fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg, rb);
+  store(st0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (kt + 1) * BKc, ra);
+      fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg + (kt + 1) * BKc, rb);
+    }
+    const char* st = st0 + cur * C::X6S_STAGE;
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+    mma_tile_x6s<C, IG>(st, st + SA, acc);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    if (more) store(st0 + (cur ^ 1) * C::X6S_STAGE);
+    __syncthreads();
+  }
+}
+
 // acc += sum_{k in [kbeg,kend)} A[m0+., k] * B[n0+., k]
 // IG >= 0: ask LLVM for iglp_opt strategy IG in the MFMA phase (set per call site by A/B).
 template <class C, int IG = -1, class LA, class LB, class Hook>
 __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg,
                                               int kend, Acc<C>& acc, float* smem, Hook& hook) {
+  if constexpr (C::X6S) {
+    gemm_mainloop_x6s<C, IG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
+    return;
+  }
   float* As = smem;
   float* Bs = smem + 2 * C::A_STAGE;
   constexpr int BKc = C::BK;
@@ -313,6 +566,37 @@ template <class C, bool A2, bool PRIMAL = true>
 __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, int h, Acc<C>& accp, Acc<C>& acct) {
   constexpr int BKc = C::BK;
   constexpr int SA = C::A_STAGE, SB = C::B_STAGE;
+  if constexpr (C::X6) {
+#pragma unroll
+  for (int s = 0; s < BKc / 16; ++s) {
+    Split3 a[C::WTM], a2[C::WTM];
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i) {
+      a[i] = split3(frag4<C::A_KC, C::LDA, BKc>(st, arow + 32 * i, h, 2 * s),
+                    frag4<C::A_KC, C::LDA, BKc>(st, arow + 32 * i, h, 2 * s + 1));
+      if (A2)
+        a2[i] = split3(frag4<C::A_KC, C::LDA, BKc>(st + SA, arow + 32 * i, h, 2 * s),
+                       frag4<C::A_KC, C::LDA, BKc>(st + SA, arow + 32 * i, h, 2 * s + 1));
+    }
+#pragma unroll
+    for (int j = 0; j < C::WTN; ++j) {
+      const Split3 b2 = split3(frag4<C::B_KC, C::LDB, BKc>(st + 2 * SA + SB, brow + 32 * j, h, 2 * s),
+                               frag4<C::B_KC, C::LDB, BKc>(st + 2 * SA + SB, brow + 32 * j, h, 2 * s + 1));
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a[i], b2, acct.v[i][j]);
+      if (PRIMAL || A2) {
+        const Split3 b = split3(frag4<C::B_KC, C::LDB, BKc>(st + 2 * SA, brow + 32 * j, h, 2 * s),
+                                frag4<C::B_KC, C::LDB, BKc>(st + 2 * SA, brow + 32 * j, h, 2 * s + 1));
+#pragma unroll
+        for (int i = 0; i < C::WTM; ++i) {
+          if (PRIMAL) accp.v[i][j] = mfma_x6(a[i], b, accp.v[i][j]);
+          if (A2) acct.v[i][j] = mfma_x6(a2[i], b, acct.v[i][j]);
+        }
+      }
+    }
+  }
+  return;
+  }
 #pragma unroll
   for (int q = 0; q < BKc / 8; ++q) {
     float4 a[C::WTM], a2[C::WTM], b[C::WTN], b2[C::WTN];

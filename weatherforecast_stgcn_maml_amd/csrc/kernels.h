@@ -92,7 +92,7 @@ enum Variant {
 
 // Build-time defaults of the run-time knobs below.
 #ifndef SMAML_BWD_BIG_MIN
-#define SMAML_BWD_BIG_MIN (3 * 256)  // BPTT launches with >= this many 64x128 tiles use them
+#define SMAML_BWD_BIG_MIN (3 * 256)  // BPTT launches with >= this many 64-row x 128 tiles' worth of rows use the big tiles
 #endif
 #ifndef SMAML_BWDD_BIG_MIN
 #define SMAML_BWDD_BIG_MIN (3 * 256)
@@ -183,6 +183,8 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 // Fills wv for diagonal diag; returns its algorithmic flops (dual: primal + tangent GEMMs).
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
                 FwdWave& wv);
+
+const char* products_info();  // product form per GEMM family as built (kernels.hip)
 
 // ---- launchers (kernels.hip) ----
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,

@@ -19,10 +19,10 @@
 
 namespace smaml {
 
-using CfgNT = GemmCfg<128, 128, 2, 2, true, true>;    // C = A . B^T (both k-contiguous)
-using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;  // LSTM forward: wave = 32 rows x 4 gates
-using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK>;  // C = A . B   (B n-contiguous)
-using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK>;  // C = A^T . B (split-K weight grads)
+using CfgNT = GemmCfg<128, 128, 2, 2, true, true, 32, SMAML_X6_BWD>;    // C = A . B^T (both k-contiguous)
+using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;  // LSTM forward: wave = 32 rows x 4 gates
+using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK, SMAML_X6_BWD>;  // C = A . B   (B n-contiguous)
+using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK, SMAML_X6_WGRAD>;  // C = A^T . B (split-K weight grads)
 
 // ------------------------------------------------------------------------------------
 // Block-wide deterministic sum (fixed shuffle tree + fixed wave order).
@@ -100,7 +100,7 @@ struct GcnPlain {
 
 // 8 waves, 128 rows x 256 cols: one workgroup covers a row block's whole Hc=256 output,
 // so each input row is read once.
-using CfgGcn = GemmCfg<128, 256, 2, 4, true, true, SMAML_GCN_BK>;
+using CfgGcn = GemmCfg<128, 256, 2, 4, true, true, SMAML_GCN_BK, SMAML_X6_GCN>;
 
 __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
                                                            float* __restrict__ out, int cout, int remap, int relu,
@@ -906,9 +906,9 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
 // In place is safe: a workgroup reads G_t only for its own rows and units before writing them,
 // and its GEMM reads other (l, t) slabs finished on the previous diagonal.
 // 64x64 tiles for small grids (few tasks per rank) so the launch fills the chip.
-using CfgNNs = GemmCfg<64, 64, 2, 2, true, false, SMAML_NN_BK>;
+using CfgNNs = GemmCfg<64, 64, 2, 2, true, false, SMAML_NN_BK, SMAML_X6_BWD>;
 // BPTT step tile (A/B-able at build time): rows x 128 units, waves WM x WN
-using CfgBwd = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_NN_BK>;
+using CfgBwd = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_NN_BK, SMAML_X6_BWD>;
 
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv) {
@@ -1268,7 +1268,8 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 #define SMAML_BWD_STEP(CFG, D_)                                                                               \
   SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
                             w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
-  if ((int64_t)wv.n * ntm * ntn * w.Z >= w.kn.bwd_big_min) {
+  // threshold in 64-row tile units (the knob predates the 128-row tile)
+  if ((int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min) {
     count_variant(w, V_BWD_BIG);
     if (pair) {
       bwd_wave(d, w, po, e, (ntm + 7) / 8 * 8, false, wv);
@@ -1332,8 +1333,47 @@ struct ColSumHook {
   }
   __device__ __forceinline__ void operator()(const float*, int) const {}
   __device__ __forceinline__ void afrag(int i, const float4& a) { s[i] += (a.x + a.y) + (a.z + a.w); }
+  // staged split (CfgTN::X6S): the A float4s a thread stages always cover the same 4 gate rows
+  // 4q .. 4q+3 (q = tid mod BM/4); their sums are kept here and reduced over the NTH/(BM/4) threads
+  // sharing q in store().
+  static constexpr int kQ = CfgTN::BM / 4, kQT = CfgTN::NTH / kQ;
+  static_assert(!CfgTN::X6S || (CfgTN::NTH % kQ == 0 && !CfgTN::A_KC), "staged column sums: thread -> rows fixed");
+  float4 cs = f4zero();
+  template <int F4>
+  __device__ __forceinline__ void stage_a(const float4 (&r)[F4]) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      cs.x += r[i].x;
+      cs.y += r[i].y;
+      cs.z += r[i].z;
+      cs.w += r[i].w;
+    }
+  }
   // lanes 0..31 own rows wm*(WTM*32) + 32 i + lane of the tile
-  __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias) {
+  __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias, float* smem) {
+    if constexpr (CfgTN::X6S) {
+      // the mainloop ended with a barrier: its LDS is free
+      st4(smem + 4 * threadIdx.x, cs);
+      __syncthreads();
+      if ((int)threadIdx.x < kQ) {
+        float4 v = ld4(smem + 4 * threadIdx.x);
+#pragma unroll
+        for (int t = 1; t < kQT; ++t) {
+          const float4 u = ld4(smem + 4 * (threadIdx.x + kQ * t));
+          v.x += u.x;
+          v.y += u.y;
+          v.z += u.z;
+          v.w += u.w;
+        }
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int row = m0 + 4 * (int)threadIdx.x + c;
+          if (row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? e[c] : 0.f;
+        }
+      }
+      return;
+    }
     const int lane = threadIdx.x & 63, wm = (threadIdx.x >> 6) / CfgTN::WAVES_N;
 #pragma unroll
     for (int i = 0; i < CfgTN::WTM; ++i) {
@@ -1357,7 +1397,7 @@ struct ColSumHook {
     }
   }
   __device__ __forceinline__ void afrag(int, const float4&) {}
-  __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias) {
+  __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias, float*) {
     const int row = m0 + threadIdx.x;
     if (threadIdx.x < CfgTN::BM && row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? bsum : 0.f;
   }
@@ -1404,7 +1444,7 @@ struct CfgTNg : CfgTN {  // unpadded B rows
 };
 constexpr int WG_GLDS_SMEM = 3 * (CfgTNg::A_STAGE + CfgTNg::B_STAGE);
 constexpr bool kWgradGldsShape = CfgTN::BM == 512 && CfgTN::BN == 128 && CfgTN::BK == 16 && CfgTN::NTH == 512 &&
-                                 !CfgTN::A_KC && !CfgTN::B_KC;
+                                 !CfgTN::A_KC && !CfgTN::B_KC && !CfgTN::X6S;
 constexpr int WG_SMEM = (SMAML_WGRAD_GLDS && kWgradGldsShape && WG_GLDS_SMEM > CfgTN::SMEM_FLOATS) ? WG_GLDS_SMEM
                                                                                                     : CfgTN::SMEM_FLOATS;
 
@@ -1530,7 +1570,7 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
         if (row < Mrows) P[(int64_t)row * ldp + c] = acc.v[i][jj][r];
       }
     }
-  if (tn == 0) hook.store(P, m0, Mrows, ldp, ncols, with_bias != 0);
+  if (tn == 0) hook.store(P, m0, Mrows, ldp, ncols, with_bias != 0, smem);
 }
 
 template <bool DROP>
@@ -1892,4 +1932,14 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
   k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, step, b1, b2, eps, wd, max_norm);
 }
 
+}  // namespace smaml
+
+namespace smaml {
+#define SMAML_STR2(x) #x
+#define SMAML_STR(x) SMAML_STR2(x)
+// Product form per GEMM family as built (smaml_build_info): 1 = bf16x6, 0 = f32 MFMA.
+const char* products_info() {
+  return "products(1=bf16x6 f32-accurate, 0=f32 MFMA): gcn=" SMAML_STR(SMAML_X6_GCN) " gate=" SMAML_STR(
+      SMAML_X6_GATE) " gate_dual=" SMAML_STR(SMAML_X6_GATED) " bptt=" SMAML_STR(SMAML_X6_BWD) " bptt_dual=" SMAML_STR(SMAML_X6_BWDD) " wgrad=" SMAML_STR(SMAML_X6_WGRAD);
+}
 }  // namespace smaml

@@ -20,9 +20,9 @@ namespace smaml {
 #endif
 // The BPTT / dX / head duals stage four operand tiles per K-tile (gemm_dual_mainloop);
 // BK=16 keeps them at 54-80 KiB of LDS (two or more workgroups per CU).
-using CfgGateD = GemmCfg<32 * SMAML_GATED_WM, 128 * SMAML_GATE_WN, SMAML_GATED_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK>;
-using CfgNTD = GemmCfg<128, 128, 2, 2, true, true, SMAML_DUAL_BK>;
-using CfgNND = GemmCfg<64, 128, 2, 2, true, false, SMAML_DUAL_BK>;
+using CfgGateD = GemmCfg<32 * SMAML_GATED_WM, 128 * SMAML_GATE_WN, SMAML_GATED_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATED>;
+using CfgNTD = GemmCfg<128, 128, 2, 2, true, true, SMAML_DUAL_BK, SMAML_X6_BWDD>;
+using CfgNND = GemmCfg<64, 128, 2, 2, true, false, SMAML_DUAL_BK, SMAML_X6_BWDD>;
 
 __device__ __forceinline__ float block_sum_f(float v, float* red) {
 #pragma unroll
@@ -370,8 +370,8 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
 #ifndef SMAML_DIAG_BWDD
 #define SMAML_DIAG_BWDD 0  // timing diagnostics only (wrong results): 1 = kept tangent BPTT without its
 #endif                     // epilogue, 2 = without its GEMM
-using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK>;
-using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_DUAL_BK>;
+using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK, SMAML_X6_BWDD>;
+using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_DUAL_BK, SMAML_X6_BWDD>;
 
 // Tangent-only cell backward of a kept step (see kernels.hip bwd_cell_): R(dh) = the GEMM
 // accumulators, transposed through LDS so each lane works on float4 groups of 4 hidden units of
@@ -645,7 +645,7 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
   const bool kept = w.primal_kept != 0;
-  if ((int64_t)wv.n * ntm * ntn * w.Z >= w.kn.bwdd_big_min) {
+  if ((int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min) {  // 64-row tile units
     count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
     if (w.kn.bwd_pair && !w.drop.lstm()) {
       bwd_wave(d, w, po, e, (ntm + 7) / 8 * 8, true, wv);

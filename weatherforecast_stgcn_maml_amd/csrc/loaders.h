@@ -6,6 +6,27 @@
 #pragma once
 #include "gemm_core.h"
 
+// Product form per GEMM family (gemm_core.h GemmCfg X6_: 1 = f32-accurate bf16x6 on the bf16 MFMA
+// pipe, 0 = v_mfma_f32_32x32x2_f32); A/B-able at build time, default SMAML_X6.
+#ifndef SMAML_X6_GATE
+#define SMAML_X6_GATE SMAML_X6  // LSTM forward gate GEMM (primal)
+#endif
+#ifndef SMAML_X6_GATED
+#define SMAML_X6_GATED SMAML_X6  // LSTM forward gate GEMM (primal + tangent)
+#endif
+#ifndef SMAML_X6_BWD
+#define SMAML_X6_BWD SMAML_X6  // BPTT step (primal), head dh_T
+#endif
+#ifndef SMAML_X6_BWDD
+#define SMAML_X6_BWDD SMAML_X6  // BPTT step (tangent), head duals
+#endif
+#ifndef SMAML_X6_WGRAD
+#define SMAML_X6_WGRAD (SMAML_X6 ? 2 : 0)  // LSTM weight gradients (staged split: A/B 622 -> 499 ms)
+#endif
+#ifndef SMAML_X6_GCN
+#define SMAML_X6_GCN SMAML_X6  // GCN layers
+#endif
+
 // K-tile depth per GEMM family (A/B-able at build time: -DSMAML_GATE_BK=16 ...).
 #ifndef SMAML_GATE_BK
 #define SMAML_GATE_BK 16
@@ -23,7 +44,9 @@
 #define SMAML_NN_BK 16
 #endif
 #ifndef SMAML_BWD_BM
-#define SMAML_BWD_BM 64  // BPTT step tile rows (x 128 units)
+#define SMAML_BWD_BM (SMAML_X6 ? 128 : 64)  // BPTT step tile rows (x 128 units; 2x2 waves of 64x64: with the bf16x6 products
+                          // the larger wave tile halves the fragment splits per MFMA; A/B 64 -> 128: bwd 316 -> 278,
+                          // tangent bwd 472 -> 429 ms per meta-step)
 #endif
 #ifndef SMAML_BWD_WM
 #define SMAML_BWD_WM 2
