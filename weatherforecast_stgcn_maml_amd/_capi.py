@@ -134,10 +134,10 @@ def build_info() -> str:
     return lib().smaml_build_info().decode()
 
 
-def x6_families() -> dict:
-    """{family: True if its products run as bf16x6 on the bf16 MFMA pipe} from build_info()."""
+def product_forms() -> dict:
+    """{GEMM family: 0 = f32 MFMA, 1 = bf16x6 fragment split, 2 = bf16x6 staged split} (build_info())."""
     tail = build_info().split(":", 1)[1]
-    return {k: v == "1" for k, v in (kv.split("=") for kv in tail.split())}
+    return {k: int(v) for k, v in (kv.split("=") for kv in tail.split())}
 
 
 def check(rc):

@@ -35,8 +35,10 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     ``defines`` (e.g. ["SMAML_GATE_BK=16"]) build A/B variants."""
     if not force and not defines and out == OUT and up_to_date():
         return out
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(REPO, "include"),
-             "-I", CSRC, *[f"-D{d}" for d in defines]]
+    # -fno-slp-vectorize: keeps the bf16x6 split's f32 subtractions as v_sub_f32 instead of v_pk_add_f32
+    # (packed f32 VALU beside MFMAs costs extra issue cycles; A/B 2045 -> 2003 ms per meta-step)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize", "-I", os.path.join(REPO, "include"),
+             "-I", CSRC, *[f"-D{d}" for d in defines], *os.environ.get("SMAML_EXTRA_FLAGS", "").split()]
     objs, procs = [], []
     for src in SOURCES:
         obj = f"{out}.{os.path.basename(src)}.o"

@@ -1935,11 +1935,19 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
 }  // namespace smaml
 
 namespace smaml {
-#define SMAML_STR2(x) #x
-#define SMAML_STR(x) SMAML_STR2(x)
-// Product form per GEMM family as built (smaml_build_info): 1 = bf16x6, 0 = f32 MFMA.
+// Product form per GEMM family as built (smaml_build_info): 0 = f32 MFMA, 1 = bf16x6 with the
+// split on the MFMA fragments, 2 = bf16x6 with the split staged at the LDS store.
+template <class C>
+constexpr int product_form() {
+  return C::X6S ? 2 : C::X6 ? 1 : 0;
+}
 const char* products_info() {
-  return "products(1=bf16x6 f32-accurate, 0=f32 MFMA): gcn=" SMAML_STR(SMAML_X6_GCN) " gate=" SMAML_STR(
-      SMAML_X6_GATE) " gate_dual=" SMAML_STR(SMAML_X6_GATED) " bptt=" SMAML_STR(SMAML_X6_BWD) " bptt_dual=" SMAML_STR(SMAML_X6_BWDD) " wgrad=" SMAML_STR(SMAML_X6_WGRAD);
+  static char buf[256];
+  snprintf(buf, sizeof buf,
+           "products(0=f32 MFMA, 1=bf16x6 fragment split, 2=bf16x6 staged split): gcn=%d gate=%d gate_dual=%d "
+           "bptt=%d bptt_dual=%d wgrad=%d",
+           product_form<CfgGcn>(), product_form<CfgGate>(), SMAML_X6_GATED ? (SMAML_X6_GATED == 2 ? 2 : 1) : 0,
+           product_form<CfgBwd>(), SMAML_X6_BWDD ? (SMAML_X6_BWDD == 2 ? 2 : 1) : 0, product_form<CfgTN>());
+  return buf;
 }
 }  // namespace smaml

@@ -9,13 +9,13 @@
 // Product form per GEMM family (gemm_core.h GemmCfg X6_: 1 = f32-accurate bf16x6 on the bf16 MFMA
 // pipe, 0 = v_mfma_f32_32x32x2_f32); A/B-able at build time, default SMAML_X6.
 #ifndef SMAML_X6_GATE
-#define SMAML_X6_GATE SMAML_X6  // LSTM forward gate GEMM (primal)
+#define SMAML_X6_GATE (SMAML_X6 ? 2 : 0)  // LSTM forward gate GEMM (primal; staged with 256-row tiles: 268 -> 242 ms)
 #endif
 #ifndef SMAML_X6_GATED
-#define SMAML_X6_GATED SMAML_X6  // LSTM forward gate GEMM (primal + tangent)
+#define SMAML_X6_GATED (SMAML_X6 ? 2 : 0)  // LSTM forward gate GEMM (primal + tangent; staged, 256-row tiles: 406 -> 385 ms)
 #endif
 #ifndef SMAML_X6_BWD
-#define SMAML_X6_BWD SMAML_X6  // BPTT step (primal), head dh_T
+#define SMAML_X6_BWD (SMAML_X6 ? 2 : 0)  // BPTT step (primal), head dh_T (staged: A/B 286 -> 273 ms)
 #endif
 #ifndef SMAML_X6_BWDD
 #define SMAML_X6_BWDD SMAML_X6  // BPTT step (tangent), head duals
@@ -24,7 +24,7 @@
 #define SMAML_X6_WGRAD (SMAML_X6 ? 2 : 0)  // LSTM weight gradients (staged split: A/B 622 -> 499 ms)
 #endif
 #ifndef SMAML_X6_GCN
-#define SMAML_X6_GCN SMAML_X6  // GCN layers
+#define SMAML_X6_GCN (SMAML_X6 ? 2 : 0)  // GCN layers (staged: A/B 128 -> 121 ms)
 #endif
 
 // K-tile depth per GEMM family (A/B-able at build time: -DSMAML_GATE_BK=16 ...).
@@ -35,10 +35,11 @@
 #define SMAML_GATE_WN 1  // gate GEMM column waves: 1 -> 128x128 (4 waves), 2 -> 128x256 (8 waves)
 #endif
 #ifndef SMAML_GATE_WM
-#define SMAML_GATE_WM 4  // gate GEMM row waves (32 rows each): 4 -> 128-row tiles, 8 -> 256-row tiles
+#define SMAML_GATE_WM (SMAML_X6 ? 8 : 4)  // gate GEMM row waves (32 rows each): 4 -> 128-row tiles, 8 -> 256-row tiles
+                                          // (staged split: the B tile's split is shared by 256 rows; 2 WGs/CU)
 #endif
 #ifndef SMAML_GATED_WM
-#define SMAML_GATED_WM 4  // same, for the tangent (dual) gate kernel
+#define SMAML_GATED_WM (SMAML_X6 ? 8 : 4)  // same, for the tangent (dual) gate kernel
 #endif
 #ifndef SMAML_NN_BK
 #define SMAML_NN_BK 16
