@@ -557,9 +557,15 @@ namespace smaml {
 // four operand tiles are staged once (LDS: [A | A2 | B | B2] x 2 stages) and 3 MFMAs issue per
 // fragment pair. A2 is known to be zero for k < a2_kbeg (the layer-0 input has no tangent):
 // those K-tiles neither load A2 nor issue its MFMAs (a2_kbeg must be a multiple of BK).
+#ifndef SMAML_DUAL_X6S_STAGES
+#define SMAML_DUAL_X6S_STAGES 1  // LDS stages of the staged-split dual mainloop (1: register prefetch, two barriers)
+#endif
 template <class C>
 struct DualStage {
-  static constexpr int FLOATS = 2 * (2 * C::A_STAGE + 2 * C::B_STAGE);
+  static constexpr int X6S_BYTES = 2 * C::X6S_STAGE;  // [A | A2 | B | B2] images of one stage
+  static constexpr int X6S_FLOATS = SMAML_DUAL_X6S_STAGES * X6S_BYTES / 4;
+  static constexpr int FLOATS = C::X6S ? (X6S_FLOATS > C::BM * C::BN ? X6S_FLOATS : C::BM * C::BN)
+                                       : 2 * (2 * C::A_STAGE + 2 * C::B_STAGE);
 };
 
 template <class C, bool A2, bool PRIMAL = true>
@@ -625,12 +631,97 @@ __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, in
   }
 }
 
+// Staged split of the four operand tiles (C::X6S): images [A | A2 | B | B2] per stage. With one
+// stage (SMAML_DUAL_X6S_STAGES = 1) the next K-tile waits in registers during the MFMAs and is
+// stored between two barriers, which keeps the LDS at the epilogue's BM x BN floats.
+template <class C, bool PRIMAL, class LA, class LA2, class LB, class LB2>
+__device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& la2, const LB& lb, const LB2& lb2,
+                                                       int m0, int n0, int K, int a2_kbeg, Acc<C>& accp,
+                                                       Acc<C>& acct, float* smem) {
+  constexpr int BKc = C::BK;
+  constexpr int SA = C::AImg::BYTES, SB = C::BImg::BYTES;
+  constexpr int STAGE = 2 * SA + 2 * SB;
+  constexpr int NST = SMAML_DUAL_X6S_STAGES;
+  char* st0 = reinterpret_cast<char*>(smem);
+  const int nkt = (K + BKc - 1) / BKc;
+  if (nkt <= 0) return;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
+  float4 ra[C::A_F4], ra2[C::A_F4], rb[C::B_F4], rb2[C::B_F4];
+  auto fetch = [&](int k0) {
+    fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, k0, ra);
+    if (k0 >= a2_kbeg) fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la2, m0, k0, ra2);
+    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, k0, rb);
+    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb2, n0, k0, rb2);
+  };
+  auto store = [&](char* st, int k0) {
+    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
+    if (k0 >= a2_kbeg) store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st + SA, ra2);
+    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(st + 2 * SA, rb);
+    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(st + 2 * SA + SB, rb2);
+  };
+  auto mma = [&](const char* st, bool a2on) {
+#pragma unroll
+    for (int s = 0; s < BKc / 16; ++s) {
+      Split3 a[C::WTM], a2[C::WTM];
+#pragma unroll
+      for (int i = 0; i < C::WTM; ++i) {
+        a[i] = frag_x6<C::BM, C::A_KC, BKc>(st, wm * (C::WTM * 32) + 32 * i, s);
+        if (a2on) a2[i] = frag_x6<C::BM, C::A_KC, BKc>(st + SA, wm * (C::WTM * 32) + 32 * i, s);
+      }
+#pragma unroll
+      for (int j = 0; j < C::WTN; ++j) {
+        const int br = wn * (C::WTN * 32) + 32 * j;
+        const Split3 b2 = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA + SB, br, s);
+#pragma unroll
+        for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a[i], b2, acct.v[i][j]);
+        if (PRIMAL || a2on) {
+          const Split3 b = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA, br, s);
+#pragma unroll
+          for (int i = 0; i < C::WTM; ++i) {
+            if (PRIMAL) accp.v[i][j] = mfma_x6(a[i], b, accp.v[i][j]);
+            if (a2on) acct.v[i][j] = mfma_x6(a2[i], b, acct.v[i][j]);
+          }
+        }
+      }
+    }
+  };
+  fetch(0);
+  store(st0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * BKc;
+    const bool more = kt + 1 < nkt;
+    if (more) fetch(k0 + BKc);
+    const char* st = st0 + (NST == 1 ? 0 : (kt & 1) * STAGE);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+    if (k0 >= a2_kbeg)
+      mma(st, true);
+    else
+      mma(st, false);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    if (more) {
+      if (NST == 1) __syncthreads();  // every wave has read the stage
+      store(st0 + (NST == 1 ? 0 : ((kt + 1) & 1) * STAGE), k0 + BKc);
+    }
+    __syncthreads();
+  }
+}
+
 // PRIMAL = false: tangent only (acc_t += A2 . B + A . B2), acc_p untouched -- the primal
 // product is already stored (second-order sweep with the inner step's activations kept).
 template <class C, bool PRIMAL = true, class LA, class LA2, class LB, class LB2>
 __device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2, const LB& lb, const LB2& lb2,
                                                    int m0, int n0, int K, int a2_kbeg, Acc<C>& accp, Acc<C>& acct,
                                                    float* smem) {
+  if constexpr (C::X6S) {
+    gemm_dual_mainloop_x6s<C, PRIMAL>(la, la2, lb, lb2, m0, n0, K, a2_kbeg, accp, acct, smem);
+    return;
+  }
   constexpr int BKc = C::BK;
   constexpr int SA = C::A_STAGE, SB = C::B_STAGE;
   constexpr int STAGE = 2 * SA + 2 * SB;

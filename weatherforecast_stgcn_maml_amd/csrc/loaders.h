@@ -18,7 +18,7 @@
 #define SMAML_X6_BWD (SMAML_X6 ? 2 : 0)  // BPTT step (primal), head dh_T (staged: A/B 286 -> 273 ms)
 #endif
 #ifndef SMAML_X6_BWDD
-#define SMAML_X6_BWDD SMAML_X6  // BPTT step (tangent), head duals
+#define SMAML_X6_BWDD (SMAML_X6 ? 2 : 0)  // BPTT step (tangent), head duals (staged, one LDS stage: 423 -> 401 ms)
 #endif
 #ifndef SMAML_X6_WGRAD
 #define SMAML_X6_WGRAD (SMAML_X6 ? 2 : 0)  // LSTM weight gradients (staged split: A/B 622 -> 499 ms)
