@@ -34,6 +34,9 @@ constexpr int BK = 32;  // default K-tile (GemmCfg's BK_ parameter)
 #endif                // (IG template argument; A/B: fwd_dual -7, wgrad -7, GCN -2 ms; the primal
                       // gate / BPTT / dual-BPTT loops are slower with it and keep the default order)
 constexpr int NT = 256;  // threads per workgroup of the 4-wave configurations
+#ifndef SMAML_X6S_MIDSTORE
+#define SMAML_X6S_MIDSTORE 0  // staged split: next tile's stores between the two halves of the MFMA phase
+#endif
 #ifndef SMAML_X6
 #define SMAML_X6 1  // default product form of GemmCfg: 1 = bf16x6 (f32-accurate, see mfma_x6), 0 = f32 MFMA
 #endif
@@ -380,7 +383,8 @@ __device__ __forceinline__ Split3 frag_x6(const char* img, int row, int s) {
   return f;
 }
 
-template <class C, int IG = -1>
+// MFMAs of the B fragments j in [J0, J1) (all of them by default).
+template <class C, int IG = -1, int J0 = 0, int J1 = C::WTN>
 __device__ __forceinline__ void mma_tile_x6s(const char* as, const char* bs, Acc<C>& acc) {
   const int wave = threadIdx.x >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
@@ -391,7 +395,7 @@ __device__ __forceinline__ void mma_tile_x6s(const char* as, const char* bs, Acc
 #pragma unroll
     for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, C::BK>(as, wm * (C::WTM * 32) + 32 * i, s);
 #pragma unroll
-    for (int j = 0; j < C::WTN; ++j) {
+    for (int j = J0; j < J1; ++j) {
       const Split3 b = frag_x6<C::BN, C::B_KC, C::BK>(bs, wn * (C::WTN * 32) + 32 * j, s);
 #pragma unroll
       for (int i = 0; i < C::WTM; ++i) acc.v[i][j] = mfma_x6(a[i], b, acc.v[i][j]);
@@ -431,14 +435,23 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
       fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg + (kt + 1) * BKc, rb);
     }
     const char* st = st0 + cur * C::X6S_STAGE;
+    if constexpr (SMAML_X6S_MIDSTORE && C::WTN >= 2) {
+      // the next tile's split + LDS stores between the two halves of this tile's MFMAs (the
+      // other stage), so a SIMD's waves overlap them with MFMAs instead of meeting at the barrier
+      constexpr int JH = C::WTN / 2;
+      mma_tile_x6s<C, IG, 0, JH>(st, st + SA, acc);
+      if (more) store(st0 + (cur ^ 1) * C::X6S_STAGE);
+      mma_tile_x6s<C, IG, JH, C::WTN>(st, st + SA, acc);
+    } else {
 #if SMAML_PRIO
-    __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #endif
-    mma_tile_x6s<C, IG>(st, st + SA, acc);
+      mma_tile_x6s<C, IG>(st, st + SA, acc);
 #if SMAML_PRIO
-    __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
 #endif
-    if (more) store(st0 + (cur ^ 1) * C::X6S_STAGE);
+      if (more) store(st0 + (cur ^ 1) * C::X6S_STAGE);
+    }
     __syncthreads();
   }
 }

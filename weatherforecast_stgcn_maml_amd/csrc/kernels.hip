@@ -1429,6 +1429,11 @@ struct WgBDrop {
 #ifndef SMAML_WGRAD_GLDS
 #define SMAML_WGRAD_GLDS 1
 #endif
+// iglp_opt strategy for the weight-gradient mainloop (staged split: none, A/B 493 -> 483 ms)
+constexpr int kWgradIG = CfgTN::X6S ? -1 : SMAML_IGLP;
+#ifndef SMAML_WGRAD_TILE_LOADERS
+#define SMAML_WGRAD_TILE_LOADERS 0  // staged-split weight gradients through the MCKt / WgBt tile loaders
+#endif
 #ifndef SMAML_WGRAD_GLDS_IGLP
 #define SMAML_WGRAD_GLDS_IGLP -1
 #endif
@@ -1536,9 +1541,9 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
     const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
                               (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
     if (tn == 0 && with_bias) {
-      gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+      gemm_mainloop<CfgTN, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     } else {
-      gemm_mainloop<CfgTN, SMAML_IGLP>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
+      gemm_mainloop<CfgTN, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
   } else if (SMAML_WGRAD_GLDS && kWgradGldsShape && Mrows == CfgTN::BM && lb.c1 % CfgTN::BN == 0 &&
              lb.c2 % CfgTN::BN == 0) {
@@ -1549,12 +1554,19 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
       NoHook nh;
       wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, nh);
     }
+  } else if (SMAML_WGRAD_TILE_LOADERS && CfgTN::X6S && (lb.c2 == 0 || lb.c1 % CfgTN::BN == 0)) {
+    const MCKt lt{A + (int64_t)z * a_zstride, lb.K, Mrows};
+    const WgBt bt{b.B1, b.B2, b.c1, b.c2, b.K, b.Mshift};
+    if (tn == 0 && with_bias)
+      gemm_mainloop<CfgTN, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    else
+      gemm_mainloop<CfgTN, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem);
   } else if (tn == 0 && with_bias) {
-    // (the branch-free MCKt / WgBt tile loaders measured slower here: wgrad 723 -> 820 ms per
-    // meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log)
-    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    // (the branch-free MCKt / WgBt tile loaders measured slower here with the f32 MFMA: wgrad
+    // 723 -> 820 ms per meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log)
+    gemm_mainloop<CfgTN, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
-    gemm_mainloop<CfgTN, SMAML_IGLP>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    gemm_mainloop<CfgTN, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
   }
   const int ncols = lb.c1 + lb.c2;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;

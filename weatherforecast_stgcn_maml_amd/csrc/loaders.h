@@ -56,7 +56,7 @@
 #define SMAML_BWD_WN 2
 #endif
 #ifndef SMAML_GCN_BK
-#define SMAML_GCN_BK 16
+#define SMAML_GCN_BK (SMAML_X6 ? 32 : 16)  // (staged split: BK 32 measured 119 -> 116 ms)
 #endif
 // weight-gradient tile (BM x BN), waves WM x WN: all 4H = 512 gate rows of a layer in one
 // tile (8 waves of 64 x 128), so the split-K slices read each [x | h] row once
