@@ -37,6 +37,9 @@ constexpr int NT = 256;  // threads per workgroup of the 4-wave configurations
 #ifndef SMAML_X6S_MIDSTORE
 #define SMAML_X6S_MIDSTORE 0  // staged split: next tile's stores between the two halves of the MFMA phase
 #endif
+#ifndef SMAML_CHUNKED_F32
+#define SMAML_CHUNKED_F32 0  // chunked split-K mainloop (small grids) on the f32 MFMA (config 4 A/B: 1.137 ->
+#endif                       // 1.194 ms per sample-step, slower: off)
 #ifndef SMAML_X6
 #define SMAML_X6 1  // default product form of GemmCfg: 1 = bf16x6 (f32-accurate, see mfma_x6), 0 = f32 MFMA
 #endif
@@ -249,7 +252,8 @@ __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x
   return acc;
 }
 
-template <class C, int IG = -1, class Hook = NoHook>
+// F32: f32 MFMA products whatever C::X6 says (an A/B arm for the chunked split-K steps of small grids).
+template <class C, int IG = -1, class Hook = NoHook, bool F32 = false>
 __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C>& acc, Hook& hook) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
@@ -257,7 +261,7 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
   const int brow = wn * (C::WTN * 32) + (lane & 31);
   const int h = lane >> 5;
   if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
-  if constexpr (C::X6) {
+  if constexpr (C::X6 && !F32) {
 #pragma unroll
   for (int s = 0; s < C::BK / 16; ++s) {
     Split3 a[C::WTM];
@@ -553,7 +557,7 @@ __device__ __forceinline__ void gemm_mainloop_chunked(const LA& la, const LB& lb
 #endif
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
-      if (c0 + i < nkt) mma_tile<C>(As + i * C::A_STAGE, Bs + i * C::B_STAGE, acc, hook);
+      if (c0 + i < nkt) mma_tile<C, -1, NoHook, SMAML_CHUNKED_F32 != 0>(As + i * C::A_STAGE, Bs + i * C::B_STAGE, acc, hook);
 #if SMAML_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif

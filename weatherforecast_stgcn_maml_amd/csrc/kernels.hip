@@ -21,6 +21,9 @@ namespace smaml {
 
 using CfgNT = GemmCfg<128, 128, 2, 2, true, true, 32, SMAML_X6_BWD>;    // C = A . B^T (both k-contiguous)
 using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;  // LSTM forward: wave = 32 rows x 4 gates
+// split-K gate step of small grids (k_lstm_fwd_part / _cell / _cell_q): 128-row tiles whatever the
+// fused step uses (config 4 A/B with the bf16x6 products: 256-row 1.137 -> 128-row 1.031 ms per sample-step)
+using CfgGateP = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;
 using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK, SMAML_X6_BWD>;  // C = A . B   (B n-contiguous)
 using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK, SMAML_X6_WGRAD>;  // C = A^T . B (split-K weight grads)
 
@@ -228,7 +231,7 @@ struct LstmFwdB {  // logical row n = ug*128 + g*32 + jj  ->  weight row g*H + u
 // Per-task slabs are addressed with 32-bit offsets (T*M*4H < 2^31 is checked at reserve).
 // Cell epilogue of one gate tile (acc = the i, f, g, o pre-activations of 32 units x 32 rows
 // per wave, bias not yet added): gates, c_t = f c_{t-1} + i g, h_t = o tanh(c_t).
-template <int H, bool PRE = false>
+template <int H, bool PRE = false, class CfgGate = ::smaml::CfgGate>
 __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* __restrict__ th, const LayerOff& lo,
                                          float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
                                          int m0, int ug, int t, int M) {
@@ -427,10 +430,10 @@ __device__ __forceinline__ void part_mainloop(const LA& la, const LB& lb, int m0
 }
 
 template <int H>
-__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
+__global__ __launch_bounds__(CfgGateP::NTH) void k_lstm_fwd_part(
     const float* __restrict__ F, const float* __restrict__ HsAll, int64_t lsz, const float* __restrict__ theta,
     int64_t tstride, FwdWave wv, int T, int M, int S, float* __restrict__ part) {
-  __shared__ float smem[part_smem_floats<CfgGate, SMAML_FWD_PART_NCH>()];
+  __shared__ float smem[part_smem_floats<CfgGateP, SMAML_FWD_PART_NCH>()];
   int l, t, b0;
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
@@ -441,24 +444,24 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_part(
   const int64_t slab = (int64_t)z * T * M;
   const float* Hp = t > 0 ? HsAll + (int64_t)l * lsz + (slab + (int64_t)(t - 1) * M) * H : nullptr;
   int tm, ug;
-  constexpr int UPB = CfgGate::WAVES_N;
-  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+  constexpr int UPB = CfgGateP::WAVES_N;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGateP::BM - 1) / CfgGateP::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
     return;
-  const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
+  const int m0 = tm * CfgGateP::BM, n0 = ug * CfgGateP::BN;
   int kbeg, kend;
-  split_range(cin + (t > 0 ? H : 0), S, (int)blockIdx.y, CfgGate::BK, kbeg, kend);
-  Acc<CfgGate> acc;
+  split_range(cin + (t > 0 ? H : 0), S, (int)blockIdx.y, CfgGateP::BK, kbeg, kend);
+  Acc<CfgGateP> acc;
   acc.zero();
   if (kbeg < kend) {
     const SegGateBt<2> lb{{th + lo.wih, th + lo.whh}, {cin, H}, H};
     const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
-    part_mainloop<CfgGate, SMAML_FWD_PART_NCH>(la, lb, m0, n0, kbeg, kend, acc, smem);
+    part_mainloop<CfgGateP, SMAML_FWD_PART_NCH>(la, lb, m0, n0, kbeg, kend, acc, smem);
   }
-  store_part<CfgGate>(acc, part_slab<CfgGate>(part, S, (int)blockIdx.y));
+  store_part<CfgGateP>(acc, part_slab<CfgGateP>(part, S, (int)blockIdx.y));
 }
 
 template <int H>
-__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restrict__ HsAll, float* __restrict__ CsAll,
+__global__ __launch_bounds__(CfgGateP::NTH) void k_lstm_fwd_cell(float* __restrict__ HsAll, float* __restrict__ CsAll,
                                                                float* __restrict__ GsAll, int64_t lsz,
                                                                const float* __restrict__ theta, int64_t tstride,
                                                                FwdWave wv, int T, int M, int S,
@@ -467,17 +470,17 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restric
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
   int tm, ug;
-  constexpr int UPB = CfgGate::WAVES_N;
-  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+  constexpr int UPB = CfgGateP::WAVES_N;
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGateP::BM - 1) / CfgGateP::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
     return;
-  Acc<CfgGate> acc;
+  Acc<CfgGateP> acc;
   acc.zero();
   float* p0 = const_cast<float*>(part);
-  for (int q = 0; q < S; ++q) add_part<CfgGate>(acc, part_slab<CfgGate>(p0, S, q));
+  for (int q = 0; q < S; ++q) add_part<CfgGateP>(acc, part_slab<CfgGateP>(p0, S, q));
   const int z = blockIdx.z;
   const int64_t slab = (int64_t)z * T * M;
-  fwd_cell<H, true>(acc, theta + (int64_t)z * tstride, lo, GsAll + (int64_t)l * lsz * 4 + slab * (4 * H),
-              CsAll + (int64_t)l * lsz + slab * H, HsAll + (int64_t)l * lsz + slab * H, tm * CfgGate::BM, ug, t, M);
+  fwd_cell<H, true, CfgGateP>(acc, theta + (int64_t)z * tstride, lo, GsAll + (int64_t)l * lsz * 4 + slab * (4 * H),
+              CsAll + (int64_t)l * lsz + slab * H, HsAll + (int64_t)l * lsz + slab * H, tm * CfgGateP::BM, ug, t, M);
 }
 
 // The same cell step spread over 4x the threads: blockIdx.y = q picks accumulator registers
@@ -485,29 +488,29 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell(float* __restric
 // in flight together, then 4 rows' c_{t-1} loads. Sums the partials in the same order as
 // k_lstm_fwd_cell (bitwise identical results).
 template <int H>
-__global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell_q(float* __restrict__ HsAll, float* __restrict__ CsAll,
+__global__ __launch_bounds__(CfgGateP::NTH) void k_lstm_fwd_cell_q(float* __restrict__ HsAll, float* __restrict__ CsAll,
                                                                  float* __restrict__ GsAll, int64_t lsz,
                                                                  const float* __restrict__ theta, int64_t tstride,
                                                                  FwdWave wv, int T, int M, int S,
                                                                  const float* __restrict__ part) {
-  static_assert(CfgGate::WTM == 1 && CfgGate::WTN == 4, "one 32-row tile of 4 gates per wave");
-  constexpr int PER = CfgGate::WTM * CfgGate::WTN * 16 * CfgGate::NTH;
-  constexpr int UPB = CfgGate::WAVES_N;
+  static_assert(CfgGateP::WTM == 1 && CfgGateP::WTN == 4, "one 32-row tile of 4 gates per wave");
+  constexpr int PER = CfgGateP::WTM * CfgGateP::WTN * 16 * CfgGateP::NTH;
+  constexpr int UPB = CfgGateP::WAVES_N;
   int l, t, b0;
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
   int tm, ug;
-  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+  if (!gate_tile((int)blockIdx.x - b0, (M + CfgGateP::BM - 1) / CfgGateP::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
     return;
   const int q = blockIdx.y, z = blockIdx.z, tid = threadIdx.x;
-  const float* base = part + ((int64_t)z * gridDim.x + blockIdx.x) * S * PER + 4 * (q * CfgGate::NTH + tid);
+  const float* base = part + ((int64_t)z * gridDim.x + blockIdx.x) * S * PER + 4 * (q * CfgGateP::NTH + tid);
   float4 a[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) a[g] = f4zero();
   for (int sp = 0; sp < S; ++sp)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const float4 v = ld4(base + (int64_t)sp * PER + 4 * (g * 4 * CfgGate::NTH));
+      const float4 v = ld4(base + (int64_t)sp * PER + 4 * (g * 4 * CfgGateP::NTH));
       a[g] = make_float4(a[g].x + v.x, a[g].y + v.y, a[g].z + v.z, a[g].w + v.w);
     }
   const float* th = theta + (int64_t)z * tstride;
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_cell_q(float* __restr
   float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * (4 * H);
   float* Cz = CsAll + (int64_t)l * lsz + slab * H;
   float* Hz = HsAll + (int64_t)l * lsz + slab * H;
-  const int rb = tm * CfgGate::BM + acc_row<CfgGate>(0, 0) + 8 * q;  // row of register 4q
+  const int rb = tm * CfgGateP::BM + acc_row<CfgGateP>(0, 0) + 8 * q;  // row of register 4q
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
   float cpv[4];
 #pragma unroll
@@ -584,23 +587,29 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     return;
   }
   {
+    // split-K over the small-grid tile (CfgGateP): its own block offsets per problem
+    const int ntmP = (w.M + CfgGateP::BM - 1) / CfgGateP::BM;
+    const int ngrpP = (d.H + 32 * CfgGateP::WAVES_N - 1) / (32 * CfgGateP::WAVES_N);
+    FwdWave wvP{};
+    fwd_wave(d, w, po, diag, gate_blocks(ntmP, ngrpP), false, wvP);
+    const dim3 gridP(wvP.off[wvP.n], 1, w.Z);
     int kmax = 0;
-    for (int q = 0; q < wv.n; ++q) kmax = std::max(kmax, wv.lo[q].cin + (wv.t[q] > 0 ? d.H : 0));
-    const int64_t per = (int64_t)grid.x * grid.z * CfgGate::NTH * CfgGate::WTM * CfgGate::WTN * 16;
-    const int S = small_grid_splits((int64_t)wv.n * ntm * ngrp * w.Z, kmax, CfgGate::BK, per, w.wpart_floats,
+    for (int q = 0; q < wvP.n; ++q) kmax = std::max(kmax, wvP.lo[q].cin + (wvP.t[q] > 0 ? d.H : 0));
+    const int64_t per = (int64_t)gridP.x * gridP.z * CfgGateP::NTH * CfgGateP::WTM * CfgGateP::WTN * 16;
+    const int S = small_grid_splits((int64_t)wvP.n * ntmP * ngrpP * w.Z, kmax, CfgGateP::BK, per, w.wpart_floats,
                                     w.kn.split_max);
     if (S > 1) {
       count_variant(w, V_FWD_SPLIT);
-      dim3 gp(grid.x, S, grid.z);
-      SMAML_DISPATCH_H(d.H, k_lstm_fwd_part<HT><<<gp, CfgGate::NTH, 0, s>>>(w.F, w.Hs, lsz, theta, tstride, wv,
-                                                                              d.T, w.M, S, w.wpart));
+      dim3 gp(gridP.x, S, gridP.z);
+      SMAML_DISPATCH_H(d.H, k_lstm_fwd_part<HT><<<gp, CfgGateP::NTH, 0, s>>>(w.F, w.Hs, lsz, theta, tstride, wvP,
+                                                                               d.T, w.M, S, w.wpart));
       if (SMAML_FWD_CELL_Q) {
-        dim3 gq(grid.x, 4, grid.z);
-        SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell_q<HT><<<gq, CfgGate::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
-                                                                                 wv, d.T, w.M, S, w.wpart));
+        dim3 gq(gridP.x, 4, gridP.z);
+        SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell_q<HT><<<gq, CfgGateP::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta,
+                                                                                  tstride, wvP, d.T, w.M, S, w.wpart));
       } else {
-        SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell<HT><<<grid, CfgGate::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta,
-                                                                                 tstride, wv, d.T, w.M, S, w.wpart));
+        SMAML_DISPATCH_H(d.H, k_lstm_fwd_cell<HT><<<gridP, CfgGateP::NTH, 0, s>>>(w.Hs, w.Cs, w.Gs, lsz, theta,
+                                                                                  tstride, wvP, d.T, w.M, S, w.wpart));
       }
       return;
     }
