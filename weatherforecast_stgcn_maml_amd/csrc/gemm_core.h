@@ -330,8 +330,11 @@ __device__ __forceinline__ void split4(const float4& v, uint2& p0, uint2& p1, ui
   p2 = make_uint2(q2[0], q2[1]);
 }
 
+#ifndef SMAML_DIAG_NOBSPLIT
+#define SMAML_DIAG_NOBSPLIT 0  // timing diagnostic only (wrong results): B tiles stored as one RNE piece
+#endif
 // Split this thread's staged float4s of one operand tile into the image at `img` (byte base).
-template <int ROWS, int F4, int NTH, bool KC, int BK>
+template <int ROWS, int F4, int NTH, bool KC, int BK, bool ONEPIECE = false>
 __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) {
   using I = X6Img<ROWS, KC, BK>;
   const int tid = threadIdx.x;
@@ -347,12 +350,69 @@ __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) 
       off = kk * I::RS + 8 * q;
     }
     uint2 p0, p1, p2;
-    split4(r[i], p0, p1, p2);
+    if (ONEPIECE) {
+      p0 = make_uint2(pk_bf16(r[i].x, r[i].y), pk_bf16(r[i].z, r[i].w));
+      p1 = p2 = make_uint2(0u, 0u);
+    } else {
+      split4(r[i], p0, p1, p2);
+    }
     *reinterpret_cast<uint2*>(img + off) = p0;
     *reinterpret_cast<uint2*>(img + I::PLANE + off) = p1;
     *reinterpret_cast<uint2*>(img + 2 * I::PLANE + off) = p2;
   }
 }
+
+// Operand loaders that deliver pre-split pieces (PieceMap): fetch_pieces fills, for each float4
+// position of fetch_tile's thread mapping, the 4 bf16 of each plane (uint2 per plane).
+template <class L, class = void>
+struct has_pieces : std::false_type {};
+template <class L>
+struct has_pieces<L, std::void_t<decltype(L::kPieces)>> : std::true_type {};
+
+template <int ROWS, int F4, int NTH, bool KC, int BK>
+__device__ __forceinline__ void store_pieces(char* img, const uint2 (&p)[3][F4]) {
+  using I = X6Img<ROWS, KC, BK>;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < F4; ++i) {
+    const int f = tid + NTH * i;
+    int off;
+    if (KC) {
+      const int rr = f / (BK / 4), q = f % (BK / 4);
+      off = rr * I::RS + 16 * ((q >> 1) ^ I::swz(rr)) + 8 * (q & 1);
+    } else {
+      const int kk = f / (ROWS / 4), q = f % (ROWS / 4);
+      off = kk * I::RS + 8 * q;
+    }
+    *reinterpret_cast<uint2*>(img + off) = p[0][i];
+    *reinterpret_cast<uint2*>(img + I::PLANE + off) = p[1][i];
+    *reinterpret_cast<uint2*>(img + 2 * I::PLANE + off) = p[2][i];
+  }
+}
+
+// B operand staging for the staged mainloops: f32 float4s (split at the store) or pieces.
+template <class C, class LB, bool P = has_pieces<LB>::value>
+struct BStage {
+  float4 r[C::B_F4];
+  __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0) {
+    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, k0, r);
+  }
+  template <bool ONE = false>
+  __device__ __forceinline__ void store(char* img) const {
+    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK, ONE>(img, r);
+  }
+};
+template <class C, class LB>
+struct BStage<C, LB, true> {
+  uint2 p[3][C::B_F4];
+  __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0) {
+    lb.template fetch_pieces<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(n0, k0, p);
+  }
+  template <bool ONE = false>
+  __device__ __forceinline__ void store(char* img) const {
+    store_pieces<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(img, p);
+  }
+};
 
 // The three pieces of the 32-row fragment at tile row `row` (this lane's row = row + (lane & 31)
 // for KC; the fragment's first row for MC), MFMA step s (k = 16s + 8h .. 16s + 8h + 7).
@@ -421,14 +481,15 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   char* st0 = reinterpret_cast<char*>(smem);
   const int nkt = (kend - kbeg + BKc - 1) / BKc;
   if (nkt <= 0) return;
-  float4 ra[C::A_F4], rb[C::B_F4];
+  float4 ra[C::A_F4];
+  BStage<C, LB> rb;
   auto store = [&](char* st) {
     if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra);
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
-    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(st + SA, rb);
+    rb.template store<SMAML_DIAG_NOBSPLIT != 0>(st + SA);
   };
   fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg, ra);
-  fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg, rb);
+  rb.fetch(lb, n0, kbeg);
   store(st0);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
@@ -436,7 +497,7 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
     const bool more = kt + 1 < nkt;
     if (more) {
       fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (kt + 1) * BKc, ra);
-      fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, kbeg + (kt + 1) * BKc, rb);
+      rb.fetch(lb, n0, kbeg + (kt + 1) * BKc);
     }
     const char* st = st0 + cur * C::X6S_STAGE;
     if constexpr (SMAML_X6S_MIDSTORE && C::WTN >= 2) {
@@ -467,8 +528,7 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
                                               int kend, Acc<C>& acc, float* smem, Hook& hook) {
   if constexpr (C::X6S) {
     gemm_mainloop_x6s<C, IG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
-    return;
-  }
+  } else {
   float* As = smem;
   float* Bs = smem + 2 * C::A_STAGE;
   constexpr int BKc = C::BK;
@@ -504,6 +564,7 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       store_tile<C::BN, C::LDB, C::B_F4, C::NTH, C::B_KC, BKc>(Bs + (cur ^ 1) * C::B_STAGE, rb);
     }
     __syncthreads();
+  }
   }
 }
 
@@ -664,18 +725,20 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
   if (nkt <= 0) return;
   const int wave = threadIdx.x >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
-  float4 ra[C::A_F4], ra2[C::A_F4], rb[C::B_F4], rb2[C::B_F4];
+  float4 ra[C::A_F4], ra2[C::A_F4];
+  BStage<C, LB> rb;
+  BStage<C, LB2> rb2;
   auto fetch = [&](int k0) {
     fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, k0, ra);
     if (k0 >= a2_kbeg) fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la2, m0, k0, ra2);
-    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb, n0, k0, rb);
-    fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(lb2, n0, k0, rb2);
+    rb.fetch(lb, n0, k0);
+    rb2.fetch(lb2, n0, k0);
   };
   auto store = [&](char* st, int k0) {
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
     if (k0 >= a2_kbeg) store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st + SA, ra2);
-    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(st + 2 * SA, rb);
-    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, BKc>(st + 2 * SA + SB, rb2);
+    rb.template store<SMAML_DIAG_NOBSPLIT != 0>(st + 2 * SA);
+    rb2.template store<SMAML_DIAG_NOBSPLIT != 0>(st + 2 * SA + SB);
   };
   auto mma = [&](const char* st, bool a2on) {
 #pragma unroll
@@ -737,8 +800,7 @@ __device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2,
                                                    float* smem) {
   if constexpr (C::X6S) {
     gemm_dual_mainloop_x6s<C, PRIMAL>(la, la2, lb, lb2, m0, n0, K, a2_kbeg, accp, acct, smem);
-    return;
-  }
+  } else {
   constexpr int BKc = C::BK;
   constexpr int SA = C::A_STAGE, SB = C::B_STAGE;
   constexpr int STAGE = 2 * SA + 2 * SB;
@@ -783,6 +845,7 @@ __device__ __forceinline__ void gemm_dual_mainloop(const LA& la, const LA2& la2,
 #endif
     if (more) store(smem + (cur ^ 1) * STAGE, k0 + BKc);
     __syncthreads();
+  }
   }
 }
 

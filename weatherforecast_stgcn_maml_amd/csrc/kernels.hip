@@ -314,8 +314,13 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   } else {
     const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
-    const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
-    gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+    if constexpr (CfgGate::X6S && SMAML_PIECES) {
+      gemm_mainloop<CfgGate>(la, gate_bx<2>(wv.pm, {th + lo.wih, th + lo.whh}, {cin, H}, H), m0, n0, 0,
+                             cin + (t > 0 ? H : 0), acc, smem);
+    } else {
+      const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
+      gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+    }
   }
 
   fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
@@ -340,6 +345,7 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
     fl += 2.0 * w.Z * w.M * 4 * d.H * (dual ? k1 + k2 : k1);
   }
   wv.n = n;
+  wv.pm = w.pm;
   wv.off[n] = off;
   for (int q = n + 1; q <= MAX_LAYERS; ++q) wv.off[q] = off;
   return fl;
@@ -937,6 +943,7 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
     fl += (dual ? 3.0 : 1.0) * 2.0 * w.Z * w.M * 4 * d.H * d.H * segs;
   }
   wv.n = n;
+  wv.pm = w.pm;
   for (int q = n; q <= MAX_LAYERS; ++q) wv.off[q] = off;
   return fl;
 }
@@ -1113,9 +1120,15 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
       // dG cell (bwd_block) stream it in the same half of their K loops
       const bool sw = wv.pair && (l & 1) && up && nx;
       const SegKCt<2> la{{sw ? pn : (up ? pa : pn), sw ? pa : pn}, {G4, G4}, M};
-      const SegMCt<2> lb{{sw ? th + lo.whh : (up ? th + wih_up : th + lo.whh), sw ? th + wih_up : th + lo.whh},
-                         {G4, G4}, H};
-      if (ns && SMAML_DIAG_BWD != 2) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
+      const float* b0 = sw ? th + lo.whh : (up ? th + wih_up : th + lo.whh);
+      const float* b1 = sw ? th + wih_up : th + lo.whh;
+      if constexpr (CfgNN::X6S && SMAML_PIECES) {
+        if (ns && SMAML_DIAG_BWD != 2)
+          gemm_mainloop<CfgNN>(la, mc_bx<2>(wv.pm, {b0, b1}, {G4, G4}, H), m0, n0, 0, ns * G4, acc, smem);
+      } else {
+        const SegMCt<2> lb{{b0, b1}, {G4, G4}, H};
+        if (ns && SMAML_DIAG_BWD != 2) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
+      }
     }
   }
   if (SMAML_DIAG_BWD == 1) {  // timing diagnostic: GEMM phase only (keep the result live)
@@ -1956,6 +1969,33 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
 }  // namespace smaml
 
 namespace smaml {
+__global__ __launch_bounds__(256) void k_split3(const float* __restrict__ x, int64_t n, int64_t plane,
+                                                uint16_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (4 * i + 3 < n) {
+    uint2 p0, p1, p2;
+    split4(ld4(x + 4 * i), p0, p1, p2);
+    *reinterpret_cast<uint2*>(dst + 4 * i) = p0;
+    *reinterpret_cast<uint2*>(dst + plane + 4 * i) = p1;
+    *reinterpret_cast<uint2*>(dst + 2 * plane + 4 * i) = p2;
+  } else {
+    for (int64_t e = 4 * i; e < n; ++e) {
+      const float v = x[e];
+      const uint32_t u0 = pk_bf16(v, 0.f);
+      const float r = v - __builtin_bit_cast(float, u0 << 16);
+      const uint32_t u1 = pk_bf16(r, 0.f);
+      const float q = r - __builtin_bit_cast(float, u1 << 16);
+      dst[e] = (uint16_t)u0;
+      dst[plane + e] = (uint16_t)u1;
+      dst[2 * plane + e] = (uint16_t)pk_bf16(q, 0.f);
+    }
+  }
+}
+void launch_split3(hipStream_t s, const float* x, int64_t n, int64_t plane, uint16_t* dst) {
+  const int64_t blocks = (n + 4 * 256 - 1) / (4 * 256);
+  k_split3<<<dim3((unsigned)blocks), 256, 0, s>>>(x, n, plane, dst);
+}
+
 // Product form per GEMM family as built (smaml_build_info): 0 = f32 MFMA, 1 = bf16x6 with the
 // split on the MFMA fragments, 2 = bf16x6 with the split staged at the LDS store.
 template <class C>

@@ -166,6 +166,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
+    else if constexpr (CfgGateD::X6S && SMAML_PIECES)
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
+                                          gate_bx<2>(wv.pm, {th + lo.wih, th + lo.whh}, {cin, wh}, H), m0, n0, 0,
+                                          cin + wh, ap, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
                                           SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, 0,
@@ -204,6 +208,11 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+    else if constexpr (CfgGateD::X6S && SMAML_PIECES)
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
+                                          gate_bx<4>(wv.pm, {u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
+                                                     {cin, wh, wrx, wh}, H),
+                                          m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
                                           SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
@@ -547,9 +556,16 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
       const float* a1 = sw ? dGAll + oa : dGz + on;
       const float* r1 = sw ? RGsAll + oa : RGz + on;
       const int64_t w0o = up && !sw ? wih_up : lo.whh, w1o = sw ? wih_up : lo.whh;
-      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, a1}, {G4, G4}, M}, SegKCt<2>{{r0, r1}, {G4, G4}, M},
-                                        SegMCt<2>{{th + w0o, th + w1o}, {G4, G4}, H},
-                                        SegMCt<2>{{u + w0o, u + w1o}, {G4, G4}, H}, m0, n0, ns * G4, 0, ap, at, smem);
+      if constexpr (CfgNND::X6S && SMAML_PIECES)
+        gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, a1}, {G4, G4}, M}, SegKCt<2>{{r0, r1}, {G4, G4}, M},
+                                          mc_bx<2>(wv.pm, {th + w0o, th + w1o}, {G4, G4}, H),
+                                          mc_bx<2>(wv.pm, {u + w0o, u + w1o}, {G4, G4}, H), m0, n0, ns * G4, 0, ap,
+                                          at, smem);
+      else
+        gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, a1}, {G4, G4}, M}, SegKCt<2>{{r0, r1}, {G4, G4}, M},
+                                          SegMCt<2>{{th + w0o, th + w1o}, {G4, G4}, H},
+                                          SegMCt<2>{{u + w0o, u + w1o}, {G4, G4}, H}, m0, n0, ns * G4, 0, ap, at,
+                                          smem);
     }
   }
   const bool first = (t == T - 1);

@@ -5,6 +5,7 @@
 // tangent GEMMs of the second-order path) are expressed.
 #pragma once
 #include "gemm_core.h"
+#include "kernels.h"
 
 // Product form per GEMM family (gemm_core.h GemmCfg X6_: 1 = f32-accurate bf16x6 on the bf16 MFMA
 // pipe, 0 = v_mfma_f32_32x32x2_f32); A/B-able at build time, default SMAML_X6.
@@ -307,6 +308,105 @@ struct SegGateBt {
     }
   }
 };
+
+// ---- pre-split parameter operands (PieceMap, staged split) ------------------------------------
+// The same element mapping as SegGateBt / SegMCt, reading the three bf16 planes of each segment
+// (q[s] = plane-0 piece of the segment's first element, ps[s] = plane stride) instead of floats.
+__device__ __forceinline__ uint2 ldp(const uint16_t* base, uint32_t elem) {
+  return *reinterpret_cast<const uint2*>(base + elem);
+}
+template <int NS>
+struct SegGateBx {
+  static constexpr bool kPieces = true;
+  const uint16_t* q[NS];
+  int64_t ps[NS];
+  int w[NS];
+  int H;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch_pieces(int n0, int k0, uint2 (&r)[3][F4]) const {
+    static_assert(KC, "SegGateBx is a k-contiguous operand");
+    const uint16_t* b = q[0];
+    int64_t st = ps[0];
+    int ws = w[0], kk = k0;
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
+      if (kk >= ws) {
+        kk -= ws;
+        b = q[s];
+        st = ps[s];
+        ws = w[s];
+      }
+    b += kk;
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int n = n0 + f / (BK / 4);
+      const int ug = n >> 7, rem = n & 127;
+      const int j = min(ug * 32 + (rem & 31), H - 1);
+      const uint32_t e = (uint32_t)(((rem >> 5) * H + j) * ws + 4 * (f % (BK / 4)));
+      r[0][i] = ldp(b, e);
+      r[1][i] = ldp(b + st, e);
+      r[2][i] = ldp(b + 2 * st, e);
+    }
+  }
+};
+template <int NS>
+struct SegMCx {
+  static constexpr bool kPieces = true;
+  const uint16_t* q[NS];
+  int64_t ps[NS];
+  int K[NS];
+  int cols;
+  template <int ROWS, int F4, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch_pieces(int col0, int k0, uint2 (&r)[3][F4]) const {
+    static_assert(!KC, "SegMCx is an n-contiguous operand");
+    const uint16_t* b = q[0];
+    int64_t st = ps[0];
+    int ks = K[0], kk = k0;
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
+      if (kk >= ks) {
+        kk -= ks;
+        b = q[s];
+        st = ps[s];
+        ks = K[s];
+      }
+    b += (int64_t)kk * cols;
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int f = (int)threadIdx.x + NTH * i;
+      const int c = min(col0 + 4 * (f % (ROWS / 4)), cols - 4);
+      const uint32_t e = (uint32_t)((f / (ROWS / 4)) * cols + c);
+      r[0][i] = ldp(b, e);
+      r[1][i] = ldp(b + st, e);
+      r[2][i] = ldp(b + 2 * st, e);
+    }
+  }
+};
+template <int NS>
+__device__ __forceinline__ SegGateBx<NS> gate_bx(const PieceMap& pm, const float* const (&p)[NS], const int (&w)[NS],
+                                                 int H) {
+  SegGateBx<NS> r;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    r.q[s] = pm.find(p[s], r.ps[s]);
+    r.w[s] = w[s];
+  }
+  r.H = H;
+  return r;
+}
+template <int NS>
+__device__ __forceinline__ SegMCx<NS> mc_bx(const PieceMap& pm, const float* const (&p)[NS], const int (&K)[NS],
+                                            int cols) {
+  SegMCx<NS> r;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    r.q[s] = pm.find(p[s], r.ps[s]);
+    r.K[s] = K[s];
+  }
+  r.cols = cols;
+  return r;
+}
 
 // MC operand [K][cols] (cols contiguous) with zero rows at k >= K (split-K weight gradients: the
 // K tail is real, so it is zero-filled by a select, not clamped).
