@@ -29,6 +29,14 @@ def test_library_exports_every_header_symbol():
     assert L.smaml_abi_version() == _capi.ABI_VERSION
 
 
+def test_build_info_reports_every_gemm_family():
+    """smaml_build_info (host-only): the product form of each GEMM family of this build
+    (0 = f32 MFMA, 1 = bf16x6 fragment split, 2 = bf16x6 staged split)."""
+    forms = _capi.product_forms()
+    assert set(forms) == {"gcn", "gate", "gate_dual", "bptt", "bptt_dual", "wgrad"}
+    assert all(v in (0, 1, 2) for v in forms.values())
+
+
 @pytest.mark.parametrize("d", [CONFIG1, CONFIG2])
 def test_param_layout_matches_state_dict(d):
     lay, total = params.trainable_layout(d)
