@@ -316,7 +316,7 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   parts.push_back({(void**)&w.pred, seq * d.HfC * 4});
   parts.push_back({(void**)&w.dpred, seq * d.HfC * 4});
   parts.push_back({(void**)&w.wpart, wpart * 4});
-  const int64_t pcap = SMAML_PIECES ? (int64_t)zc * c->po.P + 4 : 4;  // parameter pieces (split_params)
+  const int64_t pcap = SMAML_PIECES ? (int64_t)zc * c->po.P + 8 : 8;  // parameter pieces (split_params)
   parts.push_back({(void**)&w.pcs_buf[0], 3 * pcap * 2});
   parts.push_back({(void**)&w.pcs_buf[1], 3 * pcap * 2});
   parts.push_back({(void**)&w.lpart, lblk * 4});
@@ -598,7 +598,7 @@ int split_params(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   if (!SMAML_PIECES) return SMAML_OK;
   Work& w = c->w;
   const int64_t span = tstride > 0 ? (int64_t)(w.Z - 1) * tstride + c->po.P : c->po.P;
-  const int64_t plane = (span + 3) / 4 * 4;
+  const int64_t plane = (span + 7) / 8 * 8;  // 16-B aligned planes (8-element piece loads)
   if (plane > w.pcs_cap) return fail(SMAML_EINVAL, "split_params: parameter span exceeds the reserved pieces");
   const float* src[2] = {theta, U};
   for (int i = 0; i < 2; ++i) {

@@ -281,8 +281,7 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
       for (int i = 0; i < C::WTM; ++i) acc.v[i][j] = mfma_x6(a[i], b, acc.v[i][j]);
     }
   }
-  return;
-  }
+  } else {
 #pragma unroll
   for (int q = 0; q < C::BK / 8; ++q) {
     float4 a[C::WTM], b[C::WTN];
@@ -299,6 +298,7 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
 #pragma unroll
         for (int j = 0; j < C::WTN; ++j)
           acc.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a[i], e), f4get(b[j], e), acc.v[i][j], 0, 0, 0);
+  }
   }
 }
 
@@ -362,31 +362,39 @@ __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) 
   }
 }
 
-// Operand loaders that deliver pre-split pieces (PieceMap): fetch_pieces fills, for each float4
-// position of fetch_tile's thread mapping, the 4 bf16 of each plane (uint2 per plane).
+// Operand loaders that deliver pre-split pieces (PieceMap): fetch_pieces fills, per item of 8
+// consecutive elements along the tile's contiguous axis (KC: 8 k of one row; MC: 8 rows of one k),
+// one 16-B piece vector per plane; items are dealt to threads tid, tid + NTH, ... (threads past the
+// tile's item count idle: whole waves, since the item counts are multiples of 64).
 template <class L, class = void>
 struct has_pieces : std::false_type {};
 template <class L>
 struct has_pieces<L, std::void_t<decltype(L::kPieces)>> : std::true_type {};
 
-template <int ROWS, int F4, int NTH, bool KC, int BK>
-__device__ __forceinline__ void store_pieces(char* img, const uint2 (&p)[3][F4]) {
+template <int ROWS, int BK>
+struct PieceItems {
+  static constexpr int ITEMS = ROWS * BK / 8;
+};
+
+template <int ROWS, int PI, int NTH, bool KC, int BK>
+__device__ __forceinline__ void store_pieces(char* img, const uint4 (&p)[3][PI]) {
   using I = X6Img<ROWS, KC, BK>;
-  const int tid = threadIdx.x;
+  constexpr int ITEMS = PieceItems<ROWS, BK>::ITEMS;
 #pragma unroll
-  for (int i = 0; i < F4; ++i) {
-    const int f = tid + NTH * i;
+  for (int i = 0; i < PI; ++i) {
+    const int f = (int)threadIdx.x + NTH * i;
+    if (ITEMS % NTH != 0 && f >= ITEMS) break;
     int off;
     if (KC) {
-      const int rr = f / (BK / 4), q = f % (BK / 4);
-      off = rr * I::RS + 16 * ((q >> 1) ^ I::swz(rr)) + 8 * (q & 1);
+      const int rr = f / (BK / 8), c = f % (BK / 8);
+      off = rr * I::RS + 16 * (c ^ I::swz(rr));
     } else {
-      const int kk = f / (ROWS / 4), q = f % (ROWS / 4);
-      off = kk * I::RS + 8 * q;
+      const int kk = f / (ROWS / 8), g = f % (ROWS / 8);
+      off = kk * I::RS + 16 * g;
     }
-    *reinterpret_cast<uint2*>(img + off) = p[0][i];
-    *reinterpret_cast<uint2*>(img + I::PLANE + off) = p[1][i];
-    *reinterpret_cast<uint2*>(img + 2 * I::PLANE + off) = p[2][i];
+    *reinterpret_cast<uint4*>(img + off) = p[0][i];
+    *reinterpret_cast<uint4*>(img + I::PLANE + off) = p[1][i];
+    *reinterpret_cast<uint4*>(img + 2 * I::PLANE + off) = p[2][i];
   }
 }
 
@@ -404,13 +412,15 @@ struct BStage {
 };
 template <class C, class LB>
 struct BStage<C, LB, true> {
-  uint2 p[3][C::B_F4];
+  static constexpr int PI = (PieceItems<C::BN, C::BK>::ITEMS + C::NTH - 1) / C::NTH;
+  static_assert(PieceItems<C::BN, C::BK>::ITEMS % 64 == 0, "piece items: whole waves");
+  uint4 p[3][PI];
   __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0) {
-    lb.template fetch_pieces<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(n0, k0, p);
+    lb.template fetch_pieces<C::BN, PI, C::NTH, C::B_KC, C::BK>(n0, k0, p);
   }
   template <bool ONE = false>
   __device__ __forceinline__ void store(char* img) const {
-    store_pieces<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(img, p);
+    store_pieces<C::BN, PI, C::NTH, C::B_KC, C::BK>(img, p);
   }
 };
 
@@ -679,8 +689,7 @@ __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, in
       }
     }
   }
-  return;
-  }
+  } else {
 #pragma unroll
   for (int q = 0; q < BKc / 8; ++q) {
     float4 a[C::WTM], a2[C::WTM], b[C::WTN], b2[C::WTN];
@@ -706,6 +715,7 @@ __device__ __forceinline__ void dual_mma(const float* st, int arow, int brow, in
           if (A2)
             acct.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(a2[i], e), f4get(b[j], e), acct.v[i][j], 0, 0, 0);
         }
+  }
   }
 }
 

@@ -311,9 +311,10 @@ struct SegGateBt {
 
 // ---- pre-split parameter operands (PieceMap, staged split) ------------------------------------
 // The same element mapping as SegGateBt / SegMCt, reading the three bf16 planes of each segment
-// (q[s] = plane-0 piece of the segment's first element, ps[s] = plane stride) instead of floats.
-__device__ __forceinline__ uint2 ldp(const uint16_t* base, uint32_t elem) {
-  return *reinterpret_cast<const uint2*>(base + elem);
+// (q[s] = plane-0 piece of the segment's first element, ps[s] = plane stride) in items of 8
+// consecutive elements (one 16-B load per plane; gemm_core.h store_pieces).
+__device__ __forceinline__ uint4 ldp(const uint16_t* base, uint32_t elem) {
+  return *reinterpret_cast<const uint4*>(base + elem);
 }
 template <int NS>
 struct SegGateBx {
@@ -322,9 +323,10 @@ struct SegGateBx {
   int64_t ps[NS];
   int w[NS];
   int H;
-  template <int ROWS, int F4, int NTH, bool KC, int BK>
-  __device__ __forceinline__ void fetch_pieces(int n0, int k0, uint2 (&r)[3][F4]) const {
+  template <int ROWS, int PI, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch_pieces(int n0, int k0, uint4 (&r)[3][PI]) const {
     static_assert(KC, "SegGateBx is a k-contiguous operand");
+    constexpr int ITEMS = ROWS * BK / 8;
     const uint16_t* b = q[0];
     int64_t st = ps[0];
     int ws = w[0], kk = k0;
@@ -338,12 +340,13 @@ struct SegGateBx {
       }
     b += kk;
 #pragma unroll
-    for (int i = 0; i < F4; ++i) {
+    for (int i = 0; i < PI; ++i) {
       const int f = (int)threadIdx.x + NTH * i;
-      const int n = n0 + f / (BK / 4);
+      if (ITEMS % NTH != 0 && f >= ITEMS) break;
+      const int n = n0 + f / (BK / 8);
       const int ug = n >> 7, rem = n & 127;
       const int j = min(ug * 32 + (rem & 31), H - 1);
-      const uint32_t e = (uint32_t)(((rem >> 5) * H + j) * ws + 4 * (f % (BK / 4)));
+      const uint32_t e = (uint32_t)(((rem >> 5) * H + j) * ws + 8 * (f % (BK / 8)));
       r[0][i] = ldp(b, e);
       r[1][i] = ldp(b + st, e);
       r[2][i] = ldp(b + 2 * st, e);
@@ -357,9 +360,10 @@ struct SegMCx {
   int64_t ps[NS];
   int K[NS];
   int cols;
-  template <int ROWS, int F4, int NTH, bool KC, int BK>
-  __device__ __forceinline__ void fetch_pieces(int col0, int k0, uint2 (&r)[3][F4]) const {
+  template <int ROWS, int PI, int NTH, bool KC, int BK>
+  __device__ __forceinline__ void fetch_pieces(int col0, int k0, uint4 (&r)[3][PI]) const {
     static_assert(!KC, "SegMCx is an n-contiguous operand");
+    constexpr int ITEMS = ROWS * BK / 8;
     const uint16_t* b = q[0];
     int64_t st = ps[0];
     int ks = K[0], kk = k0;
@@ -373,10 +377,11 @@ struct SegMCx {
       }
     b += (int64_t)kk * cols;
 #pragma unroll
-    for (int i = 0; i < F4; ++i) {
+    for (int i = 0; i < PI; ++i) {
       const int f = (int)threadIdx.x + NTH * i;
-      const int c = min(col0 + 4 * (f % (ROWS / 4)), cols - 4);
-      const uint32_t e = (uint32_t)((f / (ROWS / 4)) * cols + c);
+      if (ITEMS % NTH != 0 && f >= ITEMS) break;
+      const int c = min(col0 + 8 * (f % (ROWS / 8)), cols - 8);
+      const uint32_t e = (uint32_t)((f / (ROWS / 8)) * cols + c);
       r[0][i] = ldp(b, e);
       r[1][i] = ldp(b + st, e);
       r[2][i] = ldp(b + 2 * st, e);
