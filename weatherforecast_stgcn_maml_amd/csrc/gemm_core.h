@@ -79,8 +79,10 @@ struct X6Img {
   }
 };
 
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32, int X6_ = SMAML_X6>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32, int X6_ = SMAML_X6,
+          int NST_ = 2>
 struct GemmCfg {
+  static constexpr int X6S_NST = NST_;  // staged split: LDS stages (1 = register prefetch, two barriers)
   static constexpr int BK = BK_;
   // products: 0 = v_mfma_f32_32x32x2_f32; 1 = bf16x6 with the split on the MFMA fragments (mma_tile);
   // 2 = bf16x6 with the split done once per element at the LDS store (gemm_mainloop, "staged")
@@ -108,7 +110,9 @@ struct GemmCfg {
   using AImg = X6Img<BM, A_KC, BK>;
   using BImg = X6Img<BN, B_KC, BK>;
   static constexpr int X6S_STAGE = AImg::BYTES + BImg::BYTES;  // bytes per staged-split stage
-  static constexpr int SMEM_FLOATS = (X6S && X6S_STAGE / 2 > A_STAGE + B_STAGE) ? X6S_STAGE / 2 : 2 * (A_STAGE + B_STAGE);
+  static constexpr int SMEM_FLOATS = (X6S && NST_ * X6S_STAGE / 4 > 2 * (A_STAGE + B_STAGE))
+                                        ? NST_ * X6S_STAGE / 4
+                                        : 2 * (A_STAGE + B_STAGE);
 };
 
 // Loaders that fetch a whole operand tile themselves (``kTileFetch``; loaders.h "tile
@@ -509,8 +513,20 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
       fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (kt + 1) * BKc, ra);
       rb.fetch(lb, n0, kbeg + (kt + 1) * BKc);
     }
-    const char* st = st0 + cur * C::X6S_STAGE;
-    if constexpr (SMAML_X6S_MIDSTORE && C::WTN >= 2) {
+    const char* st = st0 + (C::X6S_NST == 1 ? 0 : cur * C::X6S_STAGE);
+    if constexpr (C::X6S_NST == 1) {
+#if SMAML_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+      mma_tile_x6s<C, IG>(st, st + SA, acc);
+#if SMAML_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      if (more) {
+        __syncthreads();  // every wave has read the stage
+        store(st0);
+      }
+    } else if constexpr (SMAML_X6S_MIDSTORE && C::WTN >= 2) {
       // the next tile's split + LDS stores between the two halves of this tile's MFMAs (the
       // other stage), so a SIMD's waves overlap them with MFMAs instead of meeting at the barrier
       constexpr int JH = C::WTN / 2;

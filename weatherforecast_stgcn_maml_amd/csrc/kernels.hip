@@ -25,7 +25,8 @@ using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, 
 // fused step uses (config 4 A/B with the bf16x6 products: 256-row 1.137 -> 128-row 1.031 ms per sample-step)
 using CfgGateP = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;
 using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK, SMAML_X6_BWD>;  // C = A . B   (B n-contiguous)
-using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK, SMAML_X6_WGRAD>;  // C = A^T . B (split-K weight grads)
+using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK, SMAML_X6_WGRAD,
+                      SMAML_TN_NST>;  // C = A^T . B (split-K weight grads)
 
 // ------------------------------------------------------------------------------------
 // Block-wide deterministic sum (fixed shuffle tree + fixed wave order).

@@ -70,6 +70,9 @@
 #define SMAML_EPI_PRELOAD_FWD 1  // fused forward step: load a tile's c_{t-1} before its stores
                                  // (r01 A/B: 339 -> 335.5 ms per meta-step)
 #endif
+#ifndef SMAML_TN_NST
+#define SMAML_TN_NST 2  // weight-gradient staged-split LDS stages
+#endif
 #ifndef SMAML_TN_BK
 #define SMAML_TN_BK 16
 #endif
