@@ -1,10 +1,10 @@
 #!/bin/bash
-# bf16x6 (SMAML_X6) variant: parity subset with the variant library, then bench A/B against the f32-MFMA build.
+# Parity subset with a candidate library (X6_LIB), then a bench A/B against libsmaml.so (the first A/B of the bf16x6 build).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-X6=${X6_LIB:-libsmaml_x6.so}
+X6=${X6_LIB:-libsmaml.so}
 SMAML_LIB=weatherforecast_stgcn_maml_amd/$X6 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
   -m gpu ${X6_TESTS:-tests/test_gpu_parity.py} > gpurun_out/x6_pytest.log 2>&1
 rc=$?
