@@ -924,7 +924,8 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
 // 64x64 tiles for small grids (few tasks per rank) so the launch fills the chip.
 using CfgNNs = GemmCfg<64, 64, 2, 2, true, false, SMAML_NN_BK, SMAML_X6_BWD>;
 // BPTT step tile (A/B-able at build time): rows x 128 units, waves WM x WN
-using CfgBwd = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_NN_BK, SMAML_X6_BWD>;
+using CfgBwd = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_NN_BK, SMAML_X6_BWD,
+                       SMAML_BWD_NST>;
 
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv) {
@@ -970,7 +971,8 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
 #endif
 template <class C>
 constexpr int epi_smem_floats() {
-  return C::SMEM_FLOATS > C::BM * C::BN ? C::SMEM_FLOATS : C::BM * C::BN;
+  constexpr int E = SMAML_BWD_HALFEPI ? C::BM * C::BN / 2 : C::BM * C::BN;
+  return C::SMEM_FLOATS > E ? C::SMEM_FLOATS : E;
 }
 
 
@@ -1064,11 +1066,25 @@ __device__ __forceinline__ void bwd_cell(const Acc<CfgNN>& acc, float* smem, con
                                          float* __restrict__ dhz, const float* __restrict__ Cz,
                                          const float* __restrict__ dHz, float* __restrict__ dcz, int m0, int n0,
                                          int t, int T, int M) {
-  acc_to_lds<CfgNN>(acc, smem);
-  if (m0 + CfgNN::BM <= M && n0 + CfgNN::BN <= H)  // all but the last row tile: no bounds checks
-    bwd_cell_<H, CfgNN, HEAD, false>(smem, Gz, dGz, dhz, Cz, dHz, dcz, m0, n0, t, T, M);
-  else
-    bwd_cell_<H, CfgNN, HEAD, true>(smem, Gz, dGz, dhz, Cz, dHz, dcz, m0, n0, t, T, M);
+  if constexpr (SMAML_BWD_HALFEPI) {
+    using HC = HalfRows<CfgNN>;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      if (h) __syncthreads();  // the first half's readers are done with the LDS
+      acc_to_lds_half<CfgNN>(acc, smem, h);
+      const int mh = m0 + h * HC::BM;
+      if (mh + HC::BM <= M && n0 + HC::BN <= H)
+        bwd_cell_<H, HC, HEAD, false>(smem, Gz, dGz, dhz, Cz, dHz, dcz, mh, n0, t, T, M);
+      else
+        bwd_cell_<H, HC, HEAD, true>(smem, Gz, dGz, dhz, Cz, dHz, dcz, mh, n0, t, T, M);
+    }
+  } else {
+    acc_to_lds<CfgNN>(acc, smem);
+    if (m0 + CfgNN::BM <= M && n0 + CfgNN::BN <= H)  // all but the last row tile: no bounds checks
+      bwd_cell_<H, CfgNN, HEAD, false>(smem, Gz, dGz, dhz, Cz, dHz, dcz, m0, n0, t, T, M);
+    else
+      bwd_cell_<H, CfgNN, HEAD, true>(smem, Gz, dGz, dhz, Cz, dHz, dcz, m0, n0, t, T, M);
+  }
 }
 
 // GsAll: gates in; dGAll: dG out (== GsAll: in place) and the neighbours' dG read by the GEMM;

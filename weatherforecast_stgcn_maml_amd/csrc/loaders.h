@@ -50,6 +50,14 @@
                           // the larger wave tile halves the fragment splits per MFMA; A/B 64 -> 128: bwd 316 -> 278,
                           // tangent bwd 472 -> 429 ms per meta-step)
 #endif
+// Primal BPTT LDS diet (bf16x6 build): one staged-split LDS stage and the epilogue's transpose in two
+// row halves, 64 KB -> 37 KB per workgroup (2 -> 3 workgroups per CU): A/B bwd 256 -> 244 ms.
+#ifndef SMAML_BWD_NST
+#define SMAML_BWD_NST (SMAML_X6 ? 1 : 2)  // primal BPTT staged-split LDS stages
+#endif
+#ifndef SMAML_BWD_HALFEPI
+#define SMAML_BWD_HALFEPI (SMAML_X6 ? 1 : 0)  // primal BPTT epilogue in two row halves (BM*BN/2 floats of LDS)
+#endif
 #ifndef SMAML_BWD_WM
 #define SMAML_BWD_WM 2
 #endif
@@ -689,6 +697,29 @@ __device__ __forceinline__ void acc_to_lds(const Acc<C>& acc, float* smem) {
     }
   __syncthreads();
 }
+
+// Half of the tile (rows [h*BM/2, (h+1)*BM/2)) -> smem [BM/2][BN]: written by the waves that own
+// those rows (WAVES_M == 2); ends with a barrier. Lets an epilogue run in two halves over BM*BN/2 floats.
+template <class C>
+__device__ __forceinline__ void acc_to_lds_half(const Acc<C>& acc, float* smem, int h) {
+  static_assert(C::WAVES_M == 2, "one row half per wave row");
+  const int wm = (int)(threadIdx.x >> 6) / C::WAVES_N;
+  if (wm == h) {
+#pragma unroll
+    for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < C::WTN; ++jj) {
+        const int col = acc_col<C>(jj);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) smem[(acc_row<C>(i, r) - h * (C::BM / 2)) * C::BN + col] = acc.v[i][jj][r];
+      }
+  }
+  __syncthreads();
+}
+template <class C>
+struct HalfRows {  // the epilogue's view of one row half of C's tile
+  static constexpr int BM = C::BM / 2, BN = C::BN, NTH = C::NTH;
+};
 
 __device__ __forceinline__ float4 sel4(bool c, float4 a) { return c ? a : f4zero(); }
 
