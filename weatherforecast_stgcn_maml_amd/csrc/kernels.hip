@@ -20,7 +20,8 @@
 namespace smaml {
 
 using CfgNT = GemmCfg<128, 128, 2, 2, true, true, 32, SMAML_X6_BWD>;    // C = A . B^T (both k-contiguous)
-using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;  // LSTM forward: wave = 32 rows x 4 gates
+using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE,
+                        SMAML_GATE_NST>;  // LSTM forward: wave = 32 rows x 4 gates
 // split-K gate step of small grids (k_lstm_fwd_part / _cell / _cell_q): 128-row tiles whatever the
 // fused step uses (config 4 A/B with the bf16x6 products: 256-row 1.137 -> 128-row 1.031 ms per sample-step)
 using CfgGateP = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;

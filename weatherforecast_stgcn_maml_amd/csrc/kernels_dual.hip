@@ -20,7 +20,8 @@ namespace smaml {
 #endif
 // The BPTT / dX / head duals stage four operand tiles per K-tile (gemm_dual_mainloop);
 // BK=16 keeps them at 54-80 KiB of LDS (two or more workgroups per CU).
-using CfgGateD = GemmCfg<32 * SMAML_GATED_WM, 128 * SMAML_GATE_WN, SMAML_GATED_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATED>;
+using CfgGateD = GemmCfg<32 * SMAML_GATED_WM, 128 * SMAML_GATE_WN, SMAML_GATED_WM, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATED,
+                         SMAML_GATE_NST>;
 using CfgNTD = GemmCfg<128, 128, 2, 2, true, true, SMAML_DUAL_BK, SMAML_X6_BWDD>;
 using CfgNND = GemmCfg<64, 128, 2, 2, true, false, SMAML_DUAL_BK, SMAML_X6_BWDD>;
 

@@ -39,6 +39,9 @@
 #define SMAML_GATE_WM (SMAML_X6 ? 8 : 4)  // gate GEMM row waves (32 rows each): 4 -> 128-row tiles, 8 -> 256-row tiles
                                           // (staged split: the B tile's split is shared by 256 rows; 2 WGs/CU)
 #endif
+#ifndef SMAML_GATE_NST
+#define SMAML_GATE_NST 2  // gate GEMMs' staged-split LDS stages
+#endif
 #ifndef SMAML_GATED_WM
 #define SMAML_GATED_WM (SMAML_X6 ? 8 : 4)  // same, for the tangent (dual) gate kernel
 #endif
