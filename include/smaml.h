@@ -249,15 +249,14 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
 
 /* Run-time knobs (tests / A-B; defaults = build-time values):
  *   "bwd_big_min", "bwdd_big_min": primal / tangent BPTT launches with at least this many
- *                                  64x128 tiles use them (else 64x64 or split-K tiles);
+ *                                  64-row tile units use the 128x128 tiles (else 64x64 or
+ *                                  split-K tiles);
  *   "split_max":                   split-K ways of small-grid LSTM steps (1 = off);
  *   "keep":                        cap on second-order inner steps whose primal is kept
  *                                  (-1 = the SMAML_KEEP environment variable / all that fit);
  *   "wgrad_group_max_rows":        a backward with tasks x rows <= this runs all LSTM weight
  *                                  gradients as one launch after the BPTT (batch-1 adaptation);
- *   "wgrad_group_wgs":             workgroups that grouped launch aims for;
- *   "bwd_pair":                    1 = big-tile BPTT launches deal row tiles so that the two
- *                                  readers of each dG cell run on one XCD together (0 = off). */
+ *   "wgrad_group_wgs":             workgroups that grouped launch aims for. */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

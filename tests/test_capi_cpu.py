@@ -127,6 +127,25 @@ def test_window_table_reference_schedule():
         assert reference_query_start(n) >= K * B and n - reference_query_start(n) >= B
 
 
+def test_query_start_never_inside_the_support_samples():
+    """a short stream (or S > 450) would put the reference split's query batch inside
+    the S support samples; query_starts moves it to S, or raises when the stream is too short."""
+    from weatherforecast_stgcn_maml_amd.maml import query_starts, reference_query_start
+    cfg = MamlConfig(inner_steps=2, batch=2)  # S = 4
+    assert query_starts(cfg, [600, 20, 6]) == [450, 15, 4]   # 20 -> reference split; 6 -> clamped to S
+    assert reference_query_start(6) == 4 and reference_query_start(5) == 3
+    assert query_starts(cfg, [7]) == [5]
+    with pytest.raises(ValueError):
+        query_starts(cfg, [5])                               # 4 support + 2 query samples do not fit
+    big = MamlConfig(inner_steps=10, batch=60)               # S = 600 > 450: never the reference split
+    n = synth.num_samples(stream_len_for(big, CONFIG2))
+    assert n >= 660 and query_starts(big, [n]) == [600]
+    with pytest.raises(ValueError):
+        query_starts(big, [640])
+    w = window_table(big, 1, query_start=query_starts(big, [n]))
+    assert w[:10].max() < w[10].min()                        # the query batch follows every support sample
+
+
 def test_shard_tasks_round_robin():
     got = [shard_tasks(15, r, 8) for r in range(8)]
     assert sorted(sum(got, [])) == list(range(15))

@@ -8,8 +8,15 @@ result's error against float64 (the oracle run in f64 on the same inputs) next t
 the reference's own precision (the oracle in f32 on the CPU, MKL) and requires the GPU to be no
 less accurate than that, up to a small factor for summation-order noise.
 
-Workload: BASELINE config-2 shapes (N=441, Hc=256, LSTM 4x128), one task, B=2, K=2 inner steps,
-second order, clip active and inactive: forward, BPTT, weight gradients, the tangent sweep.
+Workload: BASELINE config-2 shapes (N=441, Hc=256, LSTM 4x128), one task, B=2, K=5 inner steps
+(the bench's depth: the error of five chained Hessian-vector steps), second order, clip active and
+inactive: forward, BPTT, weight gradients, the tangent sweep.
+
+Special values (``test_bf16x6_special_values``): the split differs from an f32 MFMA only outside
+the finite bf16 range. An inf operand gives NaN, not inf (x1 = x - x0 = inf - inf), and a finite
+|x| >= 3.3961e38 (where RNE to bf16 overflows piece x0) gives NaN where f32 could still be finite;
+every |x| below that is split exactly. Both cases stay non-finite, so a NaN/inf check downstream
+sees them either way.
 """
 import numpy as np
 import pytest
@@ -36,7 +43,7 @@ def rel(a, b):
 @pytest.mark.parametrize("max_norm", [1.0, 0.02])
 def test_f32_accuracy_against_float64(max_norm):
     d = CONFIG2
-    cfg = MamlConfig(inner_steps=2, batch=2, order=2, max_norm=max_norm)
+    cfg = MamlConfig(inner_steps=5, batch=2, order=2, max_norm=max_norm)
     P = synth.init_params(21, d, gcn_bias_scale=0.1)
     names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
     theta = {k: P[k] for k in names}
@@ -78,3 +85,32 @@ def test_f32_accuracy_against_float64(max_norm):
           f"mean gpu {np.mean([r[1] for r in rows]):.3e} cpu {np.mean([r[2] for r in rows]):.3e}")
     for name, e_gpu, e_cpu in rows:
         assert e_gpu <= FACTOR * e_cpu + 1e-7, (name, e_gpu, e_cpu)
+
+
+def test_bf16x6_special_values():
+    """The GCN drop-in (k_gcn_layer, staged bf16x6 split) on rows past the graph's nodes (self loop
+    only, F3): finite inputs up to 3.38e38 are f32-accurate; inf and |x| in (3.3961e38, FLT_MAX]
+    come out non-finite (NaN) on exactly the rows that hold them."""
+    from weatherforecast_stgcn_maml_amd.model import GCNConv
+
+    torch.manual_seed(3)
+    d = CONFIG2
+    side = int(round(d.num_nodes ** 0.5))
+    lats, lons = synth.region_grid(n_lat=side, n_lon=side)
+    ei = torch.from_numpy(build_spatial_graph(lats, lons, 4)[0])
+    conv = GCNConv(24, 64)
+    with torch.no_grad():
+        conv.lin.weight.mul_(1e-3)
+    rows = d.num_nodes + 64
+    x = torch.randn(rows, 24)
+    big, inf, over = d.num_nodes + 3, d.num_nodes + 10, d.num_nodes + 20
+    x[big, 5] = 3.38e38
+    x[inf, 7] = float("inf")
+    x[over, 2] = 3.40e38
+    out = conv.to(DEV)(x.to(DEV), ei.to(DEV)).cpu()
+    ref = refcpu.gcn_conv(x.double(), ei, conv.lin.weight.detach().cpu().double(), conv.bias.detach().cpu().double())
+    fin = [r for r in range(rows) if r not in (big, inf, over)]
+    assert torch.isfinite(out[fin]).all() and torch.isfinite(out[big]).all()
+    assert rel(out[fin].numpy(), ref[fin].numpy()) < 1e-6
+    assert rel(out[big].numpy(), ref[big].numpy()) < 1e-6
+    assert not torch.isfinite(out[inf]).any() and not torch.isfinite(out[over]).any()

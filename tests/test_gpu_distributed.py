@@ -12,7 +12,6 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-TASKS = 4
 STEPS = 2
 
 
@@ -24,7 +23,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, out_q):
+def _rank_main(rank, world, port, tasks, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     import torch
@@ -45,7 +44,7 @@ def _rank_main(rank, world, port, out_q):
     names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
     lats, lons = synth.region_grid(n_lat=5, n_lon=5)
     ei = build_spatial_graph(lats, lons, 4)[0]
-    mine = shard_tasks(TASKS, rank, world)
+    mine = shard_tasks(tasks, rank, world)
     feats = [synth.make_features(synth.task_seed(j), d.num_nodes, stream_len_for(cfg, d)) for j in mine]
     ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names}, ei,
                      device="cuda:0")
@@ -57,11 +56,11 @@ def _rank_main(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-def _run(world):
+def _run(world, tasks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, tasks, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
@@ -71,15 +70,21 @@ def _run(world):
     return res
 
 
-def test_two_rank_meta_learner_matches_one_rank():
-    one = _run(1)[0]
-    two = _run(2)
-    assert sorted(two[0][1] + two[1][1]) == list(range(TASKS)) and two[0][1] and two[1][1]
+@pytest.mark.parametrize("tasks", [4, 1])
+def test_two_rank_meta_learner_matches_one_rank(tasks):
+    """tasks = 1: rank 1 holds no task; it still joins the one all-reduce with zeros and takes
+    the replicated AdamW step (maml.py Z == 0 path), so both ranks end on the 1-rank theta."""
+    one = _run(1, tasks)[0]
+    two = _run(2, tasks)
+    assert sorted(two[0][1] + two[1][1]) == list(range(tasks))
+    assert bool(two[1][1]) == (tasks > 1)
     # replicated outer step on the all-reduced meta-gradient: bitwise identical on every rank
     assert np.array_equal(two[0][2], two[1][2])
     assert two[0][3] == two[1][3]  # meta_loss (all-reduced query-loss sum) identical too
     # and the 1-rank result up to the summation order of the task meta-gradients
     err = np.linalg.norm(two[0][2] - one[2]) / np.linalg.norm(one[2])
     assert err <= 1e-6, err
+    if tasks == 1:  # one task: the same sum on both sides, bitwise
+        assert np.array_equal(two[0][2], one[2])
     assert not np.array_equal(one[2], np.zeros_like(one[2]))
     np.testing.assert_allclose(two[0][3], one[3], rtol=1e-6)

@@ -456,9 +456,8 @@ def test_dropout_masks_follow_task_ids_not_groups():
 
 
 # ----------------------------------------------------------------------------- bench tile configs
-# The config-2 bench launches 4,420 BPTT workgroups per diagonal and runs the 64x128-tile
-# k_lstm_bwd_step / k_lstm_bwd_dual; launches under `bwd_big_min` (768) workgroups take the
-# 64x64 or split-K variants instead. These tests run every variant against the oracle and
+# The config-2 bench runs the 128x128-tile k_lstm_bwd_step / k_lstm_bwd_dual; launches under
+# `bwd_big_min` (768) 64-row tile units take the 64x64 or split-K variants instead. These tests run every variant against the oracle and
 # assert through the library's launch counters (smaml_variant_counts) which ones ran.
 _ORACLE = {}
 
@@ -483,15 +482,14 @@ def _check_meta_step(res, ml, ref, d, names, n_tasks, K):
         assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
 
 
-@pytest.mark.parametrize("pair", [0, 1])
 @pytest.mark.parametrize("keep", [-1, 0, 1])
-def test_second_order_bench_tiles_b32(keep, pair):
+def test_second_order_bench_tiles_b32(keep):
     """1 task x B=32 x K=2 at config-2 shapes (M = 14,112 sequences): a diagonal with all 4
-    layers holds 4 x 221 = 884 >= 768 BPTT tiles, so the bench's 64x128 k_lstm_bwd_step and
-    k_lstm_bwd_dual run (kept-primal and recomputed-primal forms by `keep`); the short corner
-    diagonals run the 64x64 tiles. Per-step losses, query MSE and the second-order
-    meta-gradient against the oracle (train_hybrid_maml_v5.py:110-184 + torch autograd).
-    `pair`: the BPTT kernels' paired block order (bwd_block) off / on."""
+    layers holds 4 x 111 x 2 = 888 >= 768 64-row tile units, so the bench's 128x128
+    k_lstm_bwd_step and k_lstm_bwd_dual run (kept-primal and recomputed-primal forms by `keep`);
+    the short corner diagonals run the 64x64 tiles. Per-step losses, query MSE and the
+    second-order meta-gradient against the oracle (train_hybrid_maml_v5.py:110-184 + torch
+    autograd)."""
     d = CONFIG2
     cfg = MamlConfig(inner_steps=2, batch=32, order=2)
     P = synth.init_params(13, d, gcn_bias_scale=0.1)
@@ -501,7 +499,6 @@ def test_second_order_bench_tiles_b32(keep, pair):
     ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=None)
     ml.set_tasks(feats)
     ml.ctx.set_option("keep", keep)
-    ml.ctx.set_option("bwd_pair", pair)
     ml.ctx.variant_counts(reset=True)
     res = ml.meta_step()
     vc = ml.ctx.variant_counts()
@@ -519,7 +516,7 @@ def test_second_order_bench_tiles_b32(keep, pair):
 
 def test_second_order_bench_tiles_b32_dropout():
     """The bench-size tiles with train-mode dropout (0.2 / 0.2: the masked loaders and the
-    dropout variants of the 64x128 BPTT and tangent BPTT kernels) against the oracle's restated
+    dropout variants of the 128x128 BPTT and tangent BPTT kernels) against the oracle's restated
     masks: 1 task x B=32 x K=1, second order."""
     d = CONFIG2
     cfg = MamlConfig(inner_steps=1, batch=32, order=2)
@@ -542,12 +539,11 @@ def test_second_order_bench_tiles_b32_dropout():
     _check_meta_step(res, ml, ref, d, names, 1, cfg.inner_steps)
 
 
-@pytest.mark.parametrize("tiles", ["big", "big_pair", "small", "split"])
+@pytest.mark.parametrize("tiles", ["big", "small", "split"])
 @pytest.mark.parametrize("keep", [-1, 0])
 def test_second_order_tile_variants_task_groups(tiles, keep):
     """Every BPTT tile variant forced at config-2 shapes (B=1, K=2, 3 tasks run in task groups
-    of 2): 64x128 tiles (the bench's; also in the paired block order, whose 7 row tiles per
-    problem pad to 8), 64x64 tiles, and the split-K small-grid steps."""
+    of 2): 128x128 tiles (the bench's), 64x64 tiles, and the split-K small-grid steps."""
     d = CONFIG2
     cfg = MamlConfig(inner_steps=2, batch=1, order=2)
     P = synth.init_params(14, d, gcn_bias_scale=0.1)
@@ -557,8 +553,7 @@ def test_second_order_tile_variants_task_groups(tiles, keep):
     ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=2)
     ml.set_tasks(feats)
     assert len(ml._groups) == 2
-    big = 0 if tiles.startswith("big") else 1 << 30
-    ml.ctx.set_option("bwd_pair", 1 if tiles == "big_pair" else 0)
+    big = 0 if tiles == "big" else 1 << 30
     ml.ctx.set_option("bwd_big_min", big)
     ml.ctx.set_option("bwdd_big_min", big)
     ml.ctx.set_option("split_max", 4 if tiles == "split" else 1)
@@ -566,9 +561,9 @@ def test_second_order_tile_variants_task_groups(tiles, keep):
     ml.ctx.variant_counts(reset=True)
     res = ml.meta_step()
     vc = ml.ctx.variant_counts()
-    dual = ("bwd_dual_big" if tiles.startswith("big") else "bwd_dual_small") + ("_kept" if keep else "")
+    dual = ("bwd_dual_big" if tiles == "big" else "bwd_dual_small") + ("_kept" if keep else "")
     assert vc[dual] > 0, vc
-    if tiles.startswith("big"):
+    if tiles == "big":
         assert vc["bwd_big"] > 0 and vc["bwd_small"] == vc["bwd_split"] == 0, vc
     elif tiles == "small":
         assert vc["bwd_small"] > 0 and vc["bwd_big"] == vc["bwd_split"] == 0 and vc["fwd_split"] == 0, vc

@@ -1,0 +1,169 @@
+"""Second-order MAML at the inner-step depth the benchmarks run (BASELINE config 2: K=5; config 5:
+K=10) against the CPU oracle (train_hybrid_maml_v5.py:110-184 restated in oracle/refcpu.py, the
+meta-gradient by torch autograd through every inner step, create_graph=True).
+
+What K > 2 exercises that the K = 2 tests do not: kept-primal slots >= 2 (each
+slot i >= 1 holds its own Hs / Cs / Gs / dG / dh), the v-recursion chained over K-1 `k_axpy_dot`
+passes, and the per-step theta_k / g_k / ||g_k|| / clip-coefficient stores beyond k = 1.
+
+Tolerances (BASELINE): per-step losses <= 1e-5 rel, query MSE <= 1e-4 rel,
+meta-gradient <= 1e-4 rel-L2 per parameter tensor.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import refcpu
+from weatherforecast_stgcn_maml_amd import params, synth
+from weatherforecast_stgcn_maml_amd.config import CONFIG2, CONFIG5, SEED, MamlConfig
+from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
+from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+DIAGS = CONFIG2.window_size + CONFIG2.lstm_num_layers - 1  # 27 wavefront launches per sweep step
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def split(P):
+    names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
+    return {k: P[k] for k in names}, {k: v for k, v in P.items() if k not in names}, names
+
+
+def grid_edges(d):
+    side = int(round(d.num_nodes ** 0.5))
+    lats, lons = synth.region_grid(n_lat=side, n_lon=side)
+    return build_spatial_graph(lats, lons, 4)[0]
+
+
+_ORACLE = {}
+
+
+def oracle(key, d, P, names, feats, ei, cfg, qidx):
+    if key not in _ORACLE:
+        PT = refcpu.to_torch(P)
+        _ORACLE[key] = refcpu.meta_step({k: PT[k] for k in names}, {k: v for k, v in PT.items() if k not in names},
+                                        [refcpu.TaskData(f, ei, d) for f in feats], qidx, cfg.inner_steps,
+                                        cfg.batch, cfg.inner_steps * cfg.batch, cfg.inner_lr, cfg.max_norm,
+                                        cfg.order)
+    return _ORACLE[key]
+
+
+def check(res, ml, ref, d, names, n_tasks, K):
+    losses = res.losses.cpu().numpy()
+    norms = res.norms.cpu().numpy()
+    for j in range(n_tasks):
+        assert rel(losses[:K, j], [r[0] for r in ref["step_records"][j]]) < 1e-5
+        assert rel(norms[:K, j], [r[1] for r in ref["step_records"][j]]) < 1e-5
+        assert abs(losses[-1, j] - ref["query_losses"][j]) < 1e-4 * ref["query_losses"][j]
+    mg = params.unpack(ml.meta_grad, d, 0)
+    for k in names:
+        assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
+
+
+# ----------------------------------------------------------------------------- (a) config 2, K = 5
+K5_CFG = MamlConfig(inner_steps=5, batch=4, order=2, max_norm=0.01)  # grad norms 0.014-0.016
+
+
+@pytest.mark.parametrize("keep", [-1, 0, 3])
+def test_second_order_k5_cfg2_bench_tiles(keep):
+    """Config-2 shapes, 2 tasks x B=4 x K=5, second order, clip active on every inner step
+    (max_norm 0.01), task groups of one (the meta-gradient summed over groups). The bench's
+    128x128 BPTT / tangent-BPTT tiles are forced on every diagonal (bwd_big_min = bwdd_big_min = 0);
+    keep = -1 keeps all 5 inner steps' primal (the bench's setting), 0 recomputes every step's
+    primal in the sweep, 3 keeps steps 4, 3, 2 (slots 0-2) and recomputes steps 1, 0."""
+    d, cfg = CONFIG2, K5_CFG
+    P = synth.init_params(23, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(2300 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2)]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=1)
+    ml.set_tasks(feats)
+    assert len(ml._groups) == 2
+    ml.ctx.set_option("bwd_big_min", 0)
+    ml.ctx.set_option("bwdd_big_min", 0)
+    ml.ctx.set_option("keep", keep)
+    ml.ctx.variant_counts(reset=True)
+    res = ml.meta_step()
+    vc = ml.ctx.variant_counts()
+    K, G = cfg.inner_steps, len(ml._groups)
+    kept = K if keep < 0 else keep
+    assert ml.ctx.so_kept_steps() == kept
+    assert vc["bwd_small"] == vc["bwd_split"] == 0 and vc["bwd_dual_small"] == vc["bwd_dual_small_kept"] == 0, vc
+    assert vc["bwd_big"] == G * (K + 1) * DIAGS, vc          # K inner steps + the query backward
+    assert vc["bwd_dual_big_kept"] == G * kept * DIAGS, vc   # tangent-only sweep steps
+    assert vc["bwd_dual_big"] == G * (K - kept) * DIAGS, vc  # primal recomputed at theta_k
+    assert vc["fwd_dual_kept"] == G * kept * DIAGS and vc["fwd_dual"] == G * (K - kept) * DIAGS, vc
+    ref = oracle("k5", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
+    assert all(r[2] < 1.0 for rec in ref["step_records"] for r in rec), "clip must be active on every step"
+    check(res, ml, ref, d, names, 2, K)
+
+
+# ----------------------------------------------------------------------------- (b) config 5, K = 10
+def test_second_order_k10_cfg5():
+    """BASELINE config-5 shapes (N=1024, Hc=512, LSTM 4x128), 1 task x B=1 x K=10, every inner
+    step's primal kept (slots 0-9)."""
+    d = CONFIG5
+    cfg = MamlConfig(inner_steps=10, batch=1, order=2)
+    P = synth.init_params(24, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(2400, d.num_nodes, stream_len_for(cfg, d))]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml.set_tasks(feats)
+    ml.ctx.variant_counts(reset=True)
+    res = ml.meta_step()
+    vc = ml.ctx.variant_counts()
+    assert ml.ctx.so_kept_steps() == 10
+    assert vc["fwd_dual"] == 0 and vc["fwd_dual_kept"] == 10 * (d.window_size + d.lstm_num_layers - 1), vc
+    ref = oracle("k10", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
+    check(res, ml, ref, d, names, 1, cfg.inner_steps)
+
+
+# ----------------------------------------------------------------------------- (c) the benched step
+def test_bench_configuration_properties_and_determinism():
+    """The bench's own meta-step: BASELINE config 2 (15 tasks x B=32 x T=24 x N=441, K=5, second
+    order, task_group "auto" = 3 groups of 5 with all 5 steps kept), seeded as bench.py seeds it.
+    Too large for the oracle, so size-independent properties: every loss / norm / meta-gradient
+    entry finite, the query MSE near the target variance (unit-variance synthetic targets at
+    init), theta moves; and the whole step is bitwise reproducible (losses, norms, meta-gradient
+    and the post-AdamW theta of a second run from the same state)."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=5, batch=32, order=2)
+    P = synth.init_params(SEED, d)
+    theta, gcn, _ = split(P)
+    ei = grid_edges(d)
+    T = stream_len_for(cfg, d)
+    feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T) for j in range(15)]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml.set_tasks(feats)
+    assert [len(g) for _, g in ml._groups] == [5, 5, 5]
+    theta0, m0, v0 = ml.theta.clone(), ml.m.clone(), ml.v.clone()
+    runs = []
+    for _ in range(2):
+        ml.theta.copy_(theta0)
+        ml.m.copy_(m0)
+        ml.v.copy_(v0)
+        ml.step = 0
+        ml.ctx.variant_counts(reset=True)
+        res = ml.meta_step()
+        assert ml.ctx.so_kept_steps() == cfg.inner_steps
+        vc = ml.ctx.variant_counts()
+        assert vc["bwd_dual_big_kept"] > 0 and vc["bwd_dual_big"] == 0, vc
+        runs.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone(), ml.theta.cpu().clone(),
+                     res.meta_loss))
+    L, N, G, TH, ML = runs[0]
+    assert np.isfinite(L.numpy()).all() and np.isfinite(N.numpy()).all() and np.isfinite(G.numpy()).all()
+    assert 0.5 < float(L[-1].mean()) < 2.0
+    assert float(N.min()) > 0.0
+    assert float(G.norm()) > 0.0 and not torch.equal(TH, theta0.cpu())
+    assert np.isfinite(ML)
+    for a, b in zip(runs[0][:4], runs[1][:4]):
+        assert torch.equal(a, b)
+    assert runs[0][4] == runs[1][4]

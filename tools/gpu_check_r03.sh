@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-3 GPU check: the -m gpu suite (or the test ids in $TESTS), smoke, then the default bench.
+# Each GPU step has its own time limit; the first failure ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${TAG:-r03}
+timeout -k 10 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/} \
+  > gpurun_out/${TAG}_pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc
+if [ -n "${SMOKE:-1}" ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
+  tail -1 gpurun_out/${TAG}_smoke.log
+fi
+if [ -n "${BENCH:-1}" ]; then
+  timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
+  tail -1 gpurun_out/${TAG}_bench.log | cut -c1-400
+fi

@@ -69,9 +69,13 @@ class ClimateAwareLRScheduler:
 
 def random_sampler_order(n: int) -> torch.Tensor:
     """The order a ``DataLoader(ds, batch_size=1, shuffle=True)`` (adapt_hybrid_v5.py:179; PyG's
-    loader is torch's) yields in one epoch, drawing from the global torch RNG exactly as it does:
-    the iterator first draws its ``_base_seed`` (one int64), then ``RandomSampler`` draws its
-    own seed (one int64) and runs ``randperm`` on a generator seeded with it."""
+    loader is torch's) yields in one epoch, drawing from the global torch RNG as it does: the
+    iterator first draws its ``_base_seed`` (one int64), then ``RandomSampler`` draws its own seed
+    (one int64) and runs ``randperm`` on a generator seeded with it. This reproduces the
+    reference's order for its first epoch, and for every epoch only when the adaptation is
+    dropout-free: ``adaptModel`` trains in train mode, where each step's ``nn.Dropout`` also draws
+    from the global RNG, so from epoch 2 its shuffle depends on draws this path does not make.
+    Parity with train-mode adaptation therefore replays recorded orders (``adapt(orders=...)``)."""
     torch.empty((), dtype=torch.int64).random_()  # _BaseDataLoaderIter._base_seed
     seed = int(torch.empty((), dtype=torch.int64).random_().item())
     g = torch.Generator()

@@ -23,8 +23,21 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+STAMP = OUT + ".flags"  # the extra flags the default library was built with (build-flag changes rebuild it)
+
+
+def extra_flags() -> list:
+    return os.environ.get("SMAML_EXTRA_FLAGS", "").split()
+
+
 def up_to_date() -> bool:
     if not os.path.exists(OUT):
+        return False
+    try:
+        with open(STAMP) as f:
+            if f.read() != " ".join(extra_flags()):
+                return False
+    except OSError:
         return False
     t = os.path.getmtime(OUT)
     return all(os.path.getmtime(p) <= t for p in SOURCES + HEADERS)
@@ -38,25 +51,35 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     # -fno-slp-vectorize: keeps the bf16x6 split's f32 subtractions as v_sub_f32 instead of v_pk_add_f32
     # (packed f32 VALU beside MFMAs costs extra issue cycles; A/B 2045 -> 2003 ms per meta-step)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize", "-I", os.path.join(REPO, "include"),
-             "-I", CSRC, *[f"-D{d}" for d in defines], *os.environ.get("SMAML_EXTRA_FLAGS", "").split()]
+             "-I", CSRC, *[f"-D{d}" for d in defines], *extra_flags()]
     objs, procs = [], []
-    for src in SOURCES:
-        obj = f"{out}.{os.path.basename(src)}.o"
-        cmd = [hipcc(), *flags, "-c", src, "-o", obj]
+    try:
+        for src in SOURCES:
+            obj = f"{out}.{os.path.basename(src)}.o"
+            cmd = [hipcc(), *flags, "-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append(subprocess.Popen(cmd))
+            objs.append(obj)
+        rcs = [p.wait() for p in procs]
+        if any(rcs):
+            raise subprocess.CalledProcessError(max(rcs), "hipcc")
+        link = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", out + ".tmp"]
         if verbose:
-            print(" ".join(cmd))
-        procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
-    rcs = [p.wait() for p in procs]
-    if any(rcs):
-        raise subprocess.CalledProcessError(max(rcs), "hipcc")
-    link = [hipcc(), f"--offload-arch={ARCH}", "-shared", *objs, "-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(link))
-    subprocess.run(link, check=True)
-    for o in objs:
-        os.remove(o)
-    os.replace(out + ".tmp", out)
+            print(" ".join(link))
+        subprocess.run(link, check=True)
+        os.replace(out + ".tmp", out)
+        if out == OUT:
+            with open(STAMP, "w") as f:
+                f.write(" ".join(extra_flags()))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for o in objs + [out + ".tmp"]:
+            if os.path.exists(o):
+                os.remove(o)
     return out
 
 

@@ -220,8 +220,7 @@ struct smaml_ctx {
   Staging stage;
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
-  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-            SMAML_BWD_PAIR};
+  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -316,9 +315,6 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
   parts.push_back({(void**)&w.pred, seq * d.HfC * 4});
   parts.push_back({(void**)&w.dpred, seq * d.HfC * 4});
   parts.push_back({(void**)&w.wpart, wpart * 4});
-  const int64_t pcap = SMAML_PIECES ? (int64_t)zc * c->po.P + 8 : 8;  // parameter pieces (split_params)
-  parts.push_back({(void**)&w.pcs_buf[0], 3 * pcap * 2});
-  parts.push_back({(void**)&w.pcs_buf[1], 3 * pcap * 2});
   parts.push_back({(void**)&w.lpart, lblk * 4});
   parts.push_back({(void**)&w.sqpart, (int64_t)(zc + 1) * SQB * 8});
   parts.push_back({(void**)&w.hTd, seq * d.H * 4});
@@ -360,8 +356,6 @@ int reserve(smaml_ctx* c, int Z, int B, bool so = false) {
     off += (p.second + 255) / 256 * 256;
   }
   w.wpart_floats = wpart;
-  w.pcs_cap = pcap;
-  w.pm = PieceMap{};
   HIP_TRY(hipMemset(grad, 0, (size_t)zc * c->po.P * 4));
   HIP_TRY(hipMemset(fast, 0, (size_t)zc * c->po.P * 4));
   c->arena = arena;
@@ -592,36 +586,10 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
   return SMAML_OK;
 }
 
-// Three bf16 planes of the sweep's parameter vectors (theta -> slot 0, U -> slot 1): the staged
-// LSTM kernels read their weight tiles from them (PieceMap). theta / U are constant over a sweep.
-int split_params(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* U) {
-  if (!SMAML_PIECES) return SMAML_OK;
-  Work& w = c->w;
-  const int64_t span = tstride > 0 ? (int64_t)(w.Z - 1) * tstride + c->po.P : c->po.P;
-  const int64_t plane = (span + 7) / 8 * 8;  // 16-B aligned planes (8-element piece loads)
-  if (plane > w.pcs_cap) return fail(SMAML_EINVAL, "split_params: parameter span exceeds the reserved pieces");
-  const float* src[2] = {theta, U};
-  for (int i = 0; i < 2; ++i) {
-    if (!src[i]) {
-      w.pm.src[i] = nullptr;
-      w.pm.pcs[i] = nullptr;
-      w.pm.n[i] = 0;
-      continue;
-    }
-    launch_split3(s, src[i], span, plane, w.pcs_buf[i]);
-    w.pm.src[i] = src[i];
-    w.pm.pcs[i] = w.pcs_buf[i];
-    w.pm.n[i] = plane;
-  }
-  HIP_TRY(hipGetLastError());
-  return SMAML_OK;
-}
-
 // LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront).
 int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   const Dims& d = c->d;
   Work& w = c->w;
-  TRY(split_params(c, s, theta, tstride, nullptr));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     const double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
@@ -670,7 +638,6 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   const Dims& d = c->d;
   Work& w = c->w;
   const ParamOff& po = c->po;
-  TRY(split_params(c, s, theta, tstride, nullptr));
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
   // BPTT as reverse anti-diagonals; layer l's weight gradient as soon as its t = 0 step is done,
@@ -710,7 +677,6 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
                      const float* const* xtab_dev, bool gcn_cached) {
   const Dims& d = c->d;
   Work& w = c->w;
-  TRY(split_params(c, s, theta, tstride, U));
   const int rps = d.T * d.N;
   const int zb = w.Z * w.B;
   const float* src = nullptr;
@@ -736,7 +702,6 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
 
 // Tangent of the backward pass: HU[z] = H_z U[z] (primal weight grads are not formed).
 int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride, float* HU) {
-  TRY(split_params(c, s, theta, tstride, U));
   const Dims& d = c->d;
   Work& w = c->w;
   const ParamOff& po = c->po;
@@ -864,7 +829,6 @@ int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out) {
   c->go.total = tot;
   if (const char* e = std::getenv("SMAML_BWD_BIG_MIN")) c->kn.bwd_big_min = std::atoi(e);
   if (const char* e = std::getenv("SMAML_BWDD_BIG_MIN")) c->kn.bwdd_big_min = std::atoi(e);
-  if (const char* e = std::getenv("SMAML_BWD_PAIR")) c->kn.bwd_pair = std::atoi(e) != 0;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
     delete c;
@@ -1260,8 +1224,6 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.split_max = (int)std::min<int64_t>(value, 64);
   } else if (k == "wgrad_group_max_rows" && value >= 0) {
     c->kn.wgrad_group_max_rows = (int)std::min<int64_t>(value, 1 << 30);
-  } else if (k == "bwd_pair" && (value == 0 || value == 1)) {
-    c->kn.bwd_pair = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {

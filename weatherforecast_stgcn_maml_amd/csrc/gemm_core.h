@@ -1,15 +1,22 @@
-// fp32 MFMA GEMM core for gfx950 (CDNA4).
+// GEMM core for gfx950 (CDNA4): f32 operands, f32 accumulation.
 //
-// All GEMM-shaped work on the STGCN-LSTM path goes through this mainloop with
-// v_mfma_f32_32x32x2_f32 (exact f32 in / f32 accumulate, the f32 MFMA peak rate).
+// All GEMM-shaped work on the STGCN-LSTM path goes through these mainloops. Products (GemmCfg X6_):
+//   2 (default, "staged bf16x6"): the thread that stages a float4 of an operand splits it into three
+//     bf16 pieces (x = x0 + x1 + x2, exact to 2^-27 |x|) written to bf16 LDS planes; each 16-k step
+//     issues six v_mfma_f32_32x32x16_bf16 (the piece products a_i b_j with i + j <= 2, f32
+//     accumulation): f32-accurate products at 6/16 of the f32 MFMA's cost (mfma_x6, split4);
+//   1 ("fragment split"): f32 LDS images, the split on each wave's MFMA fragments (split3);
+//   0: v_mfma_f32_32x32x2_f32 (exact f32 products) from f32 LDS images (-DSMAML_X6=0).
+// Special values: the split is exact for every finite |x| < 3.3961e38; an inf operand, or a finite
+// one at or above that (its RNE piece x0 overflows to inf), makes the products NaN (inf - inf),
+// where f32 MFMA products could give inf or, for |x| in [3.3961e38, FLT_MAX], a finite value.
 //
-// K order: inside a BK=32 tile, MFMA k-step s (0..15) of lane half h (= lane>>5) covers
-// k = 16h + s, so one lane's 16 k-values of a row are contiguous: a k-contiguous ("KC")
-// operand is kept row-major in LDS ([rows][BK+4], written with ds_write_b128) and each
-// lane fetches 4 k-steps of a fragment with ONE conflict-free ds_read_b128 (row stride 36
-// floats puts the 16 rows of every ds_read_b128 lane group on distinct 4-bank slots).
-// An "MC" operand (rows contiguous, e.g. W_hh used as [k][n]) is kept k-major in LDS
-// ([BK][rows+4], ds_write_b128) and read with ds_read_b32 (lanes read consecutive rows).
+// f32 LDS images (X6_ 0 / 1), K order: inside a K-tile, MFMA k-step s of lane half h (= lane>>5)
+// covers k = (BK/2) h + s, so one lane's k-values of a row are contiguous: a k-contiguous ("KC")
+// operand is kept row-major in LDS ([rows][BK+4], written with ds_write_b128) and each lane fetches
+// 4 k-steps of a fragment with ONE conflict-free ds_read_b128. An "MC" operand (rows contiguous,
+// e.g. W_hh used as [k][n]) is kept k-major in LDS ([BK][rows+4]) and read with ds_read_b32.
+// The staged bf16 images (X6Img) are described at their definition.
 //
 // Staging: global -> registers (float4 per lane) -> LDS, double buffered with one barrier
 // per K-tile, so the global loads of tile k+1 are in flight while tile k's MFMAs issue.
@@ -34,12 +41,6 @@ constexpr int BK = 32;  // default K-tile (GemmCfg's BK_ parameter)
 #endif                // (IG template argument; A/B: fwd_dual -7, wgrad -7, GCN -2 ms; the primal
                       // gate / BPTT / dual-BPTT loops are slower with it and keep the default order)
 constexpr int NT = 256;  // threads per workgroup of the 4-wave configurations
-#ifndef SMAML_X6S_MIDSTORE
-#define SMAML_X6S_MIDSTORE 0  // staged split: next tile's stores between the two halves of the MFMA phase
-#endif
-#ifndef SMAML_CHUNKED_F32
-#define SMAML_CHUNKED_F32 0  // chunked split-K mainloop (small grids) on the f32 MFMA (config 4 A/B: 1.137 ->
-#endif                       // 1.194 ms per sample-step, slower: off)
 #ifndef SMAML_X6
 #define SMAML_X6 1  // default product form of GemmCfg: 1 = bf16x6 (f32-accurate, see mfma_x6), 0 = f32 MFMA
 #endif
@@ -256,8 +257,7 @@ __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x
   return acc;
 }
 
-// F32: f32 MFMA products whatever C::X6 says (an A/B arm for the chunked split-K steps of small grids).
-template <class C, int IG = -1, class Hook = NoHook, bool F32 = false>
+template <class C, int IG = -1, class Hook = NoHook>
 __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C>& acc, Hook& hook) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / C::WAVES_N, wn = wave % C::WAVES_N;
@@ -265,7 +265,7 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
   const int brow = wn * (C::WTN * 32) + (lane & 31);
   const int h = lane >> 5;
   if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
-  if constexpr (C::X6 && !F32) {
+  if constexpr (C::X6) {
 #pragma unroll
   for (int s = 0; s < C::BK / 16; ++s) {
     Split3 a[C::WTM];
@@ -334,11 +334,8 @@ __device__ __forceinline__ void split4(const float4& v, uint2& p0, uint2& p1, ui
   p2 = make_uint2(q2[0], q2[1]);
 }
 
-#ifndef SMAML_DIAG_NOBSPLIT
-#define SMAML_DIAG_NOBSPLIT 0  // timing diagnostic only (wrong results): B tiles stored as one RNE piece
-#endif
 // Split this thread's staged float4s of one operand tile into the image at `img` (byte base).
-template <int ROWS, int F4, int NTH, bool KC, int BK, bool ONEPIECE = false>
+template <int ROWS, int F4, int NTH, bool KC, int BK>
 __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) {
   using I = X6Img<ROWS, KC, BK>;
   const int tid = threadIdx.x;
@@ -354,77 +351,22 @@ __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) 
       off = kk * I::RS + 8 * q;
     }
     uint2 p0, p1, p2;
-    if (ONEPIECE) {
-      p0 = make_uint2(pk_bf16(r[i].x, r[i].y), pk_bf16(r[i].z, r[i].w));
-      p1 = p2 = make_uint2(0u, 0u);
-    } else {
-      split4(r[i], p0, p1, p2);
-    }
+    split4(r[i], p0, p1, p2);
     *reinterpret_cast<uint2*>(img + off) = p0;
     *reinterpret_cast<uint2*>(img + I::PLANE + off) = p1;
     *reinterpret_cast<uint2*>(img + 2 * I::PLANE + off) = p2;
   }
 }
 
-// Operand loaders that deliver pre-split pieces (PieceMap): fetch_pieces fills, per item of 8
-// consecutive elements along the tile's contiguous axis (KC: 8 k of one row; MC: 8 rows of one k),
-// one 16-B piece vector per plane; items are dealt to threads tid, tid + NTH, ... (threads past the
-// tile's item count idle: whole waves, since the item counts are multiples of 64).
-template <class L, class = void>
-struct has_pieces : std::false_type {};
-template <class L>
-struct has_pieces<L, std::void_t<decltype(L::kPieces)>> : std::true_type {};
-
-template <int ROWS, int BK>
-struct PieceItems {
-  static constexpr int ITEMS = ROWS * BK / 8;
-};
-
-template <int ROWS, int PI, int NTH, bool KC, int BK>
-__device__ __forceinline__ void store_pieces(char* img, const uint4 (&p)[3][PI]) {
-  using I = X6Img<ROWS, KC, BK>;
-  constexpr int ITEMS = PieceItems<ROWS, BK>::ITEMS;
-#pragma unroll
-  for (int i = 0; i < PI; ++i) {
-    const int f = (int)threadIdx.x + NTH * i;
-    if (ITEMS % NTH != 0 && f >= ITEMS) break;
-    int off;
-    if (KC) {
-      const int rr = f / (BK / 8), c = f % (BK / 8);
-      off = rr * I::RS + 16 * (c ^ I::swz(rr));
-    } else {
-      const int kk = f / (ROWS / 8), g = f % (ROWS / 8);
-      off = kk * I::RS + 16 * g;
-    }
-    *reinterpret_cast<uint4*>(img + off) = p[0][i];
-    *reinterpret_cast<uint4*>(img + I::PLANE + off) = p[1][i];
-    *reinterpret_cast<uint4*>(img + 2 * I::PLANE + off) = p[2][i];
-  }
-}
-
-// B operand staging for the staged mainloops: f32 float4s (split at the store) or pieces.
-template <class C, class LB, bool P = has_pieces<LB>::value>
+// B operand staging for the staged mainloops: f32 float4s, split at the LDS store.
+template <class C, class LB>
 struct BStage {
   float4 r[C::B_F4];
   __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0) {
     fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, k0, r);
   }
-  template <bool ONE = false>
   __device__ __forceinline__ void store(char* img) const {
-    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK, ONE>(img, r);
-  }
-};
-template <class C, class LB>
-struct BStage<C, LB, true> {
-  static constexpr int PI = (PieceItems<C::BN, C::BK>::ITEMS + C::NTH - 1) / C::NTH;
-  static_assert(PieceItems<C::BN, C::BK>::ITEMS % 64 == 0, "piece items: whole waves");
-  uint4 p[3][PI];
-  __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0) {
-    lb.template fetch_pieces<C::BN, PI, C::NTH, C::B_KC, C::BK>(n0, k0, p);
-  }
-  template <bool ONE = false>
-  __device__ __forceinline__ void store(char* img) const {
-    store_pieces<C::BN, PI, C::NTH, C::B_KC, C::BK>(img, p);
+    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(img, r);
   }
 };
 
@@ -500,7 +442,7 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   auto store = [&](char* st) {
     if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra);
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
-    rb.template store<SMAML_DIAG_NOBSPLIT != 0>(st + SA);
+    rb.store(st + SA);
   };
   fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg, ra);
   rb.fetch(lb, n0, kbeg);
@@ -526,13 +468,6 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
         __syncthreads();  // every wave has read the stage
         store(st0);
       }
-    } else if constexpr (SMAML_X6S_MIDSTORE && C::WTN >= 2) {
-      // the next tile's split + LDS stores between the two halves of this tile's MFMAs (the
-      // other stage), so a SIMD's waves overlap them with MFMAs instead of meeting at the barrier
-      constexpr int JH = C::WTN / 2;
-      mma_tile_x6s<C, IG, 0, JH>(st, st + SA, acc);
-      if (more) store(st0 + (cur ^ 1) * C::X6S_STAGE);
-      mma_tile_x6s<C, IG, JH, C::WTN>(st, st + SA, acc);
     } else {
 #if SMAML_PRIO
       __builtin_amdgcn_s_setprio(1);
@@ -644,7 +579,7 @@ __device__ __forceinline__ void gemm_mainloop_chunked(const LA& la, const LB& lb
 #endif
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
-      if (c0 + i < nkt) mma_tile<C, -1, NoHook, SMAML_CHUNKED_F32 != 0>(As + i * C::A_STAGE, Bs + i * C::B_STAGE, acc, hook);
+      if (c0 + i < nkt) mma_tile<C, -1, NoHook>(As + i * C::A_STAGE, Bs + i * C::B_STAGE, acc, hook);
 #if SMAML_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -763,8 +698,8 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
   auto store = [&](char* st, int k0) {
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
     if (k0 >= a2_kbeg) store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st + SA, ra2);
-    rb.template store<SMAML_DIAG_NOBSPLIT != 0>(st + 2 * SA);
-    rb2.template store<SMAML_DIAG_NOBSPLIT != 0>(st + 2 * SA + SB);
+    rb.store(st + 2 * SA);
+    rb2.store(st + 2 * SA + SB);
   };
   auto mma = [&](const char* st, bool a2on) {
 #pragma unroll

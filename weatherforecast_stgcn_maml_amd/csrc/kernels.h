@@ -108,11 +108,7 @@ struct Knobs {
   int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
   int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
   int wgrad_group_wgs;       // workgroups that grouped launch aims for
-  int bwd_pair;              // big-tile BPTT launches in the paired block order (bwd_block)
 };
-#ifndef SMAML_BWD_PAIR
-#define SMAML_BWD_PAIR 0
-#endif
 #ifndef SMAML_WGRAD_GROUP_ROWS
 #define SMAML_WGRAD_GROUP_ROWS 2048
 #endif
@@ -121,36 +117,8 @@ struct Knobs {
 #endif
 
 // Activations of one forward pass for Z tasks x B samples (M = B*N sequences per task).
-#ifndef SMAML_PIECES
-#define SMAML_PIECES 0  // staged LSTM kernels read theta / U as pre-split pieces (PieceMap, split_params);
-#endif                  // parity-green but slower (A/B 1882 -> 1974 ms: 3 x 8-B piece loads per float4)
-// bf16 pieces of the parameter vectors a sweep reads as GEMM B operands (split_params, api.cpp):
-// slot i maps the f32 range [src[i], src[i] + n[i]) to three planes pcs[i] + {0, n, 2n}[piece] of
-// the same element order (x0 = RNE(x), x1 = RNE(x - x0), x2 = RNE(x - x0 - x1)), so the weight tiles
-// reach the LDS images without a per-workgroup split. Slot 0: theta, slot 1: the tangent direction U.
-struct PieceMap {
-  const float* src[2];
-  const uint16_t* pcs[2];
-  int64_t n[2];
-  // pieces of the f32 element at p (plane 0) and the plane stride; the sweep's launcher checks on
-  // the host that every operand it passes lies in a slot
-  __device__ __forceinline__ const uint16_t* find(const float* p, int64_t& stride) const {
-    const int i = (n[1] > 0 && p >= src[1] && p < src[1] + n[1]) ? 1 : 0;
-    stride = n[i];
-    return pcs[i] + (p - src[i]);
-  }
-  bool covers(const float* p, int64_t len) const {
-    for (int i = 0; i < 2; ++i)
-      if (n[i] > 0 && p >= src[i] && p + len <= src[i] + n[i]) return true;
-    return false;
-  }
-};
-
 struct Work {
   int Z, B, M;
-  PieceMap pm;             // parameter pieces of the current sweep (split_params)
-  uint16_t* pcs_buf[2];    // piece planes, 3 x pcs_cap bf16 per slot
-  int64_t pcs_cap;
   int64_t* vcount;         // [NVAR] launch counters (ctx-owned; may be null)
   Knobs kn;
   float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
@@ -195,7 +163,6 @@ struct FwdWave {
   int n;
   int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
   LayerOff lo[MAX_LAYERS];
-  PieceMap pm;
 };
 // Backward counterpart: problems (l, t) with (L-1-l) + (T-1-t) = e. Step (l, t) forms
 //   dh = [dG(l+1, t) | dG(l, t+1)] . [W_ih(l+1) ; W_hh(l)]   (one K = 8H GEMM; the dX of the
@@ -205,8 +172,6 @@ struct BwdWave {
   int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
   LayerOff lo[MAX_LAYERS];
   int64_t wih_up[MAX_LAYERS];  // W_ih offset of layer l+1 (unused at the top layer)
-  int pair;  // 1: paired block order (bwd_block; off[] spaced by a multiple of 8 row tiles)
-  PieceMap pm;
 };
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv);
@@ -215,8 +180,6 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
                 FwdWave& wv);
 
 const char* products_info();  // product form per GEMM family as built (kernels.hip)
-// Three bf16 planes of x[0, n) into dst (plane p at dst + p * plane, plane >= n, a multiple of 4); see PieceMap.
-void launch_split3(hipStream_t s, const float* x, int64_t n, int64_t plane, uint16_t* dst);
 
 // ---- launchers (kernels.hip) ----
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,

@@ -7,13 +7,15 @@
 //   k_head_loss        Linear head + view/reshape + MSELoss (F4 row permutation)
 //                      hybrid_model.py:105-115, train_hybrid_maml_v5.py:119,133
 //   k_lstm_bwd_step    BPTT of the cell (loss.backward through LSTM)   train_hybrid_maml_v5.py:134
-//   k_wgrad            dW_ih | dW_hh | db  as a split-K fp32 MFMA GEMM over B*N*T rows
+//   k_wgrad            dW_ih | dW_hh | db  as a split-K GEMM over B*N*T rows
 //   k_clip_sgd         clip_grad_norm_(1.0) + SGD(lr)   train_hybrid_maml_v5.py:135-139
 //   k_adamw            clip + AdamW (outer)             train_hybrid_maml_v5.py:174-179,245-249
 //
-// Every GEMM-shaped contraction runs on v_mfma_f32_32x32x2_f32 (gemm_core.h). All
-// reductions are in a fixed order (no float atomics), so results are bitwise
-// reproducible run to run and across ranks.
+// Every GEMM-shaped contraction takes f32 operands and accumulates in f32 through gemm_core.h:
+// by default as f32-accurate "bf16x6" products on v_mfma_f32_32x32x16_bf16 (each operand split
+// into three bf16 pieces, six piece products per 16-k step; gemm_core.h mfma_x6), or with
+// -DSMAML_X6=0 on v_mfma_f32_32x32x2_f32. All reductions are in a fixed order (no float
+// atomics), so results are bitwise reproducible run to run and across ranks.
 #include "kernels.h"
 #include "loaders.h"
 
@@ -316,13 +318,8 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   } else {
     const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
-    if constexpr (CfgGate::X6S && SMAML_PIECES) {
-      gemm_mainloop<CfgGate>(la, gate_bx<2>(wv.pm, {th + lo.wih, th + lo.whh}, {cin, H}, H), m0, n0, 0,
-                             cin + (t > 0 ? H : 0), acc, smem);
-    } else {
-      const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
-      gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
-    }
+    const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
+    gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   }
 
   fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
@@ -347,7 +344,6 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
     fl += 2.0 * w.Z * w.M * 4 * d.H * (dual ? k1 + k2 : k1);
   }
   wv.n = n;
-  wv.pm = w.pm;
   wv.off[n] = off;
   for (int q = n + 1; q <= MAX_LAYERS; ++q) wv.off[q] = off;
   return fl;
@@ -734,7 +730,7 @@ __global__ __launch_bounds__(128) void k_head_loss_small(const float* __restrict
                                                          float* __restrict__ pred, float* __restrict__ dpred,
                                                          float* __restrict__ lpart, int lblocks, int M, int H, int HfC,
                                                          int N, int Hf, int C, int yrow0, int yld, int B, float dscale) {
-  __shared__ float hs[SMAML_HEAD_MAX_H];
+  __shared__ __attribute__((aligned(16))) float hs[SMAML_HEAD_MAX_H];  // read as float4
   __shared__ float red[2];
   const int z = blockIdx.z, m = blockIdx.x, cc = threadIdx.x;
   const float* th = theta + (int64_t)z * tstride;
@@ -946,7 +942,6 @@ double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blo
     fl += (dual ? 3.0 : 1.0) * 2.0 * w.Z * w.M * 4 * d.H * d.H * segs;
   }
   wv.n = n;
-  wv.pm = w.pm;
   for (int q = n; q <= MAX_LAYERS; ++q) wv.off[q] = off;
   return fl;
 }
@@ -1108,7 +1103,6 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
   const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int z = bk.z;
   const int m0 = mb * CfgNN::BM, n0 = bk.y * CfgNN::BN;
-  if (m0 >= M) return;  // padding tile of the paired order
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;  // gates in
@@ -1134,19 +1128,9 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
         gemm_mainloop<CfgNN>(SegKC{{pn, nullptr, nullptr, nullptr}, {G4, 0, 0, 0}, M},
                              SegMC{{th + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, 0, G4, acc, smem);
     } else {
-      // paired order: odd layers take the recurrent segment first, so both readers of a shared
-      // dG cell (bwd_block) stream it in the same half of their K loops
-      const bool sw = wv.pair && (l & 1) && up && nx;
-      const SegKCt<2> la{{sw ? pn : (up ? pa : pn), sw ? pa : pn}, {G4, G4}, M};
-      const float* b0 = sw ? th + lo.whh : (up ? th + wih_up : th + lo.whh);
-      const float* b1 = sw ? th + wih_up : th + lo.whh;
-      if constexpr (CfgNN::X6S && SMAML_PIECES) {
-        if (ns && SMAML_DIAG_BWD != 2)
-          gemm_mainloop<CfgNN>(la, mc_bx<2>(wv.pm, {b0, b1}, {G4, G4}, H), m0, n0, 0, ns * G4, acc, smem);
-      } else {
-        const SegMCt<2> lb{{b0, b1}, {G4, G4}, H};
-        if (ns && SMAML_DIAG_BWD != 2) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
-      }
+      const SegKCt<2> la{{up ? pa : pn, pn}, {G4, G4}, M};
+      const SegMCt<2> lb{{up ? th + wih_up : th + lo.whh, th + lo.whh}, {G4, G4}, H};
+      if (ns && SMAML_DIAG_BWD != 2) gemm_mainloop<CfgNN>(la, lb, m0, n0, 0, ns * G4, acc, smem);
     }
   }
   if (SMAML_DIAG_BWD == 1) {  // timing diagnostic: GEMM phase only (keep the result live)
@@ -1304,17 +1288,12 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
   const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
-  const bool pair = w.kn.bwd_pair && !w.drop.lstm();
 #define SMAML_BWD_STEP(CFG, D_)                                                                               \
   SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
                             w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
   // threshold in 64-row tile units (the knob predates the 128-row tile)
   if ((int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min) {
     count_variant(w, V_BWD_BIG);
-    if (pair) {
-      bwd_wave(d, w, po, e, (ntm + 7) / 8 * 8, false, wv);
-      wv.pair = 1;
-    }
     dim3 grid(wv.off[wv.n], ntn, w.Z);
     if (w.drop.lstm()) {
       SMAML_BWD_STEP(CfgBwd, true);
@@ -1987,33 +1966,6 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
 }  // namespace smaml
 
 namespace smaml {
-__global__ __launch_bounds__(256) void k_split3(const float* __restrict__ x, int64_t n, int64_t plane,
-                                                uint16_t* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (4 * i + 3 < n) {
-    uint2 p0, p1, p2;
-    split4(ld4(x + 4 * i), p0, p1, p2);
-    *reinterpret_cast<uint2*>(dst + 4 * i) = p0;
-    *reinterpret_cast<uint2*>(dst + plane + 4 * i) = p1;
-    *reinterpret_cast<uint2*>(dst + 2 * plane + 4 * i) = p2;
-  } else {
-    for (int64_t e = 4 * i; e < n; ++e) {
-      const float v = x[e];
-      const uint32_t u0 = pk_bf16(v, 0.f);
-      const float r = v - __builtin_bit_cast(float, u0 << 16);
-      const uint32_t u1 = pk_bf16(r, 0.f);
-      const float q = r - __builtin_bit_cast(float, u1 << 16);
-      dst[e] = (uint16_t)u0;
-      dst[plane + e] = (uint16_t)u1;
-      dst[2 * plane + e] = (uint16_t)pk_bf16(q, 0.f);
-    }
-  }
-}
-void launch_split3(hipStream_t s, const float* x, int64_t n, int64_t plane, uint16_t* dst) {
-  const int64_t blocks = (n + 4 * 256 - 1) / (4 * 256);
-  k_split3<<<dim3((unsigned)blocks), 256, 0, s>>>(x, n, plane, dst);
-}
-
 // Product form per GEMM family as built (smaml_build_info): 0 = f32 MFMA, 1 = bf16x6 with the
 // split on the MFMA fragments, 2 = bf16x6 with the split staged at the LDS store.
 template <class C>

@@ -167,10 +167,6 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
-    else if constexpr (CfgGateD::X6S && SMAML_PIECES)
-      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
-                                          gate_bx<2>(wv.pm, {th + lo.wih, th + lo.whh}, {cin, wh}, H), m0, n0, 0,
-                                          cin + wh, ap, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
                                           SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, 0,
@@ -209,11 +205,6 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
-    else if constexpr (CfgGateD::X6S && SMAML_PIECES)
-      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
-                                          gate_bx<4>(wv.pm, {u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
-                                                     {cin, wh, wrx, wh}, H),
-                                          m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
                                           SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
@@ -509,7 +500,6 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int z = bk.z;
   const int m0 = mb * CfgNND::BM, n0 = bk.y * CfgNND::BN;
-  if (m0 >= M) return;  // padding tile of the paired order
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
@@ -550,23 +540,14 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                           SegMC{{th + lo.whh, nullptr}, {G4, 0}, H},
                                           SegMC{{u + lo.whh, nullptr}, {G4, 0}, H}, m0, n0, G4, 0, ap, at, smem);
     } else if (ns && SMAML_DIAG_BWDD != 2) {
-      // paired order (k_lstm_bwd_step): odd layers take the recurrent segment first
-      const bool sw = wv.pair && (l & 1) && up && nx;
-      const float* a0 = up && !sw ? dGAll + oa : dGz + on;
-      const float* r0 = up && !sw ? RGsAll + oa : RGz + on;
-      const float* a1 = sw ? dGAll + oa : dGz + on;
-      const float* r1 = sw ? RGsAll + oa : RGz + on;
-      const int64_t w0o = up && !sw ? wih_up : lo.whh, w1o = sw ? wih_up : lo.whh;
-      if constexpr (CfgNND::X6S && SMAML_PIECES)
-        gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, a1}, {G4, G4}, M}, SegKCt<2>{{r0, r1}, {G4, G4}, M},
-                                          mc_bx<2>(wv.pm, {th + w0o, th + w1o}, {G4, G4}, H),
-                                          mc_bx<2>(wv.pm, {u + w0o, u + w1o}, {G4, G4}, H), m0, n0, ns * G4, 0, ap,
-                                          at, smem);
-      else
-        gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, a1}, {G4, G4}, M}, SegKCt<2>{{r0, r1}, {G4, G4}, M},
-                                          SegMCt<2>{{th + w0o, th + w1o}, {G4, G4}, H},
-                                          SegMCt<2>{{u + w0o, u + w1o}, {G4, G4}, H}, m0, n0, ns * G4, 0, ap, at,
-                                          smem);
+      const float* a0 = up ? dGAll + oa : dGz + on;
+      const float* r0 = up ? RGsAll + oa : RGz + on;
+      const int64_t w0o = up ? wih_up : lo.whh;
+      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, dGz + on}, {G4, G4}, M},
+                                        SegKCt<2>{{r0, RGz + on}, {G4, G4}, M},
+                                        SegMCt<2>{{th + w0o, th + lo.whh}, {G4, G4}, H},
+                                        SegMCt<2>{{u + w0o, u + lo.whh}, {G4, G4}, H}, m0, n0, ns * G4, 0, ap, at,
+                                        smem);
     }
   }
   const bool first = (t == T - 1);
@@ -664,10 +645,6 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   const bool kept = w.primal_kept != 0;
   if ((int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min) {  // 64-row tile units
     count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
-    if (w.kn.bwd_pair && !w.drop.lstm()) {
-      bwd_wave(d, w, po, e, (ntm + 7) / 8 * 8, true, wv);
-      wv.pair = 1;
-    }
     if (kept)
       bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
     else

@@ -323,110 +323,6 @@ struct SegGateBt {
   }
 };
 
-// ---- pre-split parameter operands (PieceMap, staged split) ------------------------------------
-// The same element mapping as SegGateBt / SegMCt, reading the three bf16 planes of each segment
-// (q[s] = plane-0 piece of the segment's first element, ps[s] = plane stride) in items of 8
-// consecutive elements (one 16-B load per plane; gemm_core.h store_pieces).
-__device__ __forceinline__ uint4 ldp(const uint16_t* base, uint32_t elem) {
-  return *reinterpret_cast<const uint4*>(base + elem);
-}
-template <int NS>
-struct SegGateBx {
-  static constexpr bool kPieces = true;
-  const uint16_t* q[NS];
-  int64_t ps[NS];
-  int w[NS];
-  int H;
-  template <int ROWS, int PI, int NTH, bool KC, int BK>
-  __device__ __forceinline__ void fetch_pieces(int n0, int k0, uint4 (&r)[3][PI]) const {
-    static_assert(KC, "SegGateBx is a k-contiguous operand");
-    constexpr int ITEMS = ROWS * BK / 8;
-    const uint16_t* b = q[0];
-    int64_t st = ps[0];
-    int ws = w[0], kk = k0;
-#pragma unroll
-    for (int s = 1; s < NS; ++s)
-      if (kk >= ws) {
-        kk -= ws;
-        b = q[s];
-        st = ps[s];
-        ws = w[s];
-      }
-    b += kk;
-#pragma unroll
-    for (int i = 0; i < PI; ++i) {
-      const int f = (int)threadIdx.x + NTH * i;
-      if (ITEMS % NTH != 0 && f >= ITEMS) break;
-      const int n = n0 + f / (BK / 8);
-      const int ug = n >> 7, rem = n & 127;
-      const int j = min(ug * 32 + (rem & 31), H - 1);
-      const uint32_t e = (uint32_t)(((rem >> 5) * H + j) * ws + 8 * (f % (BK / 8)));
-      r[0][i] = ldp(b, e);
-      r[1][i] = ldp(b + st, e);
-      r[2][i] = ldp(b + 2 * st, e);
-    }
-  }
-};
-template <int NS>
-struct SegMCx {
-  static constexpr bool kPieces = true;
-  const uint16_t* q[NS];
-  int64_t ps[NS];
-  int K[NS];
-  int cols;
-  template <int ROWS, int PI, int NTH, bool KC, int BK>
-  __device__ __forceinline__ void fetch_pieces(int col0, int k0, uint4 (&r)[3][PI]) const {
-    static_assert(!KC, "SegMCx is an n-contiguous operand");
-    constexpr int ITEMS = ROWS * BK / 8;
-    const uint16_t* b = q[0];
-    int64_t st = ps[0];
-    int ks = K[0], kk = k0;
-#pragma unroll
-    for (int s = 1; s < NS; ++s)
-      if (kk >= ks) {
-        kk -= ks;
-        b = q[s];
-        st = ps[s];
-        ks = K[s];
-      }
-    b += (int64_t)kk * cols;
-#pragma unroll
-    for (int i = 0; i < PI; ++i) {
-      const int f = (int)threadIdx.x + NTH * i;
-      if (ITEMS % NTH != 0 && f >= ITEMS) break;
-      const int c = min(col0 + 8 * (f % (ROWS / 8)), cols - 8);
-      const uint32_t e = (uint32_t)((f / (ROWS / 8)) * cols + c);
-      r[0][i] = ldp(b, e);
-      r[1][i] = ldp(b + st, e);
-      r[2][i] = ldp(b + 2 * st, e);
-    }
-  }
-};
-template <int NS>
-__device__ __forceinline__ SegGateBx<NS> gate_bx(const PieceMap& pm, const float* const (&p)[NS], const int (&w)[NS],
-                                                 int H) {
-  SegGateBx<NS> r;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    r.q[s] = pm.find(p[s], r.ps[s]);
-    r.w[s] = w[s];
-  }
-  r.H = H;
-  return r;
-}
-template <int NS>
-__device__ __forceinline__ SegMCx<NS> mc_bx(const PieceMap& pm, const float* const (&p)[NS], const int (&K)[NS],
-                                            int cols) {
-  SegMCx<NS> r;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    r.q[s] = pm.find(p[s], r.ps[s]);
-    r.K[s] = K[s];
-  }
-  r.cols = cols;
-  return r;
-}
-
 // MC operand [K][cols] (cols contiguous) with zero rows at k >= K (split-K weight gradients: the
 // K tail is real, so it is zero-filled by a select, not clamped).
 struct MCKt {
@@ -658,18 +554,9 @@ __device__ __forceinline__ T wave_sel(const T (&a)[N], int p) {
     if (q == p) v = a[q];
   return v;
 }
-// BPTT diagonal block -> (problem p, row tile mb). Problems p and p+1 (layers l and l-1) share one
-// operand cell: dG(l, t+1) is p's recurrent segment and p+1's layer-above segment. In the paired
-// order (wv.pair) blocks are dealt 8 row tiles of each problem in turn, so row tile mb of p and of
-// p+1 are 8 linear ids apart -- same XCD (round robin), dispatched together -- and the second
-// reader of each shared dG row finds it in that XCD's L2. (Off: problem-major, as launched.)
+// BPTT diagonal block -> (problem p, row tile mb), problem-major as launched.
 template <class WV>
 __device__ __forceinline__ int bwd_block(const WV& wv, int bx, int& mb) {
-  if (wv.pair) {
-    const int per = 8 * wv.n, g = bx / per, r = bx - g * per;
-    mb = g * 8 + (r & 7);
-    return r >> 3;
-  }
   const int p = wave_index(wv, bx);
   mb = bx - wave_sel(wv.off, p);
   return p;

@@ -5,7 +5,7 @@ Constructor signature, attributes (``base_stgcn``, ``lstm``, ``output_layer``,
 (``extract_base_features``, ``forward``, ``get_trainable_parameters``,
 ``freeze_base_model``, ``unfreeze_base_model``) and state_dict keys follow
 ``hybrid_model.py:6-134``. ``forward`` runs the whole STGCN-LSTM forward in libsmaml.so:
-GCN x4 (fp32 MFMA, F3 semantics), the 4-layer LSTM batched over nodes (the reference's
+GCN x4 (f32 products on the MFMA pipe, F3 semantics), the 4-layer LSTM batched over nodes (the reference's
 per-node loop, F6, is one batched recurrence here), head. No CPU fallback.
 
 With grad enabled, ``forward`` is a ``torch.autograd.Function`` (``_HybridFn``): its backward

@@ -31,13 +31,30 @@ def reference_query_start(n_samples: int) -> int:
     return int(0.75 * min(600, n_samples))
 
 
+def query_starts(cfg: MamlConfig, n_samples: Sequence[int], support: Optional[int] = None) -> List[int]:
+    """First query sample of each task for ``MetaLearner.default_windows``: the reference split
+    (``reference_query_start``) when it lies past the S support samples the inner loop reads
+    ((k*B + b) mod S), else S itself, so the query batch never re-uses a support sample (the
+    reference, with 15 support samples, never meets this case; a stream shorter than about S/0.75
+    samples or S > 450 does). Raises ValueError when the B query samples do not fit the stream."""
+    S = support or cfg.support_samples or cfg.inner_steps * cfg.batch
+    out = []
+    for n in n_samples:
+        q0 = max(S, reference_query_start(n))
+        if q0 + cfg.batch > n:
+            raise ValueError(f"a task stream of {n} samples cannot hold {S} support samples followed by a "
+                             f"{cfg.batch}-sample query batch (need >= {S + cfg.batch}; see stream_len_for)")
+        out.append(q0)
+    return out
+
+
 def window_table(cfg: MamlConfig, n_tasks: int, support: Optional[int] = None,
                  query_start=None) -> np.ndarray:
     """int32 [(K+1)][tasks][B]: support step k uses samples (k*B + b) mod S (with B=1,
     S=15 this is the reference's 6 epochs x first 15 support samples, :124-127); the
     query batch uses samples q0 .. q0+B-1 (``query_ds[0]`` when B=1, :162-164). ``query_start``:
-    one int or one per task (default S; MetaLearner passes ``reference_query_start`` of each
-    task's stream)."""
+    one int or one per task (default S; MetaLearner passes ``query_starts`` of its tasks'
+    streams)."""
     K, B = cfg.inner_steps, cfg.batch
     S = support or cfg.support_samples or K * B
     q0 = np.broadcast_to(np.asarray(S if query_start is None else query_start, np.int64), (n_tasks,))
@@ -50,10 +67,12 @@ def window_table(cfg: MamlConfig, n_tasks: int, support: Optional[int] = None,
 
 def stream_len_for(cfg: MamlConfig, dims: ModelDims, support: Optional[int] = None) -> int:
     """Shortest feature stream whose reference split (``reference_query_start``) puts the query
-    batch after the S support samples, with B query samples available."""
+    batch after the S support samples, with B query samples available. For S > 450 the reference
+    split (75 % of at most 600 samples) cannot lie past S; the stream then holds S + B samples and
+    ``query_starts`` places the query batch at S."""
     S = support or cfg.support_samples or cfg.inner_steps * cfg.batch
     n = S + cfg.batch
-    while reference_query_start(n) < min(S, 450) or n - reference_query_start(n) < cfg.batch:
+    while reference_query_start(n) < min(S, 450) or n < max(S, reference_query_start(n)) + cfg.batch:
         n += 1
     return synth.t_total_for(n, dims.window_size, dims.forecast_horizon)
 
@@ -161,9 +180,10 @@ class MetaLearner:
 
     def default_windows(self) -> np.ndarray:
         """The window table meta_step uses without an explicit one: support samples
-        (k*B + b) mod S, query batch from ``reference_query_start`` of each task's stream."""
+        (k*B + b) mod S, query batch from ``query_starts`` (the reference split of each task's
+        stream, never inside the support samples)."""
         n = [synth.num_samples(f.shape[0], self.dims.window_size, self.dims.forecast_horizon) for f in self.tasks]
-        return window_table(self.cfg, len(self.tasks), query_start=[reference_query_start(x) for x in n])
+        return window_table(self.cfg, len(self.tasks), query_start=query_starts(self.cfg, n))
 
     def meta_step(self, windows: Optional[np.ndarray] = None, fast_out=None, sync=True,
                   lr: Optional[float] = None) -> StepResult:
