@@ -348,3 +348,43 @@ def test_evaluate_regional_matches_validate_adapted(golden_dir, name):
             want = float(z[f"{v}/{k}"])
             assert abs(res[v][k] - want) <= 1e-4 * abs(want), (v, k, res[v][k], want)
     assert abs(res["average_mse"] - float(z["average_mse"])) <= 1e-4 * float(z["average_mse"])
+
+
+@pytest.mark.parametrize("p_gcn", [0.0, 0.2])
+def test_fused_gcn_matches_per_layer(p_gcn):
+    """The fused GCN stack (k_gcn_mlp: rows t >= 1, all four convs in registers) and the t = 0 rows'
+    per-layer path against the all-rows per-layer kernel (gcn_fused 0): same features and
+    predictions up to summation order, the same dropout masks (conv1..conv3 at p_gcn), and at
+    p_gcn = 0 the oracle's GCN stack (hybrid_model.py:60-78) on every row."""
+    d = CONFIG2
+    P = synth.init_params(33, d, gcn_bias_scale=0.1)
+    Ptr, Pg, _ = split(P)
+    ei = grid_edges(d)
+    ctx = _capi.Context(d, 0)
+    ctx.set_graph(ei)
+    ctx.set_gcn_params(params.pack({k: torch.from_numpy(v) for k, v in Pg.items()}, d, which=1, device=DEV))
+    theta = params.pack({k: torch.from_numpy(v) for k, v in Ptr.items()}, d, device=DEV)
+    feats = synth.make_features(synth.task_seed(3), d.num_nodes, synth.t_total_for(8))
+    xs_np = [np.ascontiguousarray(synth.sample_xy(feats, i)[0]) for i in (0, 3, 7)]
+    xs = [torch.from_numpy(x).to(DEV) for x in xs_np]
+    st = _capi.stream_ptr(torch)
+    ctx.set_task_ids([5])
+    out = []
+    for fused in (1, 0):
+        ctx.set_option("gcn_fused", fused)
+        ctx.set_dropout(p_gcn, 0.0, 77)
+        pred = torch.empty(len(xs) * d.num_nodes * d.forecast_horizon, d.output_channels, device=DEV)
+        F = torch.empty(len(xs), d.window_size * d.num_nodes, d.hidden_channels, device=DEV)
+        ctx.forward(st, theta, xs, pred, F)
+        torch.cuda.synchronize()
+        out.append((F.cpu().numpy(), pred.cpu().numpy()))
+    (Ff, pf), (Fl, pl) = out
+    assert rel(Ff, Fl) < 2e-6 and rel(pf, pl) < 2e-6
+    # identical dropout masks: the zero patterns (dropout and ReLU) agree up to ReLU ties at rounding level
+    assert np.mean((Ff == 0) != (Fl == 0)) < 1e-5
+    if p_gcn == 0.0:
+        PT = refcpu.to_torch(P)
+        Pgt = {k: v for k, v in PT.items() if k.startswith("base_stgcn")}
+        for i, x in enumerate(xs_np):
+            ref = refcpu.stgcn_features(torch.from_numpy(x), torch.from_numpy(ei).long(), Pgt).numpy()
+            assert rel(Ff[i], ref) < 1e-5

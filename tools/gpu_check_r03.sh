@@ -17,3 +17,13 @@ if [ -n "${BENCH:-1}" ]; then
   timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
   tail -1 gpurun_out/${TAG}_bench.log | cut -c1-400
 fi
+if [ -n "${AB_VARIANTS:-}" ]; then
+  : > gpurun_out/${TAG}_ab.log
+  for round in $(seq 1 ${AB_ROUNDS:-2}); do
+    for v in libsmaml.so ${AB_VARIANTS}; do
+      SMAML_LIB=weatherforecast_stgcn_maml_amd/$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-sample-steps 0 --adapt-epochs 0 ${AB_BENCH_ARGS:-} > gpurun_out/ab_tmp.log 2>&1 || exit $?
+      echo "$v $(tail -1 gpurun_out/ab_tmp.log)" >> gpurun_out/${TAG}_ab.log
+    done
+  done
+  python tools/ab_summary.py gpurun_out/${TAG}_ab.log
+fi

@@ -220,7 +220,8 @@ struct smaml_ctx {
   Staging stage;
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
-  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS};
+  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
+           SMAML_GCN_FUSED};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -237,6 +238,9 @@ struct smaml_ctx {
   // batch-1 adaptation: GCN features per window of task 0 (the frozen GCN stack without dropout
   // is a pure function of the window, F2), filled on first use and reused by later epochs.
   // Invalidated by smaml_set_graph / _set_gcn_params / _set_tasks.
+  char* gcn_wimg = nullptr;
+  unsigned* bar = nullptr;    // grid-barrier arrival counter of the cooperative bookkeeping kernels
+  unsigned bar_count = 0;     // arrivals so far (host mirror: launches are stream-ordered)  // pre-split GCN weight images of the fused t >= 1 GCN (kernels_gcn.hip)
   float* ad_F = nullptr;
   int64_t ad_cap = 0;              // windows the cache holds
   std::vector<uint8_t> ad_valid;   // per window start
@@ -565,7 +569,9 @@ void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
 }
 
-// GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc].
+// GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
+// rows t >= 1 (no neighbours, F3) run all four convs in one launch (k_gcn_mlp, activations kept in
+// registers), the t = 0 rows (ELL gather) four per-layer launches over N-row blocks.
 int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
   const Dims& d = c->d;
   Work& w = c->w;
@@ -573,6 +579,30 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
   const int zb = w.Z * w.B;
   const float* src = nullptr;
   float* bufs[2] = {w.gcnA, w.gcnB};
+  if (gcn_mlp_supported(d) && c->kn.gcn_fused) {
+    if (!c->gcn_wimg) HIP_TRY(hipMalloc((void**)&c->gcn_wimg, gcn_wimg_bytes(d)));
+    GcnWOff wo;
+    for (int k = 0; k < 4; ++k) {
+      wo.w[k] = c->go.w[k];
+      wo.b[k] = c->go.b[k];
+    }
+    // the GCN parameters may change between calls (smaml_set_gcn_params keeps the pointer): re-split
+    TIMED(c, s, C_MISC, 0, launch_gcn_wsplit(s, d, c->gcn, wo, c->gcn_wimg));
+    const double rows1 = (double)zb * (d.T - 1) * d.N;
+    TIMED(c, s, C_GCN, 2.0 * rows1 * d.Hc * (d.Cin0 + 3.0 * d.Hc),
+          launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop));
+    for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks, masks indexed as rows of T*N-row samples
+      const bool last = k == 3;
+      float* dst = last ? w.F : bufs[k & 1];
+      TIMED(c, s, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
+            launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
+                             c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
+                             d.N, d.N, &w.drop, rps));
+      src = dst;
+    }
+    HIP_TRY(hipGetLastError());
+    return SMAML_OK;
+  }
   for (int k = 0; k < 4; ++k) {
     const bool last = k == 3;
     float* dst = last ? w.F : bufs[k & 1];
@@ -677,19 +707,7 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
                      const float* const* xtab_dev, bool gcn_cached) {
   const Dims& d = c->d;
   Work& w = c->w;
-  const int rps = d.T * d.N;
-  const int zb = w.Z * w.B;
-  const float* src = nullptr;
-  float* bufs[2] = {w.gcnA, w.gcnB};
-  for (int k = 0; k < 4 && !gcn_cached; ++k) {
-    const bool last = k == 3;
-    float* dst = last ? w.F : bufs[k & 1];
-    TIMED(c, s, C_GCN, 2.0 * zb * rps * c->go.cin[k] * d.Hc,
-          launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
-                           c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
-                           rps, d.N, &w.drop));
-    src = dst;
-  }
+  if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
@@ -744,6 +762,16 @@ int require_ready(smaml_ctx* c) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// the cooperative bookkeeping kernels' barrier counter (zeroed once; only ever counts up)
+int ensure_bar(smaml_ctx* c) {
+  if (c->bar) return SMAML_OK;
+  HIP_TRY(hipMalloc((void**)&c->bar, sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->bar, 0, sizeof(unsigned)));
+  HIP_TRY(hipDeviceSynchronize());
+  c->bar_count = 0;
+  return SMAML_OK;
+}
 
 }  // namespace
 
@@ -854,6 +882,8 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->so_norm) (void)hipFree(c->so_norm);
   if (c->so_coef) (void)hipFree(c->so_coef);
   if (c->so_F) (void)hipFree(c->so_F);
+  if (c->gcn_wimg) (void)hipFree(c->gcn_wimg);
+  if (c->bar) (void)hipFree(c->bar);
   ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
   for (auto& r : c->tm.recs) {
@@ -990,6 +1020,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const Dims& d = c->d;
   const int Z = (int)c->feats.size();
   const int B = batch;
+  TRY(ensure_bar(c));
   TRY(reserve(c, Z, B, order == 2));
   if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z, B));
   if (order == 2) TRY(ensure_keep(c, steps, Z, B));
@@ -1039,18 +1070,18 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
     TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
     TRY(run_backward(c, s, c->fast, P, c->grad));
-    TIMED(c, s, C_MISC, 0, launch_sqsum(s, c->grad, P, Z, c->w.sqpart));
+    // the inner SGD step (clip_grad_norm_ + SGD) of every task: one kernel
     if (so) {
       HIP_TRY(hipMemcpyAsync(c->so_grad + (int64_t)k * Z * P, c->grad, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
       TIMED(c, s, C_MISC, 0,
-            launch_clip_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm, c->so_norm + (int64_t)k * Z,
-                            c->so_coef + (int64_t)k * Z));
+            HIP_TRY(launch_inner_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
+                                     c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z, c->bar, c->bar_count)));
       if (norms)
         HIP_TRY(hipMemcpyAsync(norms + (int64_t)k * Z, c->so_norm + (int64_t)k * Z, Z * 4, hipMemcpyDeviceToDevice, s));
     } else {
       TIMED(c, s, C_MISC, 0,
-            launch_clip_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
-                            norms ? norms + (int64_t)k * Z : nullptr, nullptr));
+            HIP_TRY(launch_inner_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
+                                     norms ? norms + (int64_t)k * Z : nullptr, nullptr, c->bar, c->bar_count)));
     }
   }
   const float* const* xq = c->xtab + (int64_t)steps * Z * B;
@@ -1072,15 +1103,16 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     TRY(run_backward(c, s, c->fast, P, c->grad));
     use_primal(c, SET_MAIN);
     float* V = c->grad;
+    // w_{K-1}: the clip-adjusted direction of the last inner step at v_K (one kernel: dot + direction)
     if (steps > 0)
-      TIMED(c, s, C_MISC, 0, launch_dot(s, c->so_grad + (int64_t)(steps - 1) * Z * P, V, P, Z, c->w.sqpart));
+      TIMED(c, s, C_MISC, 0,
+            HIP_TRY(launch_sweep_update(s, V, nullptr, 0.f, c->so_grad + (int64_t)(steps - 1) * Z * P, P, Z,
+                                        c->w.sqpart, c->so_norm + (int64_t)(steps - 1) * Z,
+                                        c->so_coef + (int64_t)(steps - 1) * Z, max_norm, c->so_u, c->bar,
+                                        c->bar_count)));
     for (int k = steps - 1; k >= 0; --k) {
       const float* th = c->so_theta + (int64_t)k * Z * P;
-      const float* gk = c->so_grad + (int64_t)k * Z * P;
       const float* const* xt = c->xtab + (int64_t)k * Z * B;
-      TIMED(c, s, C_MISC, 0,
-            launch_so_dir_only(s, V, gk, P, Z, c->w.sqpart, c->so_norm + (int64_t)k * Z,
-                               c->so_coef + (int64_t)k * Z, max_norm, c->so_u));
       c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
       const int slot = steps - 1 - k;
       use_primal(c, slot < nkeep ? slot : SET_MAIN);
@@ -1089,9 +1121,12 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
-      if (k > 0)  // v_k = v_{k+1} - lr H_k w_k, and step k-1's dot g_{k-1} . v_k in the same pass
+      if (k > 0)  // v_k = v_{k+1} - lr H_k w_k and w_{k-1} (dot g_{k-1} . v_k, direction): one kernel
         TIMED(c, s, C_MISC, 0,
-              launch_axpy_dot(s, V, c->so_hu, -inner_lr, c->so_grad + (int64_t)(k - 1) * Z * P, P, Z, c->w.sqpart));
+              HIP_TRY(launch_sweep_update(s, V, c->so_hu, -inner_lr, c->so_grad + (int64_t)(k - 1) * Z * P, P, Z,
+                                          c->w.sqpart, c->so_norm + (int64_t)(k - 1) * Z,
+                                          c->so_coef + (int64_t)(k - 1) * Z, max_norm, c->so_u, c->bar,
+                                          c->bar_count)));
       else
         TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
       c->w.primal_kept = 0;
@@ -1161,11 +1196,12 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     } else {
       TRY(run_forward(c, s, theta, 0, xt));
     }
-    launch_head_loss(s, d, c->w, theta, 0, c->po, xt, 2.f * inv, true);
-    launch_loss_final(s, c->w, inv, losses + k);
+    TIMED(c, s, C_HEAD, 2.0 * c->w.M * d.HfC * d.H, launch_head_loss(s, d, c->w, theta, 0, c->po, xt, 2.f * inv, true));
+    TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + k));
     TRY(run_backward(c, s, theta, 0, c->grad));
-    launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
-                   weight_decay, max_norm);
+    TIMED(c, s, C_MISC, 0,
+          launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
+                         weight_decay, max_norm));
   }
   c->w.F = c->F_main;
   c->w.drop = Drop{};
@@ -1224,6 +1260,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.split_max = (int)std::min<int64_t>(value, 64);
   } else if (k == "wgrad_group_max_rows" && value >= 0) {
     c->kn.wgrad_group_max_rows = (int)std::min<int64_t>(value, 1 << 30);
+  } else if (k == "gcn_fused" && (value == 0 || value == 1)) {
+    c->kn.gcn_fused = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {
@@ -1367,9 +1405,10 @@ int smaml_clip_sgd(smaml_ctx* c, void* stream, float* theta, const float* grad, 
   if (!c || !theta || !grad || ntasks <= 0) return fail(SMAML_EINVAL, "bad clip_sgd arguments");
   TRY(ensure_device(c));
   if (ntasks > c->z_cap) TRY(reserve(c, ntasks, 1));
+  TRY(ensure_bar(c));
   hipStream_t s = (hipStream_t)stream;
-  launch_sqsum(s, grad, c->po.P, ntasks, c->w.sqpart);
-  launch_clip_sgd(s, theta, grad, c->po.P, ntasks, c->w.sqpart, lr, max_norm, norms, nullptr);
+  HIP_TRY(launch_inner_sgd(s, theta, grad, c->po.P, ntasks, c->w.sqpart, lr, max_norm, norms, nullptr, c->bar,
+                           c->bar_count));
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }

@@ -108,7 +108,11 @@ struct Knobs {
   int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
   int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
   int wgrad_group_wgs;       // workgroups that grouped launch aims for
+  int gcn_fused;             // 1: GCN rows t >= 1 through the fused four-layer kernel (k_gcn_mlp)
 };
+#ifndef SMAML_GCN_FUSED
+#define SMAML_GCN_FUSED 1
+#endif
 #ifndef SMAML_WGRAD_GROUP_ROWS
 #define SMAML_WGRAD_GROUP_ROWS 2048
 #endif
@@ -150,6 +154,21 @@ inline void count_variant(const Work& w, Variant v) {
 }
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
+
+// Grid-wide barrier of a cooperative launch (every block co-resident): `bar` counts block arrivals
+// since the context was made (never reset); the launch passes the count its last arrival reaches.
+// Release: the block's stores are made visible before it arrives; acquire: the waiting lane's
+// agent-scope load invalidates this CU's L1, so the block then reads the other blocks' results.
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    while ((int)(__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
+      __builtin_amdgcn_s_sleep(2);
+  }
+  __syncthreads();
+}
+int coop_blocks(int items);  // blocks of a cooperative bookkeeping launch over `items` (task, chunk) items
 #ifndef SMAML_WGRAD_MAXSPLIT
 #define SMAML_WGRAD_MAXSPLIT 128  // split-K slices per weight gradient (partial-slab capacity)
 #endif
@@ -182,10 +201,50 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
 const char* products_info();  // product form per GEMM family as built (kernels.hip)
 
 // ---- launchers (kernels.hip) ----
+// drop_rps: rows per sample of the dropout element index (default rows_per_sample; the t = 0 path of
+// run_gcn runs N-row "samples" but indexes masks as the T*N-row samples they belong to)
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
                       const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
                       const float* b, int cin, int cout, const int* ell_c, const float* ell_v, int rows_per_sample,
-                      int ell_rows, const Drop* drop = nullptr);
+                      int ell_rows, const Drop* drop = nullptr, int drop_rps = 0);
+
+// Exact unsigned division by a run-time invariant d for n < 2^31 (one 64-bit multiply):
+// m = ceil(2^(32+s) / d), s = ceil(log2 d)  =>  n / d == (n * m) >> (32 + s).
+struct FastDiv {
+  uint64_t m;
+  uint32_t s;
+  uint32_t d;
+  FastDiv() = default;
+  __host__ explicit FastDiv(uint32_t dd) : d(dd) {
+    s = 0;
+    while ((1ull << s) < dd) ++s;
+    m = (uint64_t)((((unsigned __int128)1 << (32 + s)) + dd - 1) / dd);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)(((unsigned __int128)n * m) >> (32 + s));
+  }
+};
+
+// ---- fused GCN stack for the rows t >= 1 (kernels_gcn.hip) ----
+struct GcnWOff {  // offsets of conv{1..4}.lin.weight / conv{1..4}.bias in the GCN parameter vector
+  int64_t w[4], b[4];
+};
+struct GcnMlpArgs {
+  const float* const* xtab;  // [Z*B] sample window pointers ([T*N][Cin0] each)
+  const float* gcn;          // GCN parameter vector (biases)
+  GcnWOff wo;
+  const char* wimg;          // pre-split W images (launch_gcn_wsplit)
+  float* F;                  // [Z][T][B*N][Hc]
+  int64_t R1, M;             // rows t >= 1 over all samples; B*N
+  FastDiv rows_div, b_div, n_div;
+  int rows1, N, T, B, cin0, ks1;
+  Drop dr;
+};
+bool gcn_mlp_supported(const Dims& d);
+int64_t gcn_wimg_bytes(const Dims& d);
+void launch_gcn_wsplit(hipStream_t s, const Dims& d, const float* gcn, const GcnWOff& wo, char* img);
+void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
+                    const GcnWOff& wo, const char* img, float* F, const Drop* drop);
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
@@ -252,9 +311,15 @@ struct WgMulti {
 void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs);
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
-void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part);
-void launch_clip_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, const double* part,
-                     float lr, float max_norm, float* norm_out, float* coef_out);
+// clip_grad_norm_ + SGD of every task as one cooperative kernel (k_inner_sgd); bar_count: the
+// context's running barrier-arrival count (advanced here)
+hipError_t launch_inner_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, double* part, float lr,
+                            float max_norm, float* norm_out, float* coef_out, unsigned* bar, unsigned& bar_count);
+// second-order sweep bookkeeping as one cooperative kernel (k_sweep_update): v += alpha x (x may be
+// null), U = clip-adjusted direction of (G, norms, coefs) at v
+hipError_t launch_sweep_update(hipStream_t s, float* V, const float* X, float alpha, const float* G, int64_t P, int Z,
+                               double* part, const float* norms, const float* coefs, float max_norm, float* U,
+                               unsigned* bar, unsigned& bar_count);
 void launch_sum_tasks(hipStream_t s, const float* g, int64_t P, int Z, float* out);
 void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float* out);
 void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
@@ -273,15 +338,6 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
                          int64_t tstride, const ParamOff& po);
 void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
                                const float* U, int64_t tstride, const ParamOff& po);
-void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,
-                   const float* coefs, float max_norm, float* U);
 void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha);
-// the second-order sweep's bookkeeping in two launches per inner step: dot partials g . v
-// (launch_dot for the first step, then fused into the previous step's v update), then u
-void launch_dot(hipStream_t s, const float* G, const float* V, int64_t P, int Z, double* part);
-void launch_axpy_dot(hipStream_t s, float* V, const float* X, float alpha, const float* Gn, int64_t P, int Z,
-                     double* part);
-void launch_so_dir_only(hipStream_t s, const float* V, const float* G, int64_t P, int Z, const double* part,
-                        const float* norms, const float* coefs, float max_norm, float* U);
 
 }  // namespace smaml

@@ -112,7 +112,7 @@ using CfgGcn = GemmCfg<128, 256, 2, 4, true, true, SMAML_GCN_BK, SMAML_X6_GCN>;
 __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC lb, const float* __restrict__ bias,
                                                            float* __restrict__ out, int cout, int remap, int relu,
                                                            int T, int N, int B, FastDiv ndiv, FastDiv bdiv, Drop dr,
-                                                           uint32_t dsite) {
+                                                           uint32_t dsite, int drps) {
   __shared__ float smem[CfgGcn::SMEM_FLOATS];
   const int m0 = blockIdx.x * CfgGcn::BM, n0 = blockIdx.y * CfgGcn::BN;
   Acc<CfgGcn> acc;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
       if (dr.gcn()) {
         const int g = (int)la.rps_div.div((uint32_t)row), q = row - g * la.rps;
         const int z = (int)bdiv.div((uint32_t)g), s = g - z * B;
-        didx = (((uint64_t)dr.task_id[z] * B + s) * la.rps + q) * cout;
+        didx = (((uint64_t)dr.task_id[z] * B + s) * drps + q) * cout;
       }
       int64_t orow = row;
       if (remap) {  // [g][t*N+n] -> [z][t][s*N+n]
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(CfgGcn::NTH) void k_gcn_layer(GcnA la, RowMajorKC l
 void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, const float* const* xtab,
                       const float* src, float* dst, bool remap_lstm, bool relu, const float* W,
                       const float* b, int cin, int cout, const int* ell_c, const float* ell_v,
-                      int rows_per_sample, int ell_rows, const Drop* drop) {
+                      int rows_per_sample, int ell_rows, const Drop* drop, int drop_rps) {
   // train-mode dropout after the ReLU of conv1..conv3 (hybrid_model.py:67,70,73)
   Drop dr{};
   uint32_t dsite = 0;
@@ -193,7 +193,8 @@ void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, co
   RowMajorKC lb{W, cout, cin};
   dim3 grid((la.R + CfgGcn::BM - 1) / CfgGcn::BM, (cout + CfgGcn::BN - 1) / CfgGcn::BN);
   k_gcn_layer<<<grid, CfgGcn::NTH, 0, s>>>(la, lb, b, dst, cout, remap_lstm ? 1 : 0, relu ? 1 : 0, d.T, d.N, B,
-                                           FastDiv((uint32_t)d.N), FastDiv((uint32_t)B), dr, dsite);
+                                           FastDiv((uint32_t)d.N), FastDiv((uint32_t)B), dr, dsite,
+                                           drop_rps > 0 ? drop_rps : rows_per_sample);
 }
 
 // ====================================================================================
@@ -1837,9 +1838,6 @@ __global__ void k_sqsum(const float* __restrict__ g, int64_t P, double* __restri
   if (threadIdx.x == 0) part[(int64_t)z * SQB + blockIdx.x] = s;
 }
 
-void launch_sqsum(hipStream_t s, const float* g, int64_t P, int Z, double* part) {
-  k_sqsum<<<dim3(SQB, Z), NT, 0, s>>>(g, P, part);
-}
 
 __device__ __forceinline__ float clip_coef_from(const double* part, float max_norm, float* total_out) {
   double t = 0.0;
@@ -1850,29 +1848,57 @@ __device__ __forceinline__ float clip_coef_from(const double* part, float max_no
   return coef < 1.f ? coef : 1.f;
 }
 
-__global__ void k_clip_sgd(float* __restrict__ theta, const float* __restrict__ g, int64_t P,
-                           const double* __restrict__ part, float lr, float max_norm, float* norm_out,
-                           float* coef_out) {
-  const int z = blockIdx.y;
-  float total;
-  const float coef = clip_coef_from(part + (int64_t)z * SQB, max_norm, &total);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (norm_out) norm_out[z] = total;
-    if (coef_out) coef_out[z] = coef;
+
+
+// The inner SGD step as ONE kernel (train_hybrid_maml_v5.py:135-139: clip_grad_norm_ + SGD): every
+// block computes the fp64 squared-norm partials of its (task, chunk) items -- the partition and order
+// of k_sqsum -- then, after a grid barrier, each task's clip coefficient from its SQB partials in
+// order and the SGD update of the same chunks (still in L2). Bitwise equal to k_sqsum + k_clip_sgd.
+// Launched cooperatively (every block co-resident); `bar` counts arrivals since the context was
+// made and `target` is the count after this launch's.
+__global__ __launch_bounds__(NT) void k_inner_sgd(float* __restrict__ theta, const float* __restrict__ g, int64_t P,
+                                                  int Z, double* __restrict__ part, float lr, float max_norm,
+                                                  float* norm_out, float* coef_out, unsigned* bar, unsigned target) {
+  __shared__ double red[NT / 64];
+  const int nit = SQB * Z;
+  const int64_t per = (P + SQB - 1) / SQB;
+  for (int it = blockIdx.x; it < nit; it += gridDim.x) {
+    const int z = it / SQB, b = it - z * SQB;
+    const float* gz = g + (int64_t)z * P;
+    const int64_t beg = (int64_t)b * per, end = beg + per < P ? beg + per : P;
+    double acc = 0.0;
+    for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
+      const double v = gz[i];
+      acc += v * v;
+    }
+    const double sum = block_sum_d(acc, red);
+    if (threadIdx.x == 0) part[it] = sum;
   }
-  float* tz = theta + (int64_t)z * P;
-  const float* gz = g + (int64_t)z * P;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
-    const float gc = gz[i] * coef;
-    tz[i] = fmaf(-lr, gc, tz[i]);
+  grid_barrier(bar, target);
+  for (int it = blockIdx.x; it < nit; it += gridDim.x) {
+    const int z = it / SQB, b = it - z * SQB;
+    float total;
+    const float coef = clip_coef_from(part + (int64_t)z * SQB, max_norm, &total);
+    if (b == 0 && threadIdx.x == 0) {
+      if (norm_out) norm_out[z] = total;
+      if (coef_out) coef_out[z] = coef;
+    }
+    float* tz = theta + (int64_t)z * P;
+    const float* gz = g + (int64_t)z * P;
+    const int64_t beg = (int64_t)b * per, end = beg + per < P ? beg + per : P;
+    for (int64_t i = beg + threadIdx.x; i < end; i += NT) tz[i] = fmaf(-lr, gz[i] * coef, tz[i]);
   }
 }
 
-void launch_clip_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, const double* part,
-                     float lr, float max_norm, float* norm_out, float* coef_out) {
-  int nb = (int)((P + 4 * NT - 1) / (4 * NT));
-  if (nb > 1024) nb = 1024;
-  k_clip_sgd<<<dim3(nb, Z), NT, 0, s>>>(theta, g, P, part, lr, max_norm, norm_out, coef_out);
+int coop_blocks(int items) { return items < 1024 ? items : 1024; }
+
+hipError_t launch_inner_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, double* part, float lr,
+                            float max_norm, float* norm_out, float* coef_out, unsigned* bar, unsigned& bar_count) {
+  const int nb = coop_blocks(SQB * Z);
+  bar_count += (unsigned)nb;
+  unsigned target = bar_count;
+  void* args[] = {&theta, &g, &P, &Z, &part, &lr, &max_norm, &norm_out, &coef_out, &bar, &target};
+  return hipLaunchCooperativeKernel((const void*)k_inner_sgd, dim3(nb), dim3(NT), args, 0, s);
 }
 
 __global__ void k_sum_tasks(const float* __restrict__ g, int64_t P, int Z, float* __restrict__ out) {

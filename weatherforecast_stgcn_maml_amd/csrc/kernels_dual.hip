@@ -661,107 +661,88 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
 }
 
 // ====================================================================================
-// Meta-backward bookkeeping (per task z):
-//   dot[z] = g_k . v                                     (fp64 partials, fixed order)
-//   w = c_k v - [c_k < 1] * max_norm * dot / (n (n + 1e-6)^2) * g_k
-//     = (d(c_k g_k)/d theta_k)^T v expressed as H_k w  (clip_grad_norm_ derivative)
-//   v -= lr * H_k w
-__global__ void k_dot(const float* __restrict__ a, const float* __restrict__ b, int64_t P, double* __restrict__ part) {
-  __shared__ double red[NT / 64];
-  const int z = blockIdx.y;
-  const float* az = a + (int64_t)z * P;
-  const float* bz = b + (int64_t)z * P;
-  const int64_t per = (P + SQB - 1) / SQB;
-  const int64_t beg = (int64_t)blockIdx.x * per, end = beg + per < P ? beg + per : P;
-  double acc = 0.0;
-  for (int64_t i = beg + threadIdx.x; i < end; i += NT) acc += (double)az[i] * (double)bz[i];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int i = 0; i < NT / 64; ++i) s += red[i];
-    part[(int64_t)z * SQB + blockIdx.x] = s;
-  }
-}
-
-__global__ void k_so_dir(const float* __restrict__ V, const float* __restrict__ G, int64_t P,
-                         const double* __restrict__ part, const float* __restrict__ norms,
-                         const float* __restrict__ coefs, float max_norm, float* __restrict__ Uo) {
-  const int z = blockIdx.y;
-  double dot = 0.0;
-  for (int i = 0; i < SQB; ++i) dot += part[(int64_t)z * SQB + i];
-  const float n = norms[z], c = coefs[z];
-  float beta = 0.f;
-  if (c < 1.f && n > 0.f) {
-    const double ne = (double)n + 1e-6;
-    beta = (float)((double)max_norm * dot / ((double)n * ne * ne));
-  }
-  const float* vz = V + (int64_t)z * P;
-  const float* gz = G + (int64_t)z * P;
-  float* uz = Uo + (int64_t)z * P;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x)
-    uz[i] = c * vz[i] - beta * gz[i];
-}
-
+// Meta-backward bookkeeping (per task z), the derivative of clip_grad_norm_ + SGD
+// (train_hybrid_maml_v5.py:135-139) through inner step k:
+//   w = c_k v - [c_k < 1] * max_norm * (g_k . v) / (n (n + 1e-6)^2) * g_k,   v -= lr * H_k w
 __global__ void k_axpy(float* __restrict__ V, const float* __restrict__ X, int64_t n, float alpha) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     V[i] = fmaf(alpha, X[i], V[i]);
 }
 
-// v += alpha * x, fused with the next inner step's dot partials g_next . v (same fixed partition
-// and order as k_dot): one pass over v instead of two launches.
-__global__ void k_axpy_dot(float* __restrict__ V, const float* __restrict__ X, float alpha,
-                           const float* __restrict__ Gn, int64_t P, double* __restrict__ part) {
+// The second-order sweep's per-parameter update of one inner step as ONE kernel:
+//   v += alpha * x (x = H_k w_k; skipped when x is null), dot = g . v (fp64 partials over SQB
+//   fixed chunks per task, summed in chunk order), grid barrier, then
+//   U = c v - [c < 1] max_norm dot / (n (n + 1e-6)^2) g
+// with (g, n, c) those of the inner step the sweep visits next (round 2 ran this as two launches,
+// k_axpy_dot + k_so_dir, with the same partition and order). Cooperative launch; see k_inner_sgd
+// for the barrier counter.
+__global__ __launch_bounds__(NT) void k_sweep_update(float* __restrict__ V, const float* __restrict__ X, float alpha,
+                                                     const float* __restrict__ G, int64_t P, int Z,
+                                                     double* __restrict__ part, const float* __restrict__ norms,
+                                                     const float* __restrict__ coefs, float max_norm,
+                                                     float* __restrict__ Uo, unsigned* bar, unsigned target) {
   __shared__ double red[NT / 64];
-  const int z = blockIdx.y;
-  float* vz = V + (int64_t)z * P;
-  const float* xz = X + (int64_t)z * P;
-  const float* gz = Gn + (int64_t)z * P;
+  const int nit = SQB * Z;
   const int64_t per = (P + SQB - 1) / SQB;
-  const int64_t beg = (int64_t)blockIdx.x * per, end = beg + per < P ? beg + per : P;
-  double acc = 0.0;
-  for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
-    const float v = fmaf(alpha, xz[i], vz[i]);
-    vz[i] = v;
-    acc += (double)gz[i] * (double)v;
-  }
+  for (int it = blockIdx.x; it < nit; it += gridDim.x) {
+    const int z = it / SQB, b = it - z * SQB;
+    float* vz = V + (int64_t)z * P;
+    const float* gz = G + (int64_t)z * P;
+    const int64_t beg = (int64_t)b * per, end = beg + per < P ? beg + per : P;
+    double acc = 0.0;
+    if (X) {
+      const float* xz = X + (int64_t)z * P;
+      for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
+        const float v = fmaf(alpha, xz[i], vz[i]);
+        vz[i] = v;
+        acc += (double)gz[i] * (double)v;
+      }
+    } else {
+      for (int64_t i = beg + threadIdx.x; i < end; i += NT) acc += (double)gz[i] * (double)vz[i];
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double sum = 0.0;
-    for (int i = 0; i < NT / 64; ++i) sum += red[i];
-    part[(int64_t)z * SQB + blockIdx.x] = sum;
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int i = 0; i < NT / 64; ++i) sum += red[i];
+      part[it] = sum;
+    }
+  }
+  grid_barrier(bar, target);
+  for (int it = blockIdx.x; it < nit; it += gridDim.x) {
+    const int z = it / SQB, b = it - z * SQB;
+    double dot = 0.0;
+    for (int i = 0; i < SQB; ++i) dot += part[(int64_t)z * SQB + i];
+    const float n = norms[z], c = coefs[z];
+    float beta = 0.f;
+    if (c < 1.f && n > 0.f) {
+      const double ne = (double)n + 1e-6;
+      beta = (float)((double)max_norm * dot / ((double)n * ne * ne));
+    }
+    const float* vz = V + (int64_t)z * P;
+    const float* gz = G + (int64_t)z * P;
+    float* uz = Uo + (int64_t)z * P;
+    const int64_t beg = (int64_t)b * per, end = beg + per < P ? beg + per : P;
+    for (int64_t i = beg + threadIdx.x; i < end; i += NT) uz[i] = c * vz[i] - beta * gz[i];
   }
 }
 
-void launch_dot(hipStream_t s, const float* G, const float* V, int64_t P, int Z, double* part) {
-  k_dot<<<dim3(SQB, Z), NT, 0, s>>>(G, V, P, part);
+hipError_t launch_sweep_update(hipStream_t s, float* V, const float* X, float alpha, const float* G, int64_t P, int Z,
+                               double* part, const float* norms, const float* coefs, float max_norm, float* U,
+                               unsigned* bar, unsigned& bar_count) {
+  const int nb = coop_blocks(SQB * Z);
+  bar_count += (unsigned)nb;
+  unsigned target = bar_count;
+  void* args[] = {&V, &X, &alpha, &G, &P, &Z, &part, &norms, &coefs, &max_norm, &U, &bar, &target};
+  return hipLaunchCooperativeKernel((const void*)k_sweep_update, dim3(nb), dim3(NT), args, 0, s);
 }
 
-void launch_axpy_dot(hipStream_t s, float* V, const float* X, float alpha, const float* Gn, int64_t P, int Z,
-                     double* part) {
-  k_axpy_dot<<<dim3(SQB, Z), NT, 0, s>>>(V, X, alpha, Gn, P, part);
-}
 
-// dot partials already in `part` (launch_dot / launch_axpy_dot)
-void launch_so_dir_only(hipStream_t s, const float* V, const float* G, int64_t P, int Z, const double* part,
-                        const float* norms, const float* coefs, float max_norm, float* U) {
-  int nb = (int)((P + NT - 1) / NT);
-  if (nb > 1024) nb = 1024;
-  k_so_dir<<<dim3(nb, Z), NT, 0, s>>>(V, G, P, part, norms, coefs, max_norm, U);
-}
 
-void launch_so_dir(hipStream_t s, const float* V, const float* G, int64_t P, int Z, double* part, const float* norms,
-                   const float* coefs, float max_norm, float* U) {
-  k_dot<<<dim3(SQB, Z), NT, 0, s>>>(G, V, P, part);
-  int nb = (int)((P + NT - 1) / NT);
-  if (nb > 1024) nb = 1024;
-  k_so_dir<<<dim3(nb, Z), NT, 0, s>>>(V, G, P, part, norms, coefs, max_norm, U);
-}
+
 
 void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha) {
   int nb = (int)((n + NT - 1) / NT);

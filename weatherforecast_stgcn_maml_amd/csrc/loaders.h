@@ -460,22 +460,6 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 __device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
 #endif
 
-// Exact unsigned division by a run-time invariant d for n < 2^31 (one 64-bit multiply):
-// m = ceil(2^(32+s) / d), s = ceil(log2 d)  =>  n / d == (n * m) >> (32 + s).
-struct FastDiv {
-  uint64_t m;
-  uint32_t s;
-  uint32_t d;
-  FastDiv() = default;
-  __host__ explicit FastDiv(uint32_t dd) : d(dd) {
-    s = 0;
-    while ((1ull << s) < dd) ++s;
-    m = (uint64_t)((((unsigned __int128)1 << (32 + s)) + dd - 1) / dd);
-  }
-  __device__ __forceinline__ uint32_t div(uint32_t n) const {
-    return (uint32_t)(((unsigned __int128)n * m) >> (32 + s));
-  }
-};
 
 // Uniform (SGPR) base + 32-bit byte offset: lets the compiler use global_* saddr addressing
 // with the constant part of the offset folded into the instruction's immediate.
