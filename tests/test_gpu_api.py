@@ -388,3 +388,29 @@ def test_fused_gcn_matches_per_layer(p_gcn):
         for i, x in enumerate(xs_np):
             ref = refcpu.stgcn_features(torch.from_numpy(x), torch.from_numpy(ei).long(), Pgt).numpy()
             assert rel(Ff[i], ref) < 1e-5
+
+
+def test_gate_images_bitwise():
+    """The gate GEMMs fed from pre-split weight images (launch_split_gate: bf16 pieces copied into
+    LDS with direct-to-LDS loads) form the same products as splitting the f32 weights in every
+    workgroup, in the same order: the meta-step's losses and meta-gradient are bitwise equal."""
+    from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
+
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=2, order=2)
+    P = synth.init_params(37, d, gcn_bias_scale=0.1)
+    Ptr, Pg, _ = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(3700 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2)]
+    out = []
+    for img in (1, 0):
+        ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
+        ml.set_tasks(feats)
+        ml.ctx.set_option("gate_img", img)
+        ml.ctx.variant_counts(reset=True)
+        res = ml.meta_step()
+        vc = ml.ctx.variant_counts()
+        assert (vc["fwd_img"] > 0) == bool(img), vc
+        out.append((res.losses.cpu(), ml.meta_grad.cpu().clone()))
+        del ml
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

@@ -9,11 +9,11 @@ TAG=${TAG:-r03}
 timeout -k 10 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/} \
   > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc
-if [ -n "${SMOKE:-1}" ]; then
+if [ -n "${SMOKE-1}" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
   tail -1 gpurun_out/${TAG}_smoke.log
 fi
-if [ -n "${BENCH:-1}" ]; then
+if [ -n "${BENCH-1}" ]; then
   timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
   tail -1 gpurun_out/${TAG}_bench.log | cut -c1-400
 fi

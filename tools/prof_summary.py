@@ -19,7 +19,7 @@ import sys
 
 # bench.py timing categories (api.cpp TIMED(...)) -> the kernels each category launches
 CATEGORIES = {
-    "gcn_layer": r"k_gcn_layer",
+    "gcn_layer": r"k_gcn_layer|k_gcn_mlp",
     "lstm_fwd_step": r"k_lstm_fwd_step",
     "lstm_fwd_dual": r"k_lstm_fwd_dual",
     "lstm_bwd_step": r"k_lstm_bwd_step",

@@ -28,7 +28,7 @@ EXPORTS = (
 ABI_VERSION = 4
 
 # kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
-VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_dual", "fwd_dual_kept", "bwd_big", "bwd_small", "bwd_split",
+VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kept", "fwd_dual_img", "bwd_big", "bwd_small", "bwd_split",
             "bwd_dual_big", "bwd_dual_big_kept", "bwd_dual_small", "bwd_dual_small_kept")
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)

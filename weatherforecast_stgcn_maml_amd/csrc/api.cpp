@@ -221,7 +221,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -239,6 +239,8 @@ struct smaml_ctx {
   // is a pure function of the window, F2), filled on first use and reused by later epochs.
   // Invalidated by smaml_set_graph / _set_gcn_params / _set_tasks.
   char* gcn_wimg = nullptr;
+  char* gimg_buf = nullptr;   // pre-split gate-GEMM weight images (prep_gate_images)
+  int64_t gimg_cap = 0;
   unsigned* bar = nullptr;    // grid-barrier arrival counter of the cooperative bookkeeping kernels
   unsigned bar_count = 0;     // arrivals so far (host mirror: launches are stream-ordered)  // pre-split GCN weight images of the fused t >= 1 GCN (kernels_gcn.hip)
   float* ad_F = nullptr;
@@ -616,10 +618,45 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
   return SMAML_OK;
 }
 
+// Pre-split images of theta's gate-GEMM weights for this forward (launch_split_gate; the fast
+// weights change every inner step, so every forward re-splits them: a few microseconds).
+int prep_gate_images(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* U = nullptr) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  w.gimg = GateImgs{};
+  w.gimg_src = nullptr;
+  w.gimg_u_src = nullptr;
+  if (!c->kn.gate_img || w.drop.lstm()) return SMAML_OK;  // (the dropout kernels load f32 weights)
+  GateImgs gi{};
+  const int64_t per = gate_img_bytes(d, &gi) * w.Z;
+  const int64_t need = per * (U ? 2 : 1);
+  if (need > c->gimg_cap) {
+    if (c->gimg_buf) HIP_TRY(hipFree(c->gimg_buf));
+    c->gimg_buf = nullptr;
+    c->gimg_cap = 0;
+    if (hipMalloc((void**)&c->gimg_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      return SMAML_OK;  // no room: the kernels load and split the f32 weights themselves
+    }
+    c->gimg_cap = need;
+  }
+  gi.th = c->gimg_buf;
+  TIMED(c, s, C_MISC, 0, launch_split_gate(s, d, c->po, theta, tstride, w.Z, gi, gi.th));
+  if (U) {
+    gi.u = c->gimg_buf + per;
+    TIMED(c, s, C_MISC, 0, launch_split_gate(s, d, c->po, U, tstride, w.Z, gi, gi.u));
+  }
+  w.gimg = gi;
+  w.gimg_src = theta;
+  w.gimg_u_src = U;
+  return SMAML_OK;
+}
+
 // LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront).
 int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   const Dims& d = c->d;
   Work& w = c->w;
+  TRY(prep_gate_images(c, s, theta, tstride));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     const double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
@@ -708,6 +745,7 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   const Dims& d = c->d;
   Work& w = c->w;
   if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev));
+  TRY(prep_gate_images(c, s, theta, tstride, U));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
@@ -883,6 +921,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->so_coef) (void)hipFree(c->so_coef);
   if (c->so_F) (void)hipFree(c->so_F);
   if (c->gcn_wimg) (void)hipFree(c->gcn_wimg);
+  if (c->gimg_buf) (void)hipFree(c->gimg_buf);
   if (c->bar) (void)hipFree(c->bar);
   ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
@@ -1262,6 +1301,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_group_max_rows = (int)std::min<int64_t>(value, 1 << 30);
   } else if (k == "gcn_fused" && (value == 0 || value == 1)) {
     c->kn.gcn_fused = (int)value;
+  } else if (k == "gate_img" && (value == 0 || value == 1)) {
+    c->kn.gate_img = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {

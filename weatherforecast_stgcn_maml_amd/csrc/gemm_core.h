@@ -358,16 +358,33 @@ __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) 
   }
 }
 
-// B operand staging for the staged mainloops: f32 float4s, split at the LDS store.
-template <class C, class LB>
+// B operand loaders that deliver PRE-SPLIT bf16 images (``kDmaImage``; loaders.h SegGateImg): the
+// K-tile's image is copied global -> LDS with direct-to-LDS loads (no staging VGPRs, no split, no
+// ds_write), issued into the stage the tile will be read from.
+template <class L, class = void>
+struct has_dma_image : std::false_type {};
+template <class L>
+struct has_dma_image<L, std::void_t<decltype(L::kDmaImage)>> : std::true_type {};
+
+// B operand staging for the staged mainloops: f32 float4s, split at the LDS store; or (DMA) the
+// image issued straight into the stage.
+template <class C, class LB, bool DMA = has_dma_image<LB>::value>
 struct BStage {
   float4 r[C::B_F4];
-  __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0) {
+  __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0, char*) {
     fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, k0, r);
   }
   __device__ __forceinline__ void store(char* img) const {
     store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(img, r);
   }
+};
+template <class C, class LB>
+struct BStage<C, LB, true> {
+  static_assert(C::X6S && C::X6S_NST == 2, "pre-split B images: two LDS stages (issued into the idle one)");
+  __device__ __forceinline__ void fetch(const LB& lb, int n0, int k0, char* img) {
+    lb.template issue<C::BN, C::B_KC, C::BK, C::NTH>(img, n0, k0);
+  }
+  __device__ __forceinline__ void store(char*) const {}
 };
 
 // The three pieces of the 32-row fragment at tile row `row` (this lane's row = row + (lane & 31)
@@ -437,15 +454,17 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   char* st0 = reinterpret_cast<char*>(smem);
   const int nkt = (kend - kbeg + BKc - 1) / BKc;
   if (nkt <= 0) return;
+  constexpr bool DMA = has_dma_image<LB>::value;
   float4 ra[C::A_F4];
   BStage<C, LB> rb;
   auto store = [&](char* st) {
     if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra);
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
     rb.store(st + SA);
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image chunks landed
   };
   fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg, ra);
-  rb.fetch(lb, n0, kbeg);
+  rb.fetch(lb, n0, kbeg, st0 + SA);
   store(st0);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
@@ -453,7 +472,8 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
     const bool more = kt + 1 < nkt;
     if (more) {
       fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (kt + 1) * BKc, ra);
-      rb.fetch(lb, n0, kbeg + (kt + 1) * BKc);
+      // (two stages: the idle one was last read by tile kt - 1's MFMAs, before the barrier)
+      rb.fetch(lb, n0, kbeg + (kt + 1) * BKc, st0 + (C::X6S_NST == 1 ? 0 : (cur ^ 1) * C::X6S_STAGE) + SA);
     }
     const char* st = st0 + (C::X6S_NST == 1 ? 0 : cur * C::X6S_STAGE);
     if constexpr (C::X6S_NST == 1) {
@@ -689,11 +709,12 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
   float4 ra[C::A_F4], ra2[C::A_F4];
   BStage<C, LB> rb;
   BStage<C, LB2> rb2;
+  static_assert(!has_dma_image<LB>::value && !has_dma_image<LB2>::value, "dual mainloop: f32 B operands");
   auto fetch = [&](int k0) {
     fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, k0, ra);
     if (k0 >= a2_kbeg) fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la2, m0, k0, ra2);
-    rb.fetch(lb, n0, k0);
-    rb2.fetch(lb2, n0, k0);
+    rb.fetch(lb, n0, k0, nullptr);
+    rb2.fetch(lb2, n0, k0, nullptr);
   };
   auto store = [&](char* st, int k0) {
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);

@@ -78,8 +78,10 @@ enum Variant {
   V_FWD = 0,         // k_lstm_fwd_step (fused gate GEMM + cell)
   V_FWD_DROP,        // k_lstm_fwd_step_drop
   V_FWD_SPLIT,       // k_lstm_fwd_part + k_lstm_fwd_cell (small grids)
+  V_FWD_IMG,         // k_lstm_fwd_step with pre-split weight images (also counted as V_FWD)
   V_FWDD,            // k_lstm_fwd_dual, primal recomputed
   V_FWDD_KEPT,       // k_lstm_fwd_dual, tangent only (primal kept)
+  V_FWDD_IMG,        // k_lstm_fwd_dual with pre-split weight images (also counted as one of the above)
   V_BWD_BIG,         // k_lstm_bwd_step, 64x128 tiles
   V_BWD_SMALL,       // k_lstm_bwd_step, 64x64 tiles
   V_BWD_SPLIT,       // k_lstm_bwd_part + k_lstm_bwd_cell (small grids)
@@ -109,7 +111,11 @@ struct Knobs {
   int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
   int wgrad_group_wgs;       // workgroups that grouped launch aims for
   int gcn_fused;             // 1: GCN rows t >= 1 through the fused four-layer kernel (k_gcn_mlp)
+  int gate_img;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
 };
+#ifndef SMAML_GATE_IMG
+#define SMAML_GATE_IMG 1
+#endif
 #ifndef SMAML_GCN_FUSED
 #define SMAML_GCN_FUSED 1
 #endif
@@ -121,8 +127,23 @@ struct Knobs {
 #endif
 
 // Activations of one forward pass for Z tasks x B samples (M = B*N sequences per task).
+// ---- pre-split gate-GEMM weight images (kernels.hip launch_split_gate) ----
+// Per task: for layer l, segment (W_ih | W_hh), unit group ug (32 units), K-tile kt the staged-split
+// LDS image (X6Img<128, KC, 16>: 3 bf16 planes x 128 rows x 16 k) of SegGateBt's 128 x 16 tile, so
+// the gate GEMMs copy weight tiles into LDS with direct-to-LDS loads instead of loading and
+// splitting them in every workgroup (the weights are the same for all row tiles of a launch).
+constexpr int GATE_IMG_BYTES = 3 * 128 * 16 * 2;
+struct GateImgs {
+  char* th;                    // images of theta (launch_split_gate), null = not built
+  char* u;                     // images of the tangent direction U (second-order sweep), or null
+  int64_t tstride;             // bytes per task
+  int64_t off[MAX_LAYERS][2];  // byte offset of (layer, W_ih | W_hh) in a task's images
+};
 struct Work {
   int Z, B, M;
+  GateImgs gimg;           // pre-split images of the weights the gate GEMMs read (launch_split_gate)
+  const float* gimg_src;   // the parameter vector gimg.th was split from (kernels use it only for that one)
+  const float* gimg_u_src; // ... and gimg.u (the sweep's tangent direction)
   int64_t* vcount;         // [NVAR] launch counters (ctx-owned; may be null)
   Knobs kn;
   float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
@@ -224,6 +245,10 @@ struct FastDiv {
     return (uint32_t)(((unsigned __int128)n * m) >> (32 + s));
   }
 };
+
+int64_t gate_img_bytes(const Dims& d, GateImgs* layout);  // bytes per task; fills off[] / tstride
+void launch_split_gate(hipStream_t s, const Dims& d, const ParamOff& po, const float* theta, int64_t tstride, int Z,
+                       const GateImgs& gi, char* dst);
 
 // ---- fused GCN stack for the rows t >= 1 (kernels_gcn.hip) ----
 struct GcnWOff {  // offsets of conv{1..4}.lin.weight / conv{1..4}.bias in the GCN parameter vector

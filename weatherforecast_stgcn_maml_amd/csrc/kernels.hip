@@ -282,11 +282,11 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
   }
 }
 
-template <int H, bool DROP>
+template <int H, bool DROP, bool IMG = false>
 __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                               float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
                                               const float* __restrict__ theta, int64_t tstride, FwdWave wv, int T,
-                                              int M, const Drop& dr, float* smem) {
+                                              int M, const Drop& dr, float* smem, const GateImgs* gi = nullptr) {
   int l, t, b0;
   LayerOff lo;
   const Blk bk = xcd_block();
@@ -319,8 +319,21 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     gemm_mainloop<CfgGate>(la, lb, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
   } else {
     const SegKCt<2> la{{X + (slab + (int64_t)t * M) * cin, Hp}, {cin, H}, M};
-    const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
-    gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+    if constexpr (IMG) {  // weight tiles as pre-split images (launch_split_gate)
+      const char* ib = gi->th + (int64_t)z * gi->tstride;
+      int64_t o0 = 0, o1 = 0;  // (layer l's segment offsets, selected with scalar compares)
+#pragma unroll
+      for (int q = 0; q < MAX_LAYERS; ++q)
+        if (q == l) {
+          o0 = gi->off[q][0];
+          o1 = gi->off[q][1];
+        }
+      const SegGateImg<2> lbi{{ib + o0, ib + o1}, {cin, H}};
+      gemm_mainloop<CfgGate>(la, lbi, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+    } else {
+      const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
+      gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+    }
   }
 
   fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
@@ -352,13 +365,13 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
 
 // The dropout variant holds the mask state beside the 4-gate tile: it gets the register budget
 // of 3 waves/SIMD instead of 4 (no spill).
-template <int H>
+template <int H, bool IMG>
 __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                                       float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      FwdWave wv, int T, int M, Drop dr) {
+                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
-  lstm_fwd_step<H, false>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem);
+  lstm_fwd_step<H, false, IMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi);
 }
 template <int H>
 __global__ __attribute__((amdgpu_waves_per_eu(3))) __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step_drop(
@@ -620,8 +633,71 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     }
   }
   count_variant(w, V_FWD);
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_step<HT><<<grid, CfgGate::NTH, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride,
-                                                                           wv, d.T, w.M, w.drop));
+  if (w.gimg.th && w.gimg_src == theta) {
+    count_variant(w, V_FWD_IMG);
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, true><<<grid, CfgGate::NTH, 0, s>>>(
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg)));
+  } else {
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, false><<<grid, CfgGate::NTH, 0, s>>>(
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg)));
+  }
+}
+
+// ---- pre-split gate-GEMM weight images --------------------------------------------------
+int64_t gate_img_bytes(const Dims& d, GateImgs* gi) {
+  const int nug = (d.H + 31) / 32;
+  int64_t off = 0;
+  for (int l = 0; l < d.L; ++l)
+    for (int sg = 0; sg < 2; ++sg) {
+      if (gi) gi->off[l][sg] = off;
+      const int w = sg == 0 ? (l == 0 ? d.Hc : d.H) : d.H;
+      off += (int64_t)nug * (w / 16) * GATE_IMG_BYTES;
+    }
+  if (gi) gi->tstride = off;
+  return off;
+}
+
+// One thread per (task, image, row, 4 k): weight row g*H + ug*32 + jj of image row n = g*32 + jj,
+// columns 16 kt + 4 q .. + 3 of the segment; split into three bf16 planes at the staged-split
+// store's offsets (gemm_core.h store_tile_x6, KC, BK 16).
+__global__ void k_split_gate(const float* __restrict__ theta, int64_t tstride, ParamOff po, int L, int H, int Hc,
+                             int nimg, int64_t img_tstride, char* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int z = blockIdx.y;
+  if (i >= (int64_t)nimg * 512) return;
+  const int q = (int)(i & 3), n = (int)((i >> 2) & 127), img = (int)(i >> 9);
+  const int nug = (H + 31) / 32;
+  int rem = img, l = 0, sg = 0, w = Hc;
+  for (l = 0; l < L; ++l) {
+    w = l == 0 ? Hc : H;
+    const int a = nug * (w / 16);
+    if (rem < a) { sg = 0; break; }
+    rem -= a;
+    const int b = nug * (H / 16);
+    if (rem < b) { sg = 1; w = H; break; }
+    rem -= b;
+  }
+  const int kts = w / 16, ug = rem / kts, kt = rem - ug * kts;
+  const LayerOff lo = po.lay[l];
+  const float* W = theta + (int64_t)z * tstride + (sg == 0 ? lo.wih : lo.whh);
+  const int j = min(ug * 32 + (n & 31), H - 1);
+  const float4 v = ld4(W + (int64_t)((n >> 5) * H + j) * w + 16 * kt + 4 * q);
+  uint2 p0, p1, p2;
+  split4(v, p0, p1, p2);
+  constexpr int PLANE = 128 * 32;
+  char* o = dst + (int64_t)z * img_tstride + (int64_t)img * GATE_IMG_BYTES + n * 32 + 16 * ((q >> 1) ^ ((n >> 3) & 1)) +
+            8 * (q & 1);
+  *reinterpret_cast<uint2*>(o) = p0;
+  *reinterpret_cast<uint2*>(o + PLANE) = p1;
+  *reinterpret_cast<uint2*>(o + 2 * PLANE) = p2;
+}
+
+void launch_split_gate(hipStream_t s, const Dims& d, const ParamOff& po, const float* theta, int64_t tstride, int Z,
+                       const GateImgs& gi, char* dst) {
+  const int nimg = (int)(gi.tstride / GATE_IMG_BYTES);
+  const int64_t threads = (int64_t)nimg * 512;
+  k_split_gate<<<dim3((unsigned)((threads + 255) / 256), Z), 256, 0, s>>>(theta, tstride, po, d.L, d.H, d.Hc, nimg,
+                                                                          gi.tstride, dst);
 }
 
 // ====================================================================================

@@ -104,14 +104,15 @@ __device__ __forceinline__ void fwd_dual_tangent_epi(const Acc<CfgGateD>& at, co
   }
 }
 
-template <int H, bool KEPT, bool DROP>
+// IMG: the weight tiles of theta and U come from their pre-split images (launch_split_gate).
+template <int H, bool KEPT, bool DROP, bool IMG>
 __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
                                                       float* __restrict__ HsAll, float* __restrict__ CsAll,
                                                       float* __restrict__ GsAll, float* __restrict__ RHsAll,
                                                       float* __restrict__ RCsAll, float* __restrict__ RGsAll,
                                                       int64_t lsz, const float* __restrict__ theta,
                                                       const float* __restrict__ U, int64_t tstride, FwdWave wv,
-                                                      int T, int M, Drop dr) {
+                                                      int T, int M, Drop dr, GateImgs gi) {
   __shared__ float smem[CfgGateD::SMEM_FLOATS];
   constexpr int G4 = 4 * H;
   int l, t, b0;
@@ -130,6 +131,17 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
   const int cin = lo.cin;
+  const char* ith = IMG ? gi.th + (int64_t)z * gi.tstride : nullptr;
+  const char* iu = IMG ? gi.u + (int64_t)z * gi.tstride : nullptr;
+  int64_t io0 = 0, io1 = 0;  // layer l's image offsets (W_ih | W_hh), selected with scalar compares
+  if constexpr (IMG) {
+#pragma unroll
+    for (int q = 0; q < MAX_LAYERS; ++q)
+      if (q == l) {
+        io0 = gi.off[q][0];
+        io1 = gi.off[q][1];
+      }
+  }
   const int64_t slab = (int64_t)z * T * M;
   float* Gz = Gs + slab * G4;
   float* RGz = RGs + slab * G4;
@@ -167,6 +179,9 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
+    else if constexpr (IMG)
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M}, SegGateImg<2>{{ith + io0, ith + io1}, {cin, wh}},
+                                          m0, n0, 0, cin + wh, ap, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
                                           SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, 0,
@@ -205,6 +220,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+    else if constexpr (IMG)
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
+                                          SegGateImg<4>{{iu + io0, iu + io1, ith + io0, ith + io1}, {cin, wh, wrx, wh}},
+                                          m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
                                           SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
@@ -233,10 +252,17 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   dim3 grid(wv.off[wv.n], 1, w.Z);
   const bool kept = w.primal_kept != 0, drop = w.drop.lstm();
   count_variant(w, kept ? V_FWDD_KEPT : V_FWDD);
+  const bool img = !drop && w.gimg.th && w.gimg.u && w.gimg_src == theta && w.gimg_u_src == U;
+  if (img) count_variant(w, V_FWDD_IMG);
 #define SMAML_FWD_DUAL(K_, D_)                                                                  \
-  SMAML_DISPATCH_H(d.H, k_lstm_fwd_dual<HT, K_, D_><<<grid, CfgGateD::NTH, 0, s>>>(              \
-                            w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
-                            d.T, w.M, w.drop))
+  if (img)                                                                                      \
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_dual<HT, K_, D_, !(D_)><<<grid, CfgGateD::NTH, 0, s>>>(    \
+                              w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
+                              d.T, w.M, w.drop, w.gimg)))                                       \
+  else                                                                                          \
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_dual<HT, K_, D_, false><<<grid, CfgGateD::NTH, 0, s>>>(    \
+                              w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
+                              d.T, w.M, w.drop, w.gimg)))
   if (kept && drop) {
     SMAML_FWD_DUAL(true, true);
   } else if (kept) {

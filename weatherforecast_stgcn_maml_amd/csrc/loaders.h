@@ -232,6 +232,24 @@ __device__ __forceinline__ float4 ldo(const float* base, uint32_t byteoff) {
   return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byteoff);
 }
 
+// The segment holding K index k0 (segment widths w[], k-concatenated): its base pointer, width and
+// the offset inside it. Every member is read unconditionally and the choice is made on the values:
+// the per-segment `if (kk >= ws) b = p[s]` chain became a select of member ADDRESSES, a dynamic
+// index that kept the 4-segment loaders of the tangent gate kernel in scratch memory (two scratch
+// loads per K-tile, the 112-120 B "spill" of rounds 1-2).
+template <int NS, typename P>
+__device__ __forceinline__ void seg_pick(const P (&p)[NS], const int (&w)[NS], int k0, P& b, int& ws, int& kk) {
+  static_assert(NS >= 1 && NS <= 4, "up to 4 segments");
+  // every member read unconditionally first, then selected as values
+  const P p0 = p[0], p1 = p[NS > 1 ? 1 : 0], p2 = p[NS > 2 ? 2 : 0], p3 = p[NS > 3 ? 3 : 0];
+  const int w0 = w[0], w1 = w[NS > 1 ? 1 : 0], w2 = w[NS > 2 ? 2 : 0];
+  const int e1 = w0, e2 = e1 + (NS > 1 ? w1 : 0), e3 = e2 + (NS > 2 ? w2 : 0);
+  const int s = (NS > 1 && k0 >= e1) + (NS > 2 && k0 >= e2) + (NS > 3 && k0 >= e3);
+  b = s == 0 ? p0 : s == 1 ? p1 : s == 2 ? p2 : p3;
+  kk = k0 - (s == 0 ? 0 : s == 1 ? e1 : s == 2 ? e2 : e3);
+  ws = s == 0 ? w0 : s == 1 ? w1 : s == 2 ? w2 : w[NS - 1];
+}
+
 // KC operand [rows][w_s] per segment (row stride = width), k-concatenated.
 template <int NS>
 struct SegKCt {
@@ -242,15 +260,9 @@ struct SegKCt {
   template <int ROWS, int F4, int NTH, bool KC, int BK>
   __device__ __forceinline__ void fetch(int row0, int k0, float4 (&r)[F4]) const {
     static_assert(KC, "SegKCt is a k-contiguous operand");
-    const float* b = p[0];
-    int ws = w[0], kk = k0;
-#pragma unroll
-    for (int s = 1; s < NS; ++s)
-      if (kk >= ws) {
-        kk -= ws;
-        b = p[s];
-        ws = w[s];
-      }
+    const float* b;
+    int ws, kk;
+    seg_pick<NS>(p, w, k0, b, ws, kk);
     b += kk + (int64_t)row0 * ws;  // the tile's first row: 64-bit, uniform
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
@@ -271,15 +283,9 @@ struct SegMCt {
   template <int ROWS, int F4, int NTH, bool KC, int BK>
   __device__ __forceinline__ void fetch(int col0, int k0, float4 (&r)[F4]) const {
     static_assert(!KC, "SegMCt is an n-contiguous operand");
-    const float* b = p[0];
-    int ks = K[0], kk = k0;
-#pragma unroll
-    for (int s = 1; s < NS; ++s)
-      if (kk >= ks) {
-        kk -= ks;
-        b = p[s];
-        ks = K[s];
-      }
+    const float* b;
+    int ks, kk;
+    seg_pick<NS>(p, K, k0, b, ks, kk);
     b += (int64_t)kk * cols;
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
@@ -301,15 +307,9 @@ struct SegGateBt {
   template <int ROWS, int F4, int NTH, bool KC, int BK>
   __device__ __forceinline__ void fetch(int n0, int k0, float4 (&r)[F4]) const {
     static_assert(KC, "SegGateBt is a k-contiguous operand");
-    const float* b = p[0];
-    int ws = w[0], kk = k0;
-#pragma unroll
-    for (int s = 1; s < NS; ++s)
-      if (kk >= ws) {
-        kk -= ws;
-        b = p[s];
-        ws = w[s];
-      }
+    const float* b;
+    int ws, kk;
+    seg_pick<NS>(p, w, k0, b, ws, kk);
     b += kk;
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
@@ -319,6 +319,37 @@ struct SegGateBt {
       const int j = min(ug * 32 + (rem & 31), H - 1);
       const int row = (rem >> 5) * H + j;
       r[i] = ldo(b, 4u * (uint32_t)(row * ws + 4 * (f % (BK / 4))));
+    }
+  }
+};
+
+// Gate-GEMM B operand as pre-split bf16 images (gemm_core.h has_dma_image; launch_split_gate): the
+// image of segment s, unit group ug (= n0 / 128), K-tile kt is the X6Img<128, KC, 16> at
+// p[s] + (ug * (w[s] / 16) + kt) * GATE_IMG_BYTES, with SegGateBt's row mapping (image row
+// g * 32 + jj = weight row g * H + ug * 32 + jj). Every wave copies its share of the image's 1-KB
+// chunks with global_load_lds_dwordx4 (64 lanes x 16 B, lane-contiguous in LDS).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+template <int NS>
+struct SegGateImg {
+  static constexpr bool kDmaImage = true;
+  const char* p[NS];
+  int w[NS];
+  template <int ROWS, bool KC, int BK, int NTH>
+  __device__ __forceinline__ void issue(char* dst, int n0, int k0) const {
+    static_assert(ROWS == 128 && KC && BK == 16, "gate images: 128 rows x 16 k");
+    const char* b;
+    int ws, kk;
+    seg_pick<NS>(p, w, k0, b, ws, kk);
+    const char* src = b + ((int64_t)(n0 >> 7) * (ws / BK) + kk / BK) * GATE_IMG_BYTES;
+    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    constexpr int CH = GATE_IMG_BYTES / 1024, NW = NTH / 64;
+#pragma unroll
+    for (int c = 0; c < (CH + NW - 1) / NW; ++c) {
+      const int ch = wave + NW * c;
+      if (CH % NW == 0 || ch < CH)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + ch * 1024 + 16 * lane), (lds_void_t*)(dst + ch * 1024),
+                                         16, 0, 0);
     }
   }
 };
