@@ -256,7 +256,11 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  (-1 = the SMAML_KEEP environment variable / all that fit);
  *   "wgrad_group_max_rows":        a backward with tasks x rows <= this runs all LSTM weight
  *                                  gradients as one launch after the BPTT (batch-1 adaptation);
- *   "wgrad_group_wgs":             workgroups that grouped launch aims for. */
+ *   "wgrad_group_wgs":             workgroups that grouped launch aims for;
+ *   "gcn_fused", "gate_img":       fused GCN stack for the rows t >= 1 / pre-split gate weight
+ *                                  images (1 = on, the default);
+ *   "wgrad_wide":                  weight gradients whose column count is a multiple of 256 on
+ *                                  256 x 256 tiles (1, the default) or 512 x 128 tiles (0). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -28,7 +28,7 @@ for f in ("kernels", "kernels_dual"):
         n = c["name"]
         if re.search(r"^_ZN5smaml\d+k_[a-z_]+ILi(32|64|256)E", n):
             continue
-        short = re.sub(r"^_ZN5smaml\d+", "", n)[:48]
+        short = re.sub(r"^_ZN5smaml\d+", "", n)[:int(os.environ.get("RES_W", "48"))]
         print(f"{short:48s} vgpr {c.get('VGPRs', '?'):>4s} agpr {c.get('AGPRs', '?'):>4s} "
               f"scratch {c.get('ScratchSize [bytes/lane]', '?'):>3s} occ {c.get('Occupancy [waves/SIMD]', '?'):>2s} "
               f"lds {c.get('LDS Size [bytes/block]', '?')}")

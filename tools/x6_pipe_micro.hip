@@ -30,12 +30,18 @@ using namespace smaml;
 #ifndef ILV_VALU
 #define ILV_VALU 3  // split VALU per MFMA in the pipe2 interleave
 #endif
-constexpr int BMc = MICRO_BM;
+#ifndef MICRO_BN
+#define MICRO_BN 128
+#endif
+#ifndef MICRO_WN
+#define MICRO_WN 1
+#endif
+constexpr int BMc = MICRO_BM, BNc = MICRO_BN;
 #ifndef MICRO_WM
 #define MICRO_WM (MICRO_BM / 64)  // waves along M (MICRO_BM / 128: one wave per SIMD with 128 x 128 wave tiles)
 #endif
 constexpr int WM = MICRO_WM;
-using C = GemmCfg<BMc, 128, WM, 1, false, false, 16, 2, 2>;
+using C = GemmCfg<BMc, BNc, WM, MICRO_WN, false, false, 16, 2, 2>;
 constexpr int NTH = C::NTH;
 constexpr int KCH = MICRO_KCH;
 constexpr int SLICES = MICRO_SLICES;
@@ -92,7 +98,7 @@ __device__ __forceinline__ void store_one_x6(char* img, const float4& v, int i) 
     off = rr * I::RS + 16 * ((qq >> 1) ^ I::swz(rr)) + 8 * (qq & 1);
   } else {
     const int kk = f / (ROWS / 4), qq = f % (ROWS / 4);
-    off = kk * I::RS + 8 * qq;
+    off = I::mc(kk, 8 * qq);
   }
   uint2 p0, p1, p2;
   split4(v, p0, p1, p2);
@@ -158,18 +164,18 @@ __device__ __forceinline__ void pipe2(const LA& la, const LB& lb, int kbeg, int 
 }
 
 #ifndef MICRO_WPE
-#define MICRO_WPE (64 * MICRO_WM >= 512 ? 2 : MICRO_BM / MICRO_WM >= 128 ? 1 : 2)  // waves per SIMD
+#define MICRO_WPE (64 * MICRO_WM * MICRO_WN >= 512 ? 2 : MICRO_BM / MICRO_WM >= 128 ? 1 : 2)  // waves per SIMD
 #endif
 template <int MODE>
 __global__ __attribute__((amdgpu_waves_per_eu(MICRO_WPE))) __launch_bounds__(NTH) void k_micro(const float* A0, const float* B0, float* O) {
   __shared__ float smem[C::SMEM_FLOATS];
   const int sl = blockIdx.x % SLICES;
   RowMajorMC la{A0 + (int64_t)sl * KCH * BMc, KCH, BMc};
-  RowMajorMC lb{B0 + (int64_t)sl * KCH * 128, KCH, 128};
+  RowMajorMC lb{B0 + (int64_t)sl * KCH * BNc, KCH, BNc};
   Acc<C> acc;
   acc.zero();
   if (MODE == 0) gemm_mainloop<C, -1>(la, lb, 0, 0, 0, KCH, acc, smem);
-  if (MODE == 1) gemm_mainloop<C, -1>(NoMem{BMc}, NoMem{128}, 0, 0, 0, KCH, acc, smem);
+  if (MODE == 1) gemm_mainloop<C, -1>(NoMem{BMc}, NoMem{BNc}, 0, 0, 0, KCH, acc, smem);
   if (MODE == 2) pipe2(la, lb, 0, KCH, acc, smem);
 #pragma unroll
   for (int i = 0; i < C::WTM; ++i)
@@ -177,7 +183,7 @@ __global__ __attribute__((amdgpu_waves_per_eu(MICRO_WPE))) __launch_bounds__(NTH
     for (int j = 0; j < C::WTN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        O[((int64_t)blockIdx.x * BMc + acc_row<C>(i, r)) * 128 + acc_col<C>(j)] = acc.v[i][j][r];
+        O[((int64_t)blockIdx.x * BMc + acc_row<C>(i, r)) * BNc + acc_col<C>(j)] = acc.v[i][j][r];
 }
 
 __global__ void k_fill(float* p, size_t n, size_t off) {
@@ -201,15 +207,15 @@ float timeit(K kern, int wgs, const float* A, const float* B, float* O) {
 }
 
 int main() {
-  const size_t na = (size_t)SLICES * KCH * BMc, nb = (size_t)SLICES * KCH * 128;
+  const size_t na = (size_t)SLICES * KCH * BMc, nb = (size_t)SLICES * KCH * BNc;
   float *A, *B, *O1, *O2;
   if (hipMalloc(&A, na * 4) || hipMalloc(&B, nb * 4)) return 1;
-  const int wgs = 256 * 6 * (512 / BMc);
-  if (hipMalloc(&O1, (size_t)wgs * BMc * 128 * 4) || hipMalloc(&O2, (size_t)wgs * BMc * 128 * 4)) return 1;
+  const int wgs = 256 * 6 * (512 * 128 / (BMc * BNc));
+  if (hipMalloc(&O1, (size_t)wgs * BMc * BNc * 4) || hipMalloc(&O2, (size_t)wgs * BMc * BNc * 4)) return 1;
   k_fill<<<4096, 256>>>(A, na, 0);
   k_fill<<<4096, 256>>>(B, nb, 12345);
-  const double fl = 2.0 * BMc * 128 * KCH * wgs;
-  printf("BM %d, %d threads, %d workgroups, K %d per workgroup, LDS %d B\n", BMc, NTH, wgs, KCH, C::SMEM_FLOATS * 4);
+  const double fl = 2.0 * BMc * BNc * KCH * wgs;
+  printf("BM %d BN %d, %d threads, %d workgroups, K %d per workgroup, LDS %d B\n", BMc, BNc, NTH, wgs, KCH, C::SMEM_FLOATS * 4);
   for (int rep = 0; rep < 3; ++rep) {
     const float t0 = timeit(k_micro<0>, wgs, A, B, O1);
     const float t1 = timeit(k_micro<1>, wgs, A, B, O2);
@@ -217,7 +223,7 @@ int main() {
     printf("lib %8.1f us %6.1f TF/s | noload %8.1f us %6.1f TF/s | pipe2 %8.1f us %6.1f TF/s\n", t0 * 1e3,
            fl / (t0 * 1e-3) / 1e12, t1 * 1e3, fl / (t1 * 1e-3) / 1e12, t2 * 1e3, fl / (t2 * 1e-3) / 1e12);
   }
-  std::vector<float> o1((size_t)wgs * BMc * 128), o2(o1.size());
+  std::vector<float> o1((size_t)wgs * BMc * BNc), o2(o1.size());
   hipMemcpy(o1.data(), O1, o1.size() * 4, hipMemcpyDeviceToHost);
   hipMemcpy(o2.data(), O2, o2.size() * 4, hipMemcpyDeviceToHost);
   size_t nd = 0;

@@ -221,7 +221,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -567,6 +567,8 @@ void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t
              off_b1, off_b2, with_bias, accumulate, p);
   p.drop = c->w.drop;  // B1 = drop(h_{drop_layer}) under LSTM dropout (input weights of layer >= 1)
   p.drop_layer = drop_layer;
+  count_variant(c->w, V_WGRAD);
+  if (p.wide) count_variant(c->w, V_WGRAD_WIDE);
   TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
 }
@@ -724,7 +726,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       WgradPlan& p = plans[l];
       plan_wgrad(w, w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
                  w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true,
-                 false, p);
+                 false, p, true);
       p.drop = w.drop;
       p.drop_layer = l - 1;
       gfl += 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H);
@@ -1303,6 +1305,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.gcn_fused = (int)value;
   } else if (k == "gate_img" && (value == 0 || value == 1)) {
     c->kn.gate_img = (int)value;
+  } else if (k == "wgrad_wide" && (value == 0 || value == 1)) {
+    c->kn.wgrad_wide = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {

@@ -65,12 +65,17 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
 
 // bf16-piece LDS image of one operand tile for the staged split (GemmCfg X6_ = 2): three planes
 // (x0, x1, x2), each bf16. KC operands: [rows][BK] per plane, 16-B chunks XOR-swizzled by row so the
-// ds_read_b128 fragment reads are conflict-free; MC operands: [BK][rows] per plane with a row
-// stride of 2*rows + 64 B (== 64 or 192 mod 256), read transposed by ds_read_b64_tr_b16.
+// ds_read_b128 fragment reads are conflict-free; MC operands: [BK][rows] per plane, read transposed
+// by ds_read_b64_tr_b16 (a 32-lane half reads 64 contiguous bytes of each of 4 consecutive image
+// rows). Rows of a multiple of 128 elements are unpadded (stride 2*rows B, a multiple of 256) with
+// the 64-B blocks of image row k XOR-swizzled by (k mod 4), which spreads those 4 reads over all
+// 64 banks (round 3: the padded stride cost the tangent BPTT its third workgroup per CU); narrower
+// ones keep the padded stride 2*rows + 64 B (== 64 or 192 mod 256).
 template <int ROWS, bool KC, int BK>
 struct X6Img {
   static constexpr int NCH = BK / 8;                       // 16-B chunks per KC row
-  static constexpr int RS = KC ? 2 * BK : 2 * ROWS + 64;   // bytes per image row
+  static constexpr bool MSW = !KC && ROWS % 128 == 0;      // MC image swizzled instead of padded
+  static constexpr int RS = KC ? 2 * BK : MSW ? 2 * ROWS : 2 * ROWS + 64;  // bytes per image row
   static constexpr int PLANE = KC ? ROWS * RS : BK * RS;   // bytes per plane
   static constexpr int BYTES = 3 * PLANE;
   static_assert(!KC || NCH == 2 || NCH == 4 || NCH == 8, "KC staged split: BK 16, 32 or 64");
@@ -78,6 +83,8 @@ struct X6Img {
   __device__ static __forceinline__ int swz(int r) {
     return NCH == 2 ? (r >> 3) & 1 : NCH == 4 ? (r >> 2) & 3 : (r >> 1) & 7;
   }
+  // MC: byte offset of byte b (even, 8-B chunks never split) of image row k within a plane
+  __device__ static __forceinline__ int mc(int k, int b) { return k * RS + (MSW ? b ^ ((k & 3) << 6) : b); }
 };
 
 template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32, int X6_ = SMAML_X6,
@@ -348,7 +355,7 @@ __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) 
       off = rr * I::RS + 16 * ((q >> 1) ^ I::swz(rr)) + 8 * (q & 1);
     } else {
       const int kk = f / (ROWS / 4), q = f % (ROWS / 4);
-      off = kk * I::RS + 8 * q;
+      off = I::mc(kk, 8 * q);
     }
     uint2 p0, p1, p2;
     split4(r[i], p0, p1, p2);
@@ -406,7 +413,7 @@ __device__ __forceinline__ Split3 frag_x6(const char* img, int row, int s) {
     const int g = lane >> 4, i = lane & 15;
     const int h = g >> 1;
     const int col = row + 16 * (g & 1) + 4 * (i & 3);
-    const int off = (16 * s + 8 * h + (i >> 2)) * I::RS + 2 * col;
+    const int off = I::mc(16 * s + 8 * h + (i >> 2), 2 * col);  // (row k + 4 below: same swizzle)
     typedef __attribute__((address_space(3))) bf16x4_t* lp;
     auto rd = [&](int o) {
       const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp)(img + o));
@@ -723,6 +730,37 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
     rb2.store(st + 2 * SA + SB);
   };
   auto mma = [&](const char* st, bool a2on) {
+    if constexpr (!PRIMAL) {
+      // tangent only: all A.B2 products of the step, then all A2.B ones, so only one of A / A2 (and
+      // one B fragment) is live at a time; per accumulator the order (A.B2 before A2.B) is unchanged
+#pragma unroll
+      for (int s = 0; s < BKc / 16; ++s) {
+        {
+          Split3 a[C::WTM];
+#pragma unroll
+          for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, BKc>(st, wm * (C::WTM * 32) + 32 * i, s);
+#pragma unroll
+          for (int j = 0; j < C::WTN; ++j) {
+            const Split3 b2 = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA + SB, wn * (C::WTN * 32) + 32 * j, s);
+#pragma unroll
+            for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a[i], b2, acct.v[i][j]);
+          }
+        }
+        if (a2on) {
+          Split3 a2[C::WTM];
+#pragma unroll
+          for (int i = 0; i < C::WTM; ++i)
+            a2[i] = frag_x6<C::BM, C::A_KC, BKc>(st + SA, wm * (C::WTM * 32) + 32 * i, s);
+#pragma unroll
+          for (int j = 0; j < C::WTN; ++j) {
+            const Split3 b = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA, wn * (C::WTN * 32) + 32 * j, s);
+#pragma unroll
+            for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a2[i], b, acct.v[i][j]);
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < BKc / 16; ++s) {
       Split3 a[C::WTM], a2[C::WTM];

@@ -89,6 +89,8 @@ enum Variant {
   V_BWDD_BIG_KEPT,   // k_lstm_bwd_dual, 64x128 tiles, tangent only
   V_BWDD_SMALL,      // k_lstm_bwd_dual, 64x64 tiles, primal recomputed
   V_BWDD_SMALL_KEPT, // k_lstm_bwd_dual, 64x64 tiles, tangent only
+  V_WGRAD,           // k_wgrad launches (any tile)
+  V_WGRAD_WIDE,      // k_wgrad with 256 x 256 tiles (also counted as V_WGRAD)
   NVAR
 };
 
@@ -112,6 +114,7 @@ struct Knobs {
   int wgrad_group_wgs;       // workgroups that grouped launch aims for
   int gcn_fused;             // 1: GCN rows t >= 1 through the fused four-layer kernel (k_gcn_mlp)
   int gate_img;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
+  int wgrad_wide;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -321,11 +324,12 @@ struct WgradPlan {
   int64_t kchunk;
   Drop drop;       // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
   int drop_layer;
+  bool wide;       // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
 };
 void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
                 int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                 int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,
-                WgradPlan& p);
+                WgradPlan& p, bool multi = false);
 // Several plans (same Z) in one GEMM launch + one reduce launch; their nsplit / kchunk / part are
 // re-planned for about target_wgs workgroups in total (partial slabs must fit w.wpart).
 struct WgMulti {

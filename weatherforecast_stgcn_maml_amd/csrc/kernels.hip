@@ -271,7 +271,7 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
     const float gg = tanhf_(acc.v[0][2][r] + bsum[2]);
     const float go = sigmoidf_(acc.v[0][3][r] + bsum[3]);
     const float cp = PRE ? cpv[r] : (t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f);
-    const float c = gf * cp + gi * gg;
+    const float c = lstm_cell_c(gi, gf, gg, cp);
     const float h = go * tanhf_(c);
     stb(Gz, 4u * (og), gi);
     stb(Gz, 4u * (og + H), gf);
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(CfgGateP::NTH) void k_lstm_fwd_cell_q(float* __rest
     const float gf = sigmoidf_(f4get(a[1], e) + bsum[1]);
     const float gg = tanhf_(f4get(a[2], e) + bsum[2]);
     const float go = sigmoidf_(f4get(a[3], e) + bsum[3]);
-    const float c = gf * cpv[e] + gi * gg;
+    const float c = lstm_cell_c(gi, gf, gg, cpv[e]);
     const float h = go * tanhf_(c);
     stb(Gz, 4u * (og), gi);
     stb(Gz, 4u * (og + H), gf);
@@ -1060,8 +1060,8 @@ __device__ __forceinline__ void bwd_cell_(const float* smem, const float* Gz, fl
   const bool first = (t == T - 1), past = t > 0;
   const int64_t pM = past ? (int64_t)M * H : 0;  // c_{t-1} offset (t = 0: masked)
   const int64_t tM = (int64_t)t * M;
-  struct V {
-    float4 g[4], c, cp, dc, hd;
+  struct V {  // c_t is re-derived from the gates and c_{t-1} (lstm_cell_c), not loaded
+    float4 g[4], cp, dc, hd;
   };
   auto coords = [&](int k, int& r, int& m, int& j) {
     const int item = (int)threadIdx.x + CfgNN::NTH * k;
@@ -1080,7 +1080,6 @@ __device__ __forceinline__ void bwd_cell_(const float* smem, const float* Gz, fl
     const float* gp = Gz + row * G4 + j;
 #pragma unroll
     for (int g = 0; g < 4; ++g) v.g[g] = ld4(gp + g * H);
-    v.c = ld4(Cz + row * H + j);
     v.cp = ld4(Cz + row * H - pM + j);
     v.dc = ld4(dcz + (int64_t)m * H + j);
     if (HEAD) v.hd = ld4(dHz + (int64_t)m * H + j);
@@ -1097,7 +1096,7 @@ __device__ __forceinline__ void bwd_cell_(const float* smem, const float* Gz, fl
     for (int e = 0; e < 4; ++e) {
       const float gi = f4get(v.g[0], e), gf = f4get(v.g[1], e), gg = f4get(v.g[2], e), go = f4get(v.g[3], e);
       const float d = f4get(dh, e);
-      const float tc = tanhf_(f4get(v.c, e));
+      const float tc = tanhf_(lstm_cell_c(gi, gf, gg, f4get(cp, e)));
       const float dct = f4get(dc, e) + d * go * (1.f - tc * tc);
       const float r0 = dct * gg * gi * (1.f - gi), r1 = dct * f4get(cp, e) * gf * (1.f - gf);
       const float r2 = dct * gi * (1.f - gg * gg), r3 = d * tc * go * (1.f - go);
@@ -1324,14 +1323,13 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell_q(const float* GsA
   const int j = n0 + acc_col<CfgNN>(0);
   const int rb = m0 + acc_row<CfgNN>(0, 0) + 8 * q;  // row of register 4q
   const int jc = min(j, H - 1);
-  float g[4][4], c[4], cp[4], dc[4], hd[4];
+  float g[4][4], cp[4], dc[4], hd[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {  // all loads first (clamped rows: valid addresses)
     const int m = min(rb + e, M - 1);
     const int64_t row = (int64_t)t * M + m;
 #pragma unroll
     for (int k = 0; k < 4; ++k) g[e][k] = Gz[row * G4 + k * H + jc];
-    c[e] = Cz[row * H + jc];
     cp[e] = past ? Cz[row * H - (int64_t)M * H + jc] : 0.f;
     dc[e] = first ? 0.f : dcz[(int64_t)m * H + jc];
     hd[e] = head ? dHz[(int64_t)m * H + jc] : 0.f;
@@ -1342,7 +1340,7 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell_q(const float* GsA
     if (m >= M || j >= H) continue;
     const float d = f4get(a, e) + hd[e];
     const float gi = g[e][0], gf = g[e][1], gg = g[e][2], go = g[e][3];
-    const float tc = tanhf_(c[e]);
+    const float tc = tanhf_(lstm_cell_c(gi, gf, gg, cp[e]));
     const float dct = dc[e] + d * go * (1.f - tc * tc);
     const int64_t row = (int64_t)t * M + m;
     float* gp = dGz + row * G4 + j;
@@ -1421,19 +1419,20 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 // Column sums of A (= the bias gradient) from the A fragments the MFMAs already hold in
 // registers: lane (row r = arow + 32 i, k-half h) sums its k-values; the halves are combined
 // with one cross-lane add after the mainloop (colsum_rows). No extra LDS traffic.
+template <class C>
 struct ColSumHook {
-  float s[CfgTN::WTM];
+  float s[C::WTM];
   __device__ __forceinline__ ColSumHook() {
 #pragma unroll
-    for (int i = 0; i < CfgTN::WTM; ++i) s[i] = 0.f;
+    for (int i = 0; i < C::WTM; ++i) s[i] = 0.f;
   }
   __device__ __forceinline__ void operator()(const float*, int) const {}
   __device__ __forceinline__ void afrag(int i, const float4& a) { s[i] += (a.x + a.y) + (a.z + a.w); }
-  // staged split (CfgTN::X6S): the A float4s a thread stages always cover the same 4 gate rows
+  // staged split (C::X6S): the A float4s a thread stages always cover the same 4 gate rows
   // 4q .. 4q+3 (q = tid mod BM/4); their sums are kept here and reduced over the NTH/(BM/4) threads
   // sharing q in store().
-  static constexpr int kQ = CfgTN::BM / 4, kQT = CfgTN::NTH / kQ;
-  static_assert(!CfgTN::X6S || (CfgTN::NTH % kQ == 0 && !CfgTN::A_KC), "staged column sums: thread -> rows fixed");
+  static constexpr int kQ = C::BM / 4, kQT = C::NTH / kQ;
+  static_assert(!C::X6S || (C::NTH % kQ == 0 && !C::A_KC), "staged column sums: thread -> rows fixed");
   float4 cs = f4zero();
   template <int F4>
   __device__ __forceinline__ void stage_a(const float4 (&r)[F4]) {
@@ -1447,7 +1446,7 @@ struct ColSumHook {
   }
   // lanes 0..31 own rows wm*(WTM*32) + 32 i + lane of the tile
   __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias, float* smem) {
-    if constexpr (CfgTN::X6S) {
+    if constexpr (C::X6S) {
       // the mainloop ended with a barrier: its LDS is free
       st4(smem + 4 * threadIdx.x, cs);
       __syncthreads();
@@ -1470,32 +1469,33 @@ struct ColSumHook {
       }
       return;
     }
-    const int lane = threadIdx.x & 63, wm = (threadIdx.x >> 6) / CfgTN::WAVES_N;
+    const int lane = threadIdx.x & 63, wm = (threadIdx.x >> 6) / C::WAVES_N;
 #pragma unroll
-    for (int i = 0; i < CfgTN::WTM; ++i) {
+    for (int i = 0; i < C::WTM; ++i) {
       const float v = s[i] + __shfl_xor(s[i], 32);
-      const int row = m0 + wm * (CfgTN::WTM * 32) + 32 * i + lane;
-      if (lane < 32 && (threadIdx.x >> 6) % CfgTN::WAVES_N == 0 && row < Mrows)
+      const int row = m0 + wm * (C::WTM * 32) + 32 * i + lane;
+      if (lane < 32 && (threadIdx.x >> 6) % C::WAVES_N == 0 && row < Mrows)
         P[(int64_t)row * ldp + ncols] = with_bias ? v : 0.f;
     }
   }
 };
 #else
 // A/B baseline: column sums re-read from the staged A tile in LDS once per K-tile.
+template <class C>
 struct ColSumHook {
   float bsum = 0.f;
   __device__ __forceinline__ void operator()(const float* as, int) {
-    if (threadIdx.x < CfgTN::BM) {
+    if (threadIdx.x < C::BM) {
       float s = bsum;
 #pragma unroll 8
-      for (int kk = 0; kk < CfgTN::BK; ++kk) s += as[kk * CfgTN::LDA + threadIdx.x];
+      for (int kk = 0; kk < C::BK; ++kk) s += as[kk * C::LDA + threadIdx.x];
       bsum = s;
     }
   }
   __device__ __forceinline__ void afrag(int, const float4&) {}
   __device__ __forceinline__ void store(float* P, int m0, int Mrows, int ldp, int ncols, bool with_bias, float*) {
     const int row = m0 + threadIdx.x;
-    if (threadIdx.x < CfgTN::BM && row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? bsum : 0.f;
+    if (threadIdx.x < C::BM && row < Mrows) P[(int64_t)row * ldp + ncols] = with_bias ? bsum : 0.f;
   }
 };
 #endif
@@ -1608,8 +1608,22 @@ __device__ __forceinline__ void wgrad_glds_loop(const float* A, int64_t K, const
   }
 }
 
+// Square weight-gradient tiles for the launches whose column count is a multiple of 256 (LSTM layers
+// >= 1: [x | h] = 256 columns, so each workgroup covers ALL of them): 256 x 256, 8 waves of 64 x 128.
+// Against the 512 x 128 tile (whose two column tiles each load and split the whole 512-row A) a
+// K-tile loads and splits (256 + 256) instead of (512 + 128) rows per 256 x 128 x 2 MFMA work, 20 %
+// less staging per product (micro: 196 -> 208 TF/s, profiles/r03_wgrad_tile_micro.log).
+#ifndef SMAML_WGRAD_WIDE
+#define SMAML_WGRAD_WIDE 1
+#endif
+using CfgTW = GemmCfg<256, 256, 4, 2, false, false, SMAML_TN_BK, SMAML_X6_WGRAD, SMAML_TN_NST>;
+template <class C>
+constexpr int wgrad_smem_floats() {
+  return std::is_same<C, CfgTN>::value ? WG_SMEM : C::SMEM_FLOATS;
+}
+
 // One weight-gradient workgroup: block L of a launch over ((ngroups + 7) / 8 * 8 * ntile) blocks.
-template <bool DROP>
+template <class C, bool DROP>
 __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
                                             int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn, int ntile,
                                             int nsplit, int ngroups, float* __restrict__ part, int ldp, int with_bias,
@@ -1627,67 +1641,69 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
   if (b.B2) b.B2 += (int64_t)z * b2_zstride;
   const int64_t kbeg = (int64_t)split * kchunk;
   const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
-  const int m0 = tm * CfgTN::BM, n0 = tn * CfgTN::BN;
-  Acc<CfgTN> acc;
+  const int m0 = tm * C::BM, n0 = tn * C::BN;
+  Acc<C> acc;
   acc.zero();
-  ColSumHook hook;
+  ColSumHook<C> hook;
   // k indices exceed int range only in the loaders (int64 there); the mainloop
   // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
   if (DROP) {
     const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
                               (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
     if (tn == 0 && with_bias) {
-      gemm_mainloop<CfgTN, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+      gemm_mainloop<C, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     } else {
-      gemm_mainloop<CfgTN, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
+      gemm_mainloop<C, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
     }
-  } else if (SMAML_WGRAD_GLDS && kWgradGldsShape && Mrows == CfgTN::BM && lb.c1 % CfgTN::BN == 0 &&
+  } else if (std::is_same<C, CfgTN>::value && SMAML_WGRAD_GLDS && kWgradGldsShape && Mrows == CfgTN::BM && lb.c1 % CfgTN::BN == 0 &&
              lb.c2 % CfgTN::BN == 0) {
     const float* Az = A + (int64_t)z * a_zstride;
-    if (tn == 0 && with_bias) {
-      wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, hook);
-    } else {
-      NoHook nh;
-      wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, nh);
+    if constexpr (std::is_same<C, CfgTN>::value) {
+      if (tn == 0 && with_bias) {
+        wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, hook);
+      } else {
+        NoHook nh;
+        wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, nh);
+      }
     }
-  } else if (SMAML_WGRAD_TILE_LOADERS && CfgTN::X6S && (lb.c2 == 0 || lb.c1 % CfgTN::BN == 0)) {
+  } else if (SMAML_WGRAD_TILE_LOADERS && C::X6S && (lb.c2 == 0 || lb.c1 % C::BN == 0)) {
     const MCKt lt{A + (int64_t)z * a_zstride, lb.K, Mrows};
     const WgBt bt{b.B1, b.B2, b.c1, b.c2, b.K, b.Mshift};
     if (tn == 0 && with_bias)
-      gemm_mainloop<CfgTN, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+      gemm_mainloop<C, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     else
-      gemm_mainloop<CfgTN, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem);
+      gemm_mainloop<C, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem);
   } else if (tn == 0 && with_bias) {
     // (the branch-free MCKt / WgBt tile loaders measured slower here with the f32 MFMA: wgrad
     // 723 -> 820 ms per meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log)
-    gemm_mainloop<CfgTN, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    gemm_mainloop<C, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
-    gemm_mainloop<CfgTN, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    gemm_mainloop<C, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
   }
   const int ncols = lb.c1 + lb.c2;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
 #pragma unroll
-  for (int i = 0; i < CfgTN::WTM; ++i)
+  for (int i = 0; i < C::WTM; ++i)
 #pragma unroll
-    for (int jj = 0; jj < CfgTN::WTN; ++jj) {
-      const int c = n0 + acc_col<CfgTN>(jj);
+    for (int jj = 0; jj < C::WTN; ++jj) {
+      const int c = n0 + acc_col<C>(jj);
       if (c >= ncols) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + acc_row<CfgTN>(i, r);
+        const int row = m0 + acc_row<C>(i, r);
         if (row < Mrows) P[(int64_t)row * ldp + c] = acc.v[i][jj][r];
       }
     }
   if (tn == 0) hook.store(P, m0, Mrows, ldp, ncols, with_bias != 0, smem);
 }
 
-template <bool DROP>
-__global__ __launch_bounds__(CfgTN::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
+template <class C, bool DROP>
+__global__ __launch_bounds__(C::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
                                               int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
                                               int ldp, int with_bias, Drop dr, int drop_layer) {
-  __shared__ float smem[WG_SMEM];
-  wgrad_block<DROP>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, nsplit,
+  __shared__ float smem[wgrad_smem_floats<C>()];
+  wgrad_block<C, DROP>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, nsplit,
                     ngroups, part, ldp, with_bias, dr, drop_layer, smem);
 }
 
@@ -1709,11 +1725,11 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad_multi(WgMulti mp, Drop dr)
   lb.K = p.K;
   lb.Mshift = p.Mshift;
   if (DROP && p.drop_layer >= 0)
-    wgrad_block<true>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
+    wgrad_block<CfgTN, true>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
                       p.kchunk, p.ntn, p.ntm * p.ntn, p.nsplit, p.nsplit * p.Z, p.part, p.ldp, p.with_bias ? 1 : 0,
                       dr, p.drop_layer, smem);
   else
-    wgrad_block<false>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
+    wgrad_block<CfgTN, false>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
                        p.kchunk, p.ntn, p.ntm * p.ntn, p.nsplit, p.nsplit * p.Z, p.part, p.ldp, p.with_bias ? 1 : 0,
                        dr, -1, smem);
 }
@@ -1776,11 +1792,15 @@ __global__ void k_wgrad_reduce_multi(WgMulti mp) {
 void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
                 int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                 int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,
-                WgradPlan& p) {
+                WgradPlan& p, bool multi) {
   const int ncols = c1 + c2;
   const int ldp = ncols + 1;
-  const int ntm = (Mrows + CfgTN::BM - 1) / CfgTN::BM;
-  const int ntn = (ncols + CfgTN::BN - 1) / CfgTN::BN;
+  const bool wide = !multi && SMAML_WGRAD_WIDE && w.kn.wgrad_wide && CfgTW::X6S && ncols % CfgTW::BN == 0 &&
+                    Mrows % CfgTW::BM == 0;
+  const int BMc = wide ? CfgTW::BM : CfgTN::BM, BNc = wide ? CfgTW::BN : CfgTN::BN;
+  static_assert(CfgTW::NTH == CfgTN::NTH && CfgTW::BK == CfgTN::BK, "one split-K plan for both tiles");
+  const int ntm = (Mrows + BMc - 1) / BMc;
+  const int ntn = (ncols + BNc - 1) / BNc;
   const int64_t ktiles = (K + CfgTN::BK - 1) / CfgTN::BK;
   // aim for ~2048 4-wave workgroups' worth of waves, at least 8 K-tiles per split, bounded by
   // the slab buffer
@@ -1818,6 +1838,7 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   p.ntn = ntn;
   p.nsplit = (int)nsplit;
   p.kchunk = kchunk;
+  p.wide = wide;
 }
 
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
@@ -1831,14 +1852,22 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
   const int ntile = p.ntm * p.ntn;
   const int ngroups = p.nsplit * p.Z;
   dim3 grid((unsigned)(((ngroups + 7) / 8) * 8 * ntile));
-  if (p.drop_layer >= 0 && p.drop.lstm())
-    k_wgrad<true><<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk,
-                                              p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
-                                              p.drop, p.drop_layer);
-  else
-    k_wgrad<false><<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk,
-                                               p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
-                                               p.drop, -1);
+  const bool drop = p.drop_layer >= 0 && p.drop.lstm();
+#define SMAML_WGRAD_LAUNCH(CFG, D_)                                                                            \
+  k_wgrad<CFG, D_><<<grid, CFG::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, \
+                                             p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0, \
+                                             p.drop, D_ ? p.drop_layer : -1)
+  if (p.wide) {
+    if (drop)
+      SMAML_WGRAD_LAUNCH(CfgTW, true);
+    else
+      SMAML_WGRAD_LAUNCH(CfgTW, false);
+  } else if (drop) {
+    SMAML_WGRAD_LAUNCH(CfgTN, true);
+  } else {
+    SMAML_WGRAD_LAUNCH(CfgTN, false);
+  }
+#undef SMAML_WGRAD_LAUNCH
 }
 
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p) {

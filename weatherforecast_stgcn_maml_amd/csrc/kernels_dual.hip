@@ -63,7 +63,7 @@ __device__ __forceinline__ void fwd_dual_tangent_epi(const Acc<CfgGateD>& at, co
   const uint32_t pM = past ? (uint32_t)M * H : 0u;
 #pragma unroll
   for (int r0 = 0; r0 < 16; r0 += RB) {
-    float gi[RB], gf[RB], gg[RB], go[RB], c[RB], cp[RB], rcp[RB];
+    float gi[RB], gf[RB], gg[RB], go[RB], cp[RB], rcp[RB];
 #pragma unroll
     for (int q = 0; q < RB; ++q) {
       int m = rb + racc(r0 + q);
@@ -75,7 +75,6 @@ __device__ __forceinline__ void fwd_dual_tangent_epi(const Acc<CfgGateD>& at, co
       gf[q] = ldb(Gz, 4u * (og + H));
       gg[q] = ldb(Gz, 4u * (og + 2 * H));
       go[q] = ldb(Gz, 4u * (og + 3 * H));
-      c[q] = ldb(Cz, 4u * (oh));
       cp[q] = ldb(Cz, 4u * (oh - pM));
       rcp[q] = ldb(RCz, 4u * (oh - pM));
     }
@@ -92,8 +91,8 @@ __device__ __forceinline__ void fwd_dual_tangent_epi(const Acc<CfgGateD>& at, co
       const float rg = (1.f - gg[q] * gg[q]) * (at.v[0][2][r] + bu[2]);
       const float ro = go[q] * (1.f - go[q]) * (at.v[0][3][r] + bu[3]);
       const float cpv = past ? cp[q] : 0.f, rcpv = past ? rcp[q] : 0.f;
-      const float rc = rf * cpv + gf[q] * rcpv + ri * gg[q] + gi[q] * rg;
-      const float tc = tanhf_(c[q]);
+      const float rc = lstm_cell_rc(gi[q], gf[q], gg[q], cpv, ri, rf, rg, rcpv);
+      const float tc = tanhf_(lstm_cell_c(gi[q], gf[q], gg[q], cpv));
       stb(RGz, 4u * (og), ri);
       stb(RGz, 4u * (og + H), rf);
       stb(RGz, 4u * (og + 2 * H), rg);
@@ -202,7 +201,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
         const float gg = tanhf_(ap.v[0][2][r] + bp[2]);
         const float go = sigmoidf_(ap.v[0][3][r] + bp[3]);
         const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
-        const float c = gf * cp + gi * gg;
+        const float c = lstm_cell_c(gi, gf, gg, cp);
         stb(Gz, 4u * (og), gi);
         stb(Gz, 4u * (og + H), gf);
         stb(Gz, 4u * (og + 2 * H), gg);
@@ -399,6 +398,17 @@ void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const floa
 #endif                     // epilogue, 2 = without its GEMM
 using CfgNNDs = GemmCfg<64, 64, 2, 2, true, false, SMAML_DUAL_BK, SMAML_X6_BWDD>;
 using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, false, SMAML_DUAL_BK, SMAML_X6_BWDD>;
+// Kept-step epilogue in two row halves (BM*BN/2 floats of transpose LDS): with the swizzled MC weight
+// images the staged stage is 48 KB, so the 128 x 128 tangent BPTT runs three workgroups per CU.
+#ifndef SMAML_BWDD_HALFEPI
+#define SMAML_BWDD_HALFEPI (SMAML_X6 ? 1 : 0)
+#endif
+template <class C>
+constexpr int bwdd_smem_floats() {
+  constexpr int E = (SMAML_BWDD_HALFEPI && C::WAVES_M == 2) ? C::BM * C::BN / 2 : C::BM * C::BN;
+  constexpr int S = C::X6S ? DualStage<C>::X6S_FLOATS : DualStage<C>::FLOATS;
+  return S > E ? S : E;
+}
 
 // Tangent-only cell backward of a kept step (see kernels.hip bwd_cell_): R(dh) = the GEMM
 // accumulators, transposed through LDS so each lane works on float4 groups of 4 hidden units of
@@ -418,8 +428,8 @@ __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const flo
   const bool first = (t == T - 1), past = t > 0;
   const int64_t pM = past ? (int64_t)M * H : 0;
   const int64_t tM = (int64_t)t * M;
-  struct V {
-    float4 dh, g[4], rg[4], c, rc, cp, rcp, dc, rdc, rhd;
+  struct V {  // c_t and R c_t are re-derived from the gates and c_{t-1} (lstm_cell_c / _rc)
+    float4 dh, g[4], rg[4], cp, rcp, dc, rdc, rhd;
   };
   auto coords = [&](int k, int& r, int& m, int& j) {
     const int item = (int)threadIdx.x + C::NTH * k;
@@ -443,8 +453,6 @@ __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const flo
       v.rg[g] = ld4(rp + g * H);
     }
     v.dh = ld4(dhz + row * H + j);
-    v.c = ld4(Cz + row * H + j);
-    v.rc = ld4(RCz + row * H + j);
     v.cp = ld4(Cz + row * H - pM + j);
     v.rcp = ld4(RCz + row * H - pM + j);
     v.dc = ld4(dcz + (int64_t)m * H + j);
@@ -463,8 +471,8 @@ __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const flo
       const float rdh = f4get(acc, e) + (HEAD ? f4get(v.rhd, e) : 0.f);
       const float gi = f4get(v.g[0], e), gf = f4get(v.g[1], e), gg = f4get(v.g[2], e), go = f4get(v.g[3], e);
       const float ri = f4get(v.rg[0], e), rf = f4get(v.rg[1], e), rgg = f4get(v.rg[2], e), ro = f4get(v.rg[3], e);
-      const float c = f4get(v.c, e), rc = f4get(v.rc, e);
       const float cp = past ? f4get(v.cp, e) : 0.f, rcp = past ? f4get(v.rcp, e) : 0.f;
+      const float c = lstm_cell_c(gi, gf, gg, cp), rc = lstm_cell_rc(gi, gf, gg, cp, ri, rf, rgg, rcp);
       const float dcin = first ? 0.f : f4get(v.dc, e), rdcin = first ? 0.f : f4get(v.rdc, e);
       const float tc = tanhf_(c);
       const float s2 = 1.f - tc * tc;
@@ -515,8 +523,7 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                                       int64_t lsz, const float* __restrict__ theta,
                                                       const float* __restrict__ U, int64_t tstride, BwdWave wv, int L,
                                                       int T, int M, Drop dr) {
-  __shared__ float smem[DualStage<CfgNND>::FLOATS];
-  static_assert(DualStage<CfgNND>::FLOATS >= CfgNND::BM * CfgNND::BN, "epilogue transpose fits the staging LDS");
+  __shared__ float smem[bwdd_smem_floats<CfgNND>()];
   constexpr int G4 = 4 * H;
   const Blk bk = xcd_block();
   int mb;
@@ -582,20 +589,30 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   const float* RdHz = RdHhead + (int64_t)z * M * H;
   const bool full = m0 + CfgNND::BM <= M;
   if constexpr (KEPT) {
-    acc_to_lds<CfgNND>(at, smem);
-    if (SMAML_DIAG_BWDD == 1) {  // timing diagnostic: GEMM phase only (keep the result live)
-      if (t < 0) RGz[threadIdx.x] = smem[threadIdx.x];
-      return;
-    }
-    const bool nochk = full && n0 + CfgNND::BN <= H;
+    constexpr bool HALF = SMAML_BWDD_HALFEPI && CfgNND::WAVES_M == 2;
+    using EC = std::conditional_t<HALF, HalfRows<CfgNND>, CfgNND>;
+#pragma unroll 1
+    for (int hh = 0; hh < (HALF ? 2 : 1); ++hh) {
+      if (hh) __syncthreads();  // the first half's readers are done with the LDS
+      if constexpr (HALF)
+        acc_to_lds_half<CfgNND>(at, smem, hh);
+      else
+        acc_to_lds<CfgNND>(at, smem);
+      if (SMAML_DIAG_BWDD == 1) {  // timing diagnostic: GEMM phase only (keep the result live)
+        if (t < 0) RGz[threadIdx.x] = smem[threadIdx.x];
+        continue;
+      }
+      const int mh = m0 + hh * EC::BM;
+      const bool nochk = mh + EC::BM <= M && n0 + EC::BN <= H;
 #define SMAML_KEPT_EPI(HD, CK)                                                                          \
-  bwd_dual_kept_cell_<H, CfgNND, HD, CK>(smem, Gz, RGz, dhz, Cz, RCz, dHz, RdHz, dcz, rdcz, m0, n0, t, T, M)
-    if (head) {
-      if (nochk) SMAML_KEPT_EPI(true, false); else SMAML_KEPT_EPI(true, true);
-    } else {
-      if (nochk) SMAML_KEPT_EPI(false, false); else SMAML_KEPT_EPI(false, true);
-    }
+  bwd_dual_kept_cell_<H, EC, HD, CK>(smem, Gz, RGz, dhz, Cz, RCz, dHz, RdHz, dcz, rdcz, mh, n0, t, T, M)
+      if (head) {
+        if (nochk) SMAML_KEPT_EPI(true, false); else SMAML_KEPT_EPI(true, true);
+      } else {
+        if (nochk) SMAML_KEPT_EPI(false, false); else SMAML_KEPT_EPI(false, true);
+      }
 #undef SMAML_KEPT_EPI
+    }
     return;
   }
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
@@ -618,9 +635,9 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
       const float rdh = at.v[i][jj][r] + (head ? ldb(RdHz, 4u * oc) : 0.f);
       const float gi = ldb(Gz, 4u * (og)), gf = ldb(Gz, 4u * (og + H)), gg = ldb(Gz, 4u * (og + 2 * H)), go = ldb(Gz, 4u * (og + 3 * H));
       const float ri = ldb(RGz, 4u * (og)), rf = ldb(RGz, 4u * (og + H)), rgg = ldb(RGz, 4u * (og + 2 * H)), ro = ldb(RGz, 4u * (og + 3 * H));
-      const float c = ldb(Cz, 4u * (oh)), rc = ldb(RCz, 4u * (oh));
       const float cp = t > 0 ? ldb(Cz, 4u * (oh - (uint32_t)M * H)) : 0.f;
       const float rcp = t > 0 ? ldb(RCz, 4u * (oh - (uint32_t)M * H)) : 0.f;
+      const float c = lstm_cell_c(gi, gf, gg, cp), rc = lstm_cell_rc(gi, gf, gg, cp, ri, rf, rgg, rcp);
       const float dcin = first ? 0.f : ldb(dcz, 4u * (oc));
       const float rdcin = first ? 0.f : ldb(rdcz, 4u * (oc));
       const float tc = tanhf_(c);

@@ -491,6 +491,16 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 __device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
 #endif
 
+// LSTM cell state with a fixed operation order: c_t = f c_{t-1} + i g and its tangent
+// R(c_t) = R(f) c_{t-1} + f R(c_{t-1}) + R(i) g + i R(g). Every kernel that stores c_t (or R c_t)
+// forms it here, so the backward kernels re-derive it bitwise from the stored gates and c_{t-1}
+// instead of loading it (one 4-B read per element less in the HBM-bound BPTT epilogues).
+__device__ __forceinline__ float lstm_cell_c(float gi, float gf, float gg, float cp) { return fmaf(gf, cp, gi * gg); }
+__device__ __forceinline__ float lstm_cell_rc(float gi, float gf, float gg, float cp, float ri, float rf, float rg,
+                                              float rcp) {
+  return fmaf(gi, rg, fmaf(ri, gg, fmaf(gf, rcp, rf * cp)));
+}
+
 
 // Uniform (SGPR) base + 32-bit byte offset: lets the compiler use global_* saddr addressing
 // with the constant part of the offset folded into the instruction's immediate.
