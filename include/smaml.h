@@ -260,7 +260,9 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "gcn_fused", "gate_img":       fused GCN stack for the rows t >= 1 / pre-split gate weight
  *                                  images (1 = on, the default);
  *   "wgrad_wide":                  weight gradients whose column count is a multiple of 256 on
- *                                  256 x 256 tiles (1, the default) or 512 x 128 tiles (0). */
+ *                                  256 x 256 tiles (1, the default) or 512 x 128 tiles (0);
+ *   "wgrad_pair":                  the two passes of a tangent weight gradient (LSTM layers >= 1)
+ *                                  as one split-K launch (1, the default) or two (0). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

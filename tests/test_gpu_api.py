@@ -416,11 +416,14 @@ def test_gate_images_bitwise():
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 
-def test_wgrad_wide_tiles_match_narrow():
-    """Weight gradients with 256-column problems (LSTM layers >= 1 and their tangent passes) run on
-    256 x 256 tiles by default (kernels.hip CfgTW); the 512 x 128 tiles give the same weight sums
-    (same split-K slices, same per-element MFMA order) and the bias column sums up to summation
-    order. Both second-order meta-steps agree with each other well inside the oracle tolerance."""
+@pytest.mark.parametrize("knob", ["wgrad_wide", "wgrad_pair"])
+def test_wgrad_variants_match(knob):
+    """wgrad_wide: weight gradients with 256-column problems (LSTM layers >= 1 and their tangent
+    passes) run on 256 x 256 tiles by default (kernels.hip CfgTW); the 512 x 128 tiles give the same
+    weight sums (same split-K slices, same per-element MFMA order) and the bias column sums up to
+    summation order. wgrad_pair: the tangent weight gradient's two passes (R(dG)^T [x|h] and
+    dG^T [Rx|Rh]) as one split-K launch instead of two accumulating ones (summation order only).
+    Both second-order meta-steps agree with each other well inside the oracle tolerance."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
@@ -430,14 +433,14 @@ def test_wgrad_wide_tiles_match_narrow():
     ei = grid_edges(d)
     feats = [synth.make_features(4100 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2)]
     out = []
-    for wide in (1, 0):
+    for on in (1, 0):
         ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
         ml.set_tasks(feats)
-        ml.ctx.set_option("wgrad_wide", wide)
+        ml.ctx.set_option(knob, on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()
         vc = ml.ctx.variant_counts()
-        assert vc["wgrad"] > 0 and (vc["wgrad_wide"] > 0) == bool(wide), vc
+        assert vc["wgrad"] > 0 and (vc[knob] > 0) == bool(on), vc
         out.append((res.losses.cpu().numpy(), ml.meta_grad.cpu().numpy().copy()))
         del ml
     np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-6)

@@ -221,7 +221,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -573,6 +573,25 @@ void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
 }
 
+// Tangent weight gradient of one LSTM layer as ONE split-K launch + ONE reduce:
+//   R(dW) = R(dG)^T [x | h_{t-1}] + dG^T [Rx | Rh_{t-1}]   (both problems 4H x (cin + H)).
+void timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, const float* dG, int64_t a_zstride,
+                      int Mrows, const float* X, const float* RX, int64_t b1_zstride, int c1, const float* Hh,
+                      const float* RHh, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
+                      int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, int drop_layer) {
+  WgradPlan p;
+  plan_wgrad(c->w, RdG, a_zstride, Mrows, X, b1_zstride, c1, Hh, b2_zstride, c2, K, Mshift, grad, P, off_w1, off_w2,
+             off_b1, off_b2, true, false, p);
+  pair_wgrad(p, dG, RX, RHh);
+  p.drop = c->w.drop;
+  p.drop_layer = drop_layer;
+  count_variant(c->w, V_WGRAD);
+  if (p.wide) count_variant(c->w, V_WGRAD_WIDE);
+  count_variant(c->w, V_WGRAD_PAIR);
+  TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
+  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+}
+
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
 // rows t >= 1 (no neighbours, F3) run all four convs in one launch (k_gcn_mlp, activations kept in
 // registers), the t = 0 rows (ELL gather) four per-layer launches over N-row blocks.
@@ -784,6 +803,12 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
     const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
+    if (l > 0 && c->kn.wgrad_pair) {  // both passes 4H x (cin + H): one launch
+      timed_wgrad_pair(c, s, 2.0 * 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, dGl, TM * 4 * d.H, 4 * d.H, X, RX,
+                       TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M,
+                       HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, l - 1);
+      continue;
+    }
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
                        TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false, l - 1);
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
@@ -1307,6 +1332,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.gate_img = (int)value;
   } else if (k == "wgrad_wide" && (value == 0 || value == 1)) {
     c->kn.wgrad_wide = (int)value;
+  } else if (k == "wgrad_pair" && (value == 0 || value == 1)) {
+    c->kn.wgrad_pair = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "keep" && value >= -1) {

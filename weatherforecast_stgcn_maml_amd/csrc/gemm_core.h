@@ -71,10 +71,10 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
 // the 64-B blocks of image row k XOR-swizzled by (k mod 4), which spreads those 4 reads over all
 // 64 banks (round 3: the padded stride cost the tangent BPTT its third workgroup per CU); narrower
 // ones keep the padded stride 2*rows + 64 B (== 64 or 192 mod 256).
-template <int ROWS, bool KC, int BK>
+template <int ROWS, bool KC, int BK, bool SWZ = true>
 struct X6Img {
   static constexpr int NCH = BK / 8;                       // 16-B chunks per KC row
-  static constexpr bool MSW = !KC && ROWS % 128 == 0;      // MC image swizzled instead of padded
+  static constexpr bool MSW = SWZ && !KC && ROWS % 128 == 0;  // MC image swizzled instead of padded
   static constexpr int RS = KC ? 2 * BK : MSW ? 2 * ROWS : 2 * ROWS + 64;  // bytes per image row
   static constexpr int PLANE = KC ? ROWS * RS : BK * RS;   // bytes per plane
   static constexpr int BYTES = 3 * PLANE;
@@ -88,8 +88,9 @@ struct X6Img {
 };
 
 template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KC_, bool B_KC_, int BK_ = 32, int X6_ = SMAML_X6,
-          int NST_ = 2>
+          int NST_ = 2, bool MSW_ = true>
 struct GemmCfg {
+  static constexpr bool MSW = MSW_;  // staged MC images: swizzled (unpadded) where the rows allow (X6Img)
   static constexpr int X6S_NST = NST_;  // staged split: LDS stages (1 = register prefetch, two barriers)
   static constexpr int BK = BK_;
   // products: 0 = v_mfma_f32_32x32x2_f32; 1 = bf16x6 with the split on the MFMA fragments (mma_tile);
@@ -115,8 +116,8 @@ struct GemmCfg {
   static constexpr int A_F4 = BM * BK / 4 / NTH;
   static constexpr int B_F4 = BN * BK / 4 / NTH;
   static_assert(A_F4 * 4 * NTH == BM * BK && B_F4 * 4 * NTH == BN * BK, "tile/threads");
-  using AImg = X6Img<BM, A_KC, BK>;
-  using BImg = X6Img<BN, B_KC, BK>;
+  using AImg = X6Img<BM, A_KC, BK, MSW>;
+  using BImg = X6Img<BN, B_KC, BK, MSW>;
   static constexpr int X6S_STAGE = AImg::BYTES + BImg::BYTES;  // bytes per staged-split stage
   static constexpr int SMEM_FLOATS = (X6S && NST_ * X6S_STAGE / 4 > 2 * (A_STAGE + B_STAGE))
                                         ? NST_ * X6S_STAGE / 4
@@ -342,9 +343,9 @@ __device__ __forceinline__ void split4(const float4& v, uint2& p0, uint2& p1, ui
 }
 
 // Split this thread's staged float4s of one operand tile into the image at `img` (byte base).
-template <int ROWS, int F4, int NTH, bool KC, int BK>
+template <int ROWS, int F4, int NTH, bool KC, int BK, bool SWZ = true>
 __device__ __forceinline__ void store_tile_x6(char* img, const float4 (&r)[F4]) {
-  using I = X6Img<ROWS, KC, BK>;
+  using I = X6Img<ROWS, KC, BK, SWZ>;
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < F4; ++i) {
@@ -382,7 +383,7 @@ struct BStage {
     fetch_tile<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(lb, n0, k0, r);
   }
   __device__ __forceinline__ void store(char* img) const {
-    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK>(img, r);
+    store_tile_x6<C::BN, C::B_F4, C::NTH, C::B_KC, C::BK, C::MSW>(img, r);
   }
 };
 template <class C, class LB>
@@ -396,9 +397,9 @@ struct BStage<C, LB, true> {
 
 // The three pieces of the 32-row fragment at tile row `row` (this lane's row = row + (lane & 31)
 // for KC; the fragment's first row for MC), MFMA step s (k = 16s + 8h .. 16s + 8h + 7).
-template <int ROWS, bool KC, int BK>
+template <int ROWS, bool KC, int BK, bool SWZ = true>
 __device__ __forceinline__ Split3 frag_x6(const char* img, int row, int s) {
-  using I = X6Img<ROWS, KC, BK>;
+  using I = X6Img<ROWS, KC, BK, SWZ>;
   const int lane = threadIdx.x & 63;
   Split3 f;
   if (KC) {
@@ -437,10 +438,10 @@ __device__ __forceinline__ void mma_tile_x6s(const char* as, const char* bs, Acc
   for (int s = 0; s < C::BK / 16; ++s) {
     Split3 a[C::WTM];
 #pragma unroll
-    for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, C::BK>(as, wm * (C::WTM * 32) + 32 * i, s);
+    for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, C::BK, C::MSW>(as, wm * (C::WTM * 32) + 32 * i, s);
 #pragma unroll
     for (int j = J0; j < J1; ++j) {
-      const Split3 b = frag_x6<C::BN, C::B_KC, C::BK>(bs, wn * (C::WTN * 32) + 32 * j, s);
+      const Split3 b = frag_x6<C::BN, C::B_KC, C::BK, C::MSW>(bs, wn * (C::WTN * 32) + 32 * j, s);
 #pragma unroll
       for (int i = 0; i < C::WTM; ++i) acc.v[i][j] = mfma_x6(a[i], b, acc.v[i][j]);
     }
@@ -466,7 +467,7 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   BStage<C, LB> rb;
   auto store = [&](char* st) {
     if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra);
-    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
+    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc, C::MSW>(st, ra);
     rb.store(st + SA);
     if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image chunks landed
   };
@@ -724,8 +725,8 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
     rb2.fetch(lb2, n0, k0, nullptr);
   };
   auto store = [&](char* st, int k0) {
-    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st, ra);
-    if (k0 >= a2_kbeg) store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(st + SA, ra2);
+    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc, C::MSW>(st, ra);
+    if (k0 >= a2_kbeg) store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc, C::MSW>(st + SA, ra2);
     rb.store(st + 2 * SA);
     rb2.store(st + 2 * SA + SB);
   };
@@ -738,10 +739,10 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
         {
           Split3 a[C::WTM];
 #pragma unroll
-          for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, BKc>(st, wm * (C::WTM * 32) + 32 * i, s);
+          for (int i = 0; i < C::WTM; ++i) a[i] = frag_x6<C::BM, C::A_KC, BKc, C::MSW>(st, wm * (C::WTM * 32) + 32 * i, s);
 #pragma unroll
           for (int j = 0; j < C::WTN; ++j) {
-            const Split3 b2 = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA + SB, wn * (C::WTN * 32) + 32 * j, s);
+            const Split3 b2 = frag_x6<C::BN, C::B_KC, BKc, C::MSW>(st + 2 * SA + SB, wn * (C::WTN * 32) + 32 * j, s);
 #pragma unroll
             for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a[i], b2, acct.v[i][j]);
           }
@@ -750,10 +751,10 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
           Split3 a2[C::WTM];
 #pragma unroll
           for (int i = 0; i < C::WTM; ++i)
-            a2[i] = frag_x6<C::BM, C::A_KC, BKc>(st + SA, wm * (C::WTM * 32) + 32 * i, s);
+            a2[i] = frag_x6<C::BM, C::A_KC, BKc, C::MSW>(st + SA, wm * (C::WTM * 32) + 32 * i, s);
 #pragma unroll
           for (int j = 0; j < C::WTN; ++j) {
-            const Split3 b = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA, wn * (C::WTN * 32) + 32 * j, s);
+            const Split3 b = frag_x6<C::BN, C::B_KC, BKc, C::MSW>(st + 2 * SA, wn * (C::WTN * 32) + 32 * j, s);
 #pragma unroll
             for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a2[i], b, acct.v[i][j]);
           }
@@ -766,17 +767,17 @@ __device__ __forceinline__ void gemm_dual_mainloop_x6s(const LA& la, const LA2& 
       Split3 a[C::WTM], a2[C::WTM];
 #pragma unroll
       for (int i = 0; i < C::WTM; ++i) {
-        a[i] = frag_x6<C::BM, C::A_KC, BKc>(st, wm * (C::WTM * 32) + 32 * i, s);
-        if (a2on) a2[i] = frag_x6<C::BM, C::A_KC, BKc>(st + SA, wm * (C::WTM * 32) + 32 * i, s);
+        a[i] = frag_x6<C::BM, C::A_KC, BKc, C::MSW>(st, wm * (C::WTM * 32) + 32 * i, s);
+        if (a2on) a2[i] = frag_x6<C::BM, C::A_KC, BKc, C::MSW>(st + SA, wm * (C::WTM * 32) + 32 * i, s);
       }
 #pragma unroll
       for (int j = 0; j < C::WTN; ++j) {
         const int br = wn * (C::WTN * 32) + 32 * j;
-        const Split3 b2 = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA + SB, br, s);
+        const Split3 b2 = frag_x6<C::BN, C::B_KC, BKc, C::MSW>(st + 2 * SA + SB, br, s);
 #pragma unroll
         for (int i = 0; i < C::WTM; ++i) acct.v[i][j] = mfma_x6(a[i], b2, acct.v[i][j]);
         if (PRIMAL || a2on) {
-          const Split3 b = frag_x6<C::BN, C::B_KC, BKc>(st + 2 * SA, br, s);
+          const Split3 b = frag_x6<C::BN, C::B_KC, BKc, C::MSW>(st + 2 * SA, br, s);
 #pragma unroll
           for (int i = 0; i < C::WTM; ++i) {
             if (PRIMAL) accp.v[i][j] = mfma_x6(a[i], b, accp.v[i][j]);

@@ -91,6 +91,7 @@ enum Variant {
   V_BWDD_SMALL_KEPT, // k_lstm_bwd_dual, 64x64 tiles, tangent only
   V_WGRAD,           // k_wgrad launches (any tile)
   V_WGRAD_WIDE,      // k_wgrad with 256 x 256 tiles (also counted as V_WGRAD)
+  V_WGRAD_PAIR,      // k_wgrad summing two problems (tangent weight gradient; also counted as V_WGRAD)
   NVAR
 };
 
@@ -115,12 +116,16 @@ struct Knobs {
   int gcn_fused;             // 1: GCN rows t >= 1 through the fused four-layer kernel (k_gcn_mlp)
   int gate_img;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
   int wgrad_wide;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
+  int wgrad_pair;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
 #endif
 #ifndef SMAML_GCN_FUSED
 #define SMAML_GCN_FUSED 1
+#endif
+#ifndef SMAML_WGRAD_PAIR
+#define SMAML_WGRAD_PAIR 1
 #endif
 #ifndef SMAML_WGRAD_GROUP_ROWS
 #define SMAML_WGRAD_GROUP_ROWS 2048
@@ -325,7 +330,15 @@ struct WgradPlan {
   Drop drop;       // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
   int drop_layer;
   bool wide;       // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
+  // pair (pair_wgrad): slices [nsplit1, nsplit) sum A2^T [B1s | B2s] (same shape and strides) into
+  // the same gradient; A2 == nullptr: one problem
+  const float* A2 = nullptr;
+  const float *B1s = nullptr, *B2s = nullptr;
+  int nsplit1 = 0;
 };
+// Turn a planned weight gradient into a pair with a second problem of the same shape (each problem
+// gets about half of the planned slices; one launch, one reduce, no accumulate pass).
+void pair_wgrad(WgradPlan& p, const float* A2, const float* B1s, const float* B2s);
 void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
                 int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                 int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,

@@ -28,8 +28,10 @@ using CfgGate = GemmCfg<32 * SMAML_GATE_WM, 128 * SMAML_GATE_WN, SMAML_GATE_WM, 
 // fused step uses (config 4 A/B with the bf16x6 products: 256-row 1.137 -> 128-row 1.031 ms per sample-step)
 using CfgGateP = GemmCfg<128, 128 * SMAML_GATE_WN, 4, SMAML_GATE_WN, true, true, SMAML_GATE_BK, SMAML_X6_GATE>;
 using CfgNN = GemmCfg<64, 128, 2, 2, true, false, SMAML_NN_BK, SMAML_X6_BWD>;  // C = A . B   (B n-contiguous)
+// (weight gradients keep the padded MC images: the swizzle's address math measured 502 -> 509 ms there,
+// profiles/r03_ab_wide_swizzle_crecompute.log, and their LDS sets no occupancy: one workgroup per CU)
 using CfgTN = GemmCfg<SMAML_TN_BM, SMAML_TN_BN, SMAML_TN_WM, SMAML_TN_WN, false, false, SMAML_TN_BK, SMAML_X6_WGRAD,
-                      SMAML_TN_NST>;  // C = A^T . B (split-K weight grads)
+                      SMAML_TN_NST, false>;  // C = A^T . B (split-K weight grads)
 
 // ------------------------------------------------------------------------------------
 // Block-wide deterministic sum (fixed shuffle tree + fixed wave order).
@@ -1616,18 +1618,26 @@ __device__ __forceinline__ void wgrad_glds_loop(const float* A, int64_t K, const
 #ifndef SMAML_WGRAD_WIDE
 #define SMAML_WGRAD_WIDE 1
 #endif
-using CfgTW = GemmCfg<256, 256, 4, 2, false, false, SMAML_TN_BK, SMAML_X6_WGRAD, SMAML_TN_NST>;
+using CfgTW = GemmCfg<256, 256, 4, 2, false, false, SMAML_TN_BK, SMAML_X6_WGRAD, SMAML_TN_NST, false>;
 template <class C>
 constexpr int wgrad_smem_floats() {
   return std::is_same<C, CfgTN>::value ? WG_SMEM : C::SMEM_FLOATS;
 }
 
 // One weight-gradient workgroup: block L of a launch over ((ngroups + 7) / 8 * 8 * ntile) blocks.
+// Pair (A2 != null): slices [nsplit1, nsplit) of each task sum a second problem of the same shape,
+// A2^T [B1s | B2s] (the tangent weight gradient's dG^T [Rx | Rh] beside R(dG)^T [x | h]), into the
+// same partial slabs; its slices carry no bias column (zeros).
+struct WgPair {
+  const float* A2;
+  const float *B1s, *B2s;
+  int nsplit1;
+};
 template <class C, bool DROP>
 __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
                                             int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn, int ntile,
                                             int nsplit, int ngroups, float* __restrict__ part, int ldp, int with_bias,
-                                            const Drop& dr, int drop_layer, float* smem) {
+                                            const Drop& dr, int drop_layer, float* smem, const WgPair& pr) {
   // XCD-aware: the ntile output tiles of one (split, task) group stream the same K rows of
   // A and B, so they are placed on one XCD (blocks 8 apart) to share its L2. Speed only.
   const int j = L >> 3;
@@ -1635,11 +1645,18 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
   if (g >= ngroups) return;
   const int z = g / nsplit, split = g - z * nsplit;
   const int tm = tile / ntn, tn = tile - tm * ntn;
+  const bool sec = pr.A2 != nullptr && split >= pr.nsplit1;  // this slice belongs to the pair's second problem
+  if (sec) {
+    A = pr.A2;
+    lb.B1 = pr.B1s;
+    lb.B2 = pr.B2s;
+  }
+  if (sec) with_bias = 0;
   RowMajorMC la{A + (int64_t)z * a_zstride, lb.K, Mrows};
   WgB b = lb;
   if (b.B1) b.B1 += (int64_t)z * b1_zstride;
   if (b.B2) b.B2 += (int64_t)z * b2_zstride;
-  const int64_t kbeg = (int64_t)split * kchunk;
+  const int64_t kbeg = (int64_t)(sec ? split - pr.nsplit1 : split) * kchunk;
   const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
   Acc<C> acc;
@@ -1701,10 +1718,10 @@ template <class C, bool DROP>
 __global__ __launch_bounds__(C::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
                                               int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
-                                              int ldp, int with_bias, Drop dr, int drop_layer) {
+                                              int ldp, int with_bias, Drop dr, int drop_layer, WgPair pr) {
   __shared__ float smem[wgrad_smem_floats<C>()];
   wgrad_block<C, DROP>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, nsplit,
-                    ngroups, part, ldp, with_bias, dr, drop_layer, smem);
+                    ngroups, part, ldp, with_bias, dr, drop_layer, smem, pr);
 }
 
 // Several weight gradients in ONE launch (the LSTM layers of a small-grid backward: at batch 1 each
@@ -1727,11 +1744,11 @@ __global__ __launch_bounds__(CfgTN::NTH) void k_wgrad_multi(WgMulti mp, Drop dr)
   if (DROP && p.drop_layer >= 0)
     wgrad_block<CfgTN, true>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
                       p.kchunk, p.ntn, p.ntm * p.ntn, p.nsplit, p.nsplit * p.Z, p.part, p.ldp, p.with_bias ? 1 : 0,
-                      dr, p.drop_layer, smem);
+                      dr, p.drop_layer, smem, WgPair{});
   else
     wgrad_block<CfgTN, false>((int)blockIdx.x - mp.blk[q], p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride,
                        p.kchunk, p.ntn, p.ntm * p.ntn, p.nsplit, p.nsplit * p.Z, p.part, p.ldp, p.with_bias ? 1 : 0,
-                       dr, -1, smem);
+                       dr, -1, smem, WgPair{});
 }
 
 #ifndef SMAML_REDUCE_UNROLL
@@ -1841,6 +1858,17 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   p.wide = wide;
 }
 
+void pair_wgrad(WgradPlan& p, const float* A2, const float* B1s, const float* B2s) {
+  const int64_t ktiles = (p.K + CfgTN::BK - 1) / CfgTN::BK;
+  const int64_t n1 = std::max<int64_t>(1, p.nsplit / 2);
+  p.kchunk = ((ktiles + n1 - 1) / n1) * CfgTN::BK;
+  p.nsplit1 = (int)((p.K + p.kchunk - 1) / p.kchunk);
+  p.nsplit = 2 * p.nsplit1;  // <= the planned count: fits the partial-slab buffer
+  p.A2 = A2;
+  p.B1s = B1s;
+  p.B2s = B2s;
+}
+
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
   WgB lb;
   lb.B1 = p.B1;
@@ -1856,7 +1884,7 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
 #define SMAML_WGRAD_LAUNCH(CFG, D_)                                                                            \
   k_wgrad<CFG, D_><<<grid, CFG::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, \
                                              p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0, \
-                                             p.drop, D_ ? p.drop_layer : -1)
+                                             p.drop, D_ ? p.drop_layer : -1, WgPair{p.A2, p.B1s, p.B2s, p.nsplit1})
   if (p.wide) {
     if (drop)
       SMAML_WGRAD_LAUNCH(CfgTW, true);
