@@ -991,7 +991,7 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
 // ====================================================================================
 // LSTM backward step (layer l, time t), one anti-diagonal of (l, t) per launch (BwdWave):
 //   dh = [dG(l+1,t) | dG(l,t+1)] . [W_ih(l+1) ; W_hh(l)]  (+ head dh_T at l = L-1, t = T-1)
-//                                                   [fp32 MFMA, K = 8H, 4H at the borders]
+//                                   [f32-accurate bf16x6 products, K = 8H, 4H at the borders]
 //   dc = dc_carry + dh * o * (1 - tanh(c_t)^2)
 //   dG_t = [dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tanh(c_t)*o(1-o)]  (in place over G_t)
 //   dc_carry = dc * f

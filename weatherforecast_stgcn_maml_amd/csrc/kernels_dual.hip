@@ -8,8 +8,9 @@
 //   k_head_dual        pred, R(pred) -> dpred, R(dpred)
 //   k_gemm_nn_dual     dh_T / dX and their tangents ([R(A) | A] . [W ; U])
 //   k_lstm_bwd_dual    BPTT cell step and its tangent (product rule through every gate)
-// The tangent weight gradient R(dW) = R(dG)^T [x|h] + dG^T [Rx|Rh] reuses k_wgrad (two
-// accumulating passes). All contractions are fp32 MFMA (gemm_core.h).
+// The tangent weight gradient R(dW) = R(dG)^T [x|h] + dG^T [Rx|Rh] reuses k_wgrad (layers >= 1:
+// one paired launch, layer 0: two accumulating passes). All contractions take f32 operands with
+// f32 accumulation through gemm_core.h (f32-accurate bf16x6 products by default).
 #include "kernels.h"
 #include "loaders.h"
 
