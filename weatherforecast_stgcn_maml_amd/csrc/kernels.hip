@@ -284,6 +284,58 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
   }
 }
 
+// fwd_cell through the transposed epilogue (loaders.h gate_epilogue_t): per item (row, 4 units)
+// one 16-B c_{t-1} load and six 16-B stores (i, f, g, o, c, h).
+template <int H, class CG>
+__device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __restrict__ th, const LayerOff& lo,
+                                           float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
+                                           int m0, int ug, int t, int M, float* smem) {
+  const int j = ug * 32 + (int)(threadIdx.x & 31);
+  float bsum[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bsum[g] = j < H ? th[lo.bih + g * H + j] + th[lo.bhh + g * H + j] : 0.f;
+  const bool full = m0 + CG::BM <= M, past = t > 0;
+  const uint32_t tM = (uint32_t)t * (uint32_t)M, pM = past ? (uint32_t)M * H : 0u;
+  auto coords = [&](int ml, int u, int& m, int& jq) {
+    m = m0 + ml;
+    jq = ug * 32 + u;
+    if (!full) m = min(m, M - 1);  // clamped rows read a valid address (not stored)
+    jq = min(jq, H - 4);
+  };
+  gate_epilogue_t<CG>(
+      acc, bsum, smem,
+      [&](int ml, int u) {
+        int m, jq;
+        coords(ml, u, m, jq);
+        return ldo(Cz, 4u * ((tM + (uint32_t)m) * H - pM + (uint32_t)jq));  // c_{t-1} (t = 0: selected out)
+      },
+      [&](int ml, int u, const float4 (&pre)[4], const float4& cpv) {
+        if ((!full && m0 + ml >= M) || ug * 32 + u >= H) return;
+        const uint32_t row = tM + (uint32_t)(m0 + ml), jq = (uint32_t)(ug * 32 + u);
+        const float4 cp = sel4(past, cpv);
+        float4 gi, gf, gg, go, c, hh;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float i_ = sigmoidf_(f4get(pre[0], e)), f_ = sigmoidf_(f4get(pre[1], e));
+          const float g_ = tanhf_(f4get(pre[2], e)), o_ = sigmoidf_(f4get(pre[3], e));
+          const float c_ = lstm_cell_c(i_, f_, g_, f4get(cp, e));
+          f4set(gi, e, i_);
+          f4set(gf, e, f_);
+          f4set(gg, e, g_);
+          f4set(go, e, o_);
+          f4set(c, e, c_);
+          f4set(hh, e, o_ * tanhf_(c_));
+        }
+        const uint32_t og = 4u * (row * (4 * H) + jq), oh = 4u * (row * H + jq);
+        sto(Gz, og, gi);
+        sto(Gz, og + 4u * H, gf);
+        sto(Gz, og + 8u * H, gg);
+        sto(Gz, og + 12u * H, go);
+        sto(Cz, oh, c);
+        sto(Hz, oh, hh);
+      });
+}
+
 template <int H, bool DROP, bool IMG = false>
 __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                               float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
@@ -338,7 +390,10 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     }
   }
 
-  fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
+  if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1)
+    fwd_cell_t<H, CfgGate>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem);
+  else
+    fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
 }
 
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,

@@ -104,6 +104,67 @@ __device__ __forceinline__ void fwd_dual_tangent_epi(const Acc<CfgGateD>& at, co
   }
 }
 
+// The same through the transposed epilogue (loaders.h gate_epilogue_t; KEPT steps, whose primal is
+// read from memory anyway): per item (row, 4 units) six 16-B loads (i, f, g, o, c_{t-1},
+// R c_{t-1}) and six 16-B stores (R i, R f, R g, R o, R c, R h).
+template <int H>
+__device__ __forceinline__ void fwd_dual_tangent_epi_t(const Acc<CfgGateD>& at, const float (&bu)[4],
+                                                       const float* __restrict__ Gz, float* __restrict__ RGz,
+                                                       const float* __restrict__ Cz, float* __restrict__ RCz,
+                                                       float* __restrict__ RHz, int m0, int ug, uint32_t tM, int M,
+                                                       int t, float* smem) {
+  constexpr int G4 = 4 * H;
+  const bool full = m0 + CfgGateD::BM <= M, past = t > 0;
+  const uint32_t pM = past ? (uint32_t)M * H : 0u;
+  struct V {
+    float4 g[4], cp, rcp;
+  };
+  gate_epilogue_t<CfgGateD>(
+      at, bu, smem,
+      [&](int ml, int u) {
+        const int m = full ? m0 + ml : min(m0 + ml, M - 1);  // clamped rows: valid address, not stored
+        const uint32_t jq = (uint32_t)min(ug * 32 + u, H - 4);
+        const uint32_t row = tM + (uint32_t)m;
+        const uint32_t og = 4u * (row * G4 + jq), oh = 4u * (row * H + jq);
+        V v;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v.g[g] = ldo(Gz, og + 4u * g * H);
+        v.cp = ldo(Cz, oh - 4u * pM);
+        v.rcp = ldo(RCz, oh - 4u * pM);
+        return v;
+      },
+      [&](int ml, int u, const float4 (&rpre)[4], const V& v) {
+        if ((!full && m0 + ml >= M) || ug * 32 + u >= H) return;
+        const uint32_t row = tM + (uint32_t)(m0 + ml), jq = (uint32_t)(ug * 32 + u);
+        const float4 cp = sel4(past, v.cp), rcp = sel4(past, v.rcp);
+        float4 ri, rf, rg, ro, rc, rh;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gi = f4get(v.g[0], e), gf = f4get(v.g[1], e), gg = f4get(v.g[2], e), go = f4get(v.g[3], e);
+          const float ri_ = gi * (1.f - gi) * f4get(rpre[0], e);
+          const float rf_ = gf * (1.f - gf) * f4get(rpre[1], e);
+          const float rg_ = (1.f - gg * gg) * f4get(rpre[2], e);
+          const float ro_ = go * (1.f - go) * f4get(rpre[3], e);
+          const float cpe = f4get(cp, e);
+          const float rc_ = lstm_cell_rc(gi, gf, gg, cpe, ri_, rf_, rg_, f4get(rcp, e));
+          const float tc = tanhf_(lstm_cell_c(gi, gf, gg, cpe));
+          f4set(ri, e, ri_);
+          f4set(rf, e, rf_);
+          f4set(rg, e, rg_);
+          f4set(ro, e, ro_);
+          f4set(rc, e, rc_);
+          f4set(rh, e, ro_ * tc + go * (1.f - tc * tc) * rc_);
+        }
+        const uint32_t og = 4u * (row * G4 + jq), oh = 4u * (row * H + jq);
+        sto(RGz, og, ri);
+        sto(RGz, og + 4u * H, rf);
+        sto(RGz, og + 8u * H, rg);
+        sto(RGz, og + 12u * H, ro);
+        sto(RCz, oh, rc);
+        sto(RHz, oh, rh);
+      });
+}
+
 // IMG: the weight tiles of theta and U come from their pre-split images (launch_split_gate).
 template <int H, bool KEPT, bool DROP, bool IMG>
 __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
@@ -229,6 +290,15 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
                                           SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
                                                        {cin, wh, wrx, wh}, H},
                                           m0, n0, 0, cin + wh + wrx + wh, at, smem);
+  }
+  if constexpr (KEPT && SMAML_FWD_EPI_T && CfgGateD::WAVES_N == 1) {
+    // (KEPT: the primal gates come from memory; the non-kept path re-reads the gates this lane itself
+    // stored above, which needs the accumulator-layout epilogue's lane <-> element mapping)
+    float bu[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bu[g] = j < H ? u[lo.bih + g * H + j] + u[lo.bhh + g * H + j] : 0.f;
+    fwd_dual_tangent_epi_t<H>(at, bu, Gz, RGz, Cz, RCz, RHz, m0, ug, tM, M, t, smem);
+    return;
   }
   if (j >= H) return;
   float bu[4];

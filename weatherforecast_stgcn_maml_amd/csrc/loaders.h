@@ -637,9 +637,69 @@ struct HalfRows {  // the epilogue's view of one row half of C's tile
 };
 
 __device__ __forceinline__ float4 sel4(bool c, float4 a) { return c ? a : f4zero(); }
+__device__ __forceinline__ void f4set(float4& v, int e, float x) {
+  if (e == 0) v.x = x;
+  if (e == 1) v.y = x;
+  if (e == 2) v.z = x;
+  if (e == 3) v.w = x;
+}
+#ifndef SMAML_FWD_EPI_T
+#define SMAML_FWD_EPI_T 1  // fused forward steps' cell epilogues through gate_epilogue_t (float4 items)
+#endif
 
 // Row offset (within the 32-row tile) of accumulator register r: (r&3) + 8*(r>>2).
 __device__ __forceinline__ constexpr int racc(int r) { return (r & 3) + 8 * (r >> 2); }
+
+__device__ __forceinline__ void sto(float* base, uint32_t byteoff, const float4& v) {
+  *reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + byteoff) = v;
+}
+
+// Transposed gate epilogue of the fused forward steps (round 3). A gate tile of C (WAVES_N == 1:
+// wave w owns tile rows 32w .. 32w+31; its 4 accumulator tiles are the 4 gates of the tile's 32
+// units) is handed out in items of 4 consecutive units of one row, so the epilogue's loads and
+// stores are 16 B wide (4x fewer memory instructions than the accumulator layout's 4-B accesses):
+// each wave writes its own rows, plus badd, through a private 8 KB of the (idle) staging LDS in two
+// 16-row passes (the 32-float gate blocks of row rl swapped pairwise when (rl ^ rl >> 2) is odd, so
+// the ds_write_b32 and ds_read_b128 are bank-conflict free) and reads them back as float4 items.
+// Per pass a lane has 2 items: ld(ml, u) issues both items' loads before st(ml, u, pre, v) stores
+// either (ml = tile row, u = tile unit, pre[g] = gate g of units u .. u+3). Starts with a barrier
+// (the mainloop's last LDS reads), leaves the LDS in use until the caller's next barrier.
+template <class C, class LD, class ST>
+__device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (&badd)[4], float* smem, LD&& ld,
+                                                ST&& st) {
+  static_assert(C::WAVES_N == 1 && C::WTM == 1 && C::WTN == 4, "wave = 32 rows x 4 gates x 32 units");
+  static_assert(C::SMEM_FLOATS >= C::WAVES_M * 2048, "8 KB of LDS per wave");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, jj = lane & 31, h = lane >> 5;
+  float* ws = smem + wave * 2048;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    __syncthreads();  // p = 0: the mainloop's LDS reads are done; p = 1: pass 0's reads are done
+#pragma unroll
+    for (int r = 8 * p; r < 8 * p + 8; ++r) {
+      const int rl = racc(r) + 4 * h - 16 * p;
+      const int sw = (rl ^ (rl >> 2)) & 1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ws[rl * 128 + (g ^ sw) * 32 + jj] = acc.v[0][g][r] + badd[g];
+    }
+    __syncthreads();
+    decltype(ld(0, 0)) v[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = lane + 64 * k;
+      v[k] = ld(wave * 32 + 16 * p + (i >> 3), 4 * (i & 7));
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = lane + 64 * k, rl = i >> 3, q = i & 7;
+      const int sw = (rl ^ (rl >> 2)) & 1;
+      float4 pre[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pre[g] = ld4(ws + rl * 128 + (g ^ sw) * 32 + 4 * q);
+      st(wave * 32 + 16 * p + rl, 4 * q, pre, v[k]);
+    }
+  }
+}
+
 
 // LSTM kernels are instantiated per hidden size (compile-time strides).
 #define SMAML_DISPATCH_H(HV, ...)                              \
