@@ -198,6 +198,7 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target) {
   __syncthreads();
 }
 int coop_blocks(int items);  // blocks of a cooperative bookkeeping launch over `items` (task, chunk) items
+hipError_t launch_coop(const void* fn, int nb, void** args, hipStream_t s);  // NT threads per block
 #ifndef SMAML_WGRAD_MAXSPLIT
 #define SMAML_WGRAD_MAXSPLIT 128  // split-K slices per weight gradient (partial-slab capacity)
 #endif

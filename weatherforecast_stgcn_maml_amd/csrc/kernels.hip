@@ -2080,13 +2080,27 @@ __global__ __launch_bounds__(NT) void k_inner_sgd(float* __restrict__ theta, con
 
 int coop_blocks(int items) { return items < 1024 ? items : 1024; }
 
+// The grid-barrier kernels (<= 1024 blocks of 256 threads, a few VGPRs, no LDS: 4 blocks per CU, all
+// co-resident) go through hipLaunchCooperativeKernel, whose launch-time check guarantees that
+// residency. SMAML_COOP=0 in the environment launches the same grid with a plain launch instead
+// (same kernels, same results; the profiler runs use it: rocprofv3 crashed in its exit handlers
+// after cooperative launches).
+hipError_t launch_coop(const void* fn, int nb, void** args, hipStream_t s) {
+  static const bool coop = [] {
+    const char* e = std::getenv("SMAML_COOP");
+    return !(e && e[0] == '0');
+  }();
+  if (coop) return hipLaunchCooperativeKernel(fn, dim3(nb), dim3(NT), args, 0, s);
+  return hipLaunchKernel(fn, dim3(nb), dim3(NT), args, 0, s);
+}
+
 hipError_t launch_inner_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, double* part, float lr,
                             float max_norm, float* norm_out, float* coef_out, unsigned* bar, unsigned& bar_count) {
   const int nb = coop_blocks(SQB * Z);
   bar_count += (unsigned)nb;
   unsigned target = bar_count;
   void* args[] = {&theta, &g, &P, &Z, &part, &lr, &max_norm, &norm_out, &coef_out, &bar, &target};
-  return hipLaunchCooperativeKernel((const void*)k_inner_sgd, dim3(nb), dim3(NT), args, 0, s);
+  return launch_coop((const void*)k_inner_sgd, nb, args, s);
 }
 
 __global__ void k_sum_tasks(const float* __restrict__ g, int64_t P, int Z, float* __restrict__ out) {

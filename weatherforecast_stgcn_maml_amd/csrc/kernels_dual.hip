@@ -851,7 +851,7 @@ hipError_t launch_sweep_update(hipStream_t s, float* V, const float* X, float al
   bar_count += (unsigned)nb;
   unsigned target = bar_count;
   void* args[] = {&V, &X, &alpha, &G, &P, &Z, &part, &norms, &coefs, &max_norm, &U, &bar, &target};
-  return hipLaunchCooperativeKernel((const void*)k_sweep_update, dim3(nb), dim3(NT), args, 0, s);
+  return launch_coop((const void*)k_sweep_update, nb, args, s);
 }
 
 
