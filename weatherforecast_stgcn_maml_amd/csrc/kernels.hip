@@ -1584,9 +1584,6 @@ struct WgBDrop {
 #endif
 // iglp_opt strategy for the weight-gradient mainloop (staged split: none, A/B 493 -> 483 ms)
 constexpr int kWgradIG = CfgTN::X6S ? -1 : SMAML_IGLP;
-#ifndef SMAML_WGRAD_TILE_LOADERS
-#define SMAML_WGRAD_TILE_LOADERS 0  // staged-split weight gradients through the MCKt / WgBt tile loaders
-#endif
 #ifndef SMAML_WGRAD_GLDS_IGLP
 #define SMAML_WGRAD_GLDS_IGLP -1
 #endif
@@ -1738,16 +1735,10 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
         wgrad_glds_loop(Az, lb.K, b, n0, kbeg, kend, acc, smem, nh);
       }
     }
-  } else if (SMAML_WGRAD_TILE_LOADERS && C::X6S && (lb.c2 == 0 || lb.c1 % C::BN == 0)) {
-    const MCKt lt{A + (int64_t)z * a_zstride, lb.K, Mrows};
-    const WgBt bt{b.B1, b.B2, b.c1, b.c2, b.K, b.Mshift};
-    if (tn == 0 && with_bias)
-      gemm_mainloop<C, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
-    else
-      gemm_mainloop<C, kWgradIG>(lt, bt, m0, n0, (int)kbeg, (int)kend, acc, smem);
   } else if (tn == 0 && with_bias) {
-    // (the branch-free MCKt / WgBt tile loaders measured slower here with the f32 MFMA: wgrad
-    // 723 -> 820 ms per meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log)
+    // (branch-free tile loaders for both operands measured slower here twice: with the f32 MFMA,
+    // wgrad 723 -> 820 ms per meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log; with the staged
+    // bf16x6 split and 256 x 256 tiles, 498 -> 552 ms, profiles/r03_ab_wgrad_tile_loaders.log)
     gemm_mainloop<C, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
     gemm_mainloop<C, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);

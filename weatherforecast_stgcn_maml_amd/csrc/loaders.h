@@ -354,63 +354,6 @@ struct SegGateImg {
   }
 };
 
-// MC operand [K][cols] (cols contiguous) with zero rows at k >= K (split-K weight gradients: the
-// K tail is real, so it is zero-filled by a select, not clamped).
-struct MCKt {
-  static constexpr bool kTileFetch = true;
-  const float* p;
-  int64_t K;
-  int cols;
-  template <int ROWS, int F4, int NTH, bool KC, int BK>
-  __device__ __forceinline__ void fetch(int col0, int k0, float4 (&r)[F4]) const {
-    static_assert(!KC, "MCKt is an n-contiguous operand");
-    const float* b = p + (int64_t)k0 * cols;
-    const int kmax = (int)min<int64_t>(K - k0, (int64_t)BK) - 1;  // last valid k row of this tile
-#pragma unroll
-    for (int i = 0; i < F4; ++i) {
-      const int f = (int)threadIdx.x + NTH * i;
-      const int kk = f / (ROWS / 4);
-      const int c = min(col0 + 4 * (f % (ROWS / 4)), cols - 4);
-      const float4 v = ldo(b, 4u * (uint32_t)(min(kk, kmax) * cols + c));
-      r[i] = kk <= kmax ? v : f4zero();
-    }
-  }
-};
-
-// Weight-gradient B operand (WgB) as a tile loader: Bcat[k] = [B1[k] (c1) | B2[k - Mshift] (c2)],
-// zero for k >= K, for B2 rows k < Mshift (h_{-1} = 0) and for a null B1 (no layer-0 tangent).
-// Requires every BN-wide column tile to lie inside one block (c1 a multiple of BN, or c2 = 0);
-// k_wgrad falls back to WgB otherwise.
-struct WgBt {
-  static constexpr bool kTileFetch = true;
-  const float* B1;
-  const float* B2;
-  int c1, c2;
-  int64_t K, Mshift;
-  template <int ROWS, int F4, int NTH, bool KC, int BK>
-  __device__ __forceinline__ void fetch(int col0, int k0, float4 (&r)[F4]) const {
-    static_assert(!KC, "WgBt is an n-contiguous operand");
-    const bool first = col0 < c1;  // uniform: which block this column tile reads
-    const int ld = first ? c1 : c2;
-    const int cbase = first ? col0 : col0 - c1;
-    const int64_t shift = first ? 0 : Mshift;
-    const float* src = first ? B1 : B2;
-    const int64_t kv0 = (int64_t)k0 - shift;  // source row of the tile's first k
-    const int64_t nrows = K - shift;          // valid source rows [0, nrows)
-#pragma unroll
-    for (int i = 0; i < F4; ++i) {
-      const int f = (int)threadIdx.x + NTH * i;
-      const int kk = f / (ROWS / 4);
-      const int c = min(cbase + 4 * (f % (ROWS / 4)), ld - 4);
-      const int64_t ks = kv0 + kk;
-      const bool ok = src && ks >= 0 && ks < nrows;
-      const int64_t kc = ks < 0 ? 0 : (ks >= nrows ? nrows - 1 : ks);
-      const float4 v = src ? ldo(src + kc * ld, 4u * (uint32_t)c) : f4zero();
-      r[i] = ok ? v : f4zero();
-    }
-  }
-};
-
 // Dropout mask on the x segment of an LSTM layer's input: x = drop(h_{l-1}) of one
 // (task, t) slab; element (m, k) has index base + m*H + k (kernels.h Drop, kind 2).
 struct XDrop {
