@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 profile of the default bench at HEAD: kernel trace + stats, then separate rocprofv3 --pmc
-# passes (FETCH_SIZE, WRITE_SIZE, MFMA busy, SQ instruction mix). SMAML_COOP=0: the two grid-barrier
+# passes (FETCH_SIZE, WRITE_SIZE, MFMA busy, SQ instruction mix). SMAML_COOP=0 (the default since): the grid-barrier
 # kernels are launched with a plain launch of the same grid (rocprofv3 crashed in its exit handlers
 # after hipLaunchCooperativeKernel). Each pass has its own time limit; the first failure ends the script.
 set -u

@@ -2071,15 +2071,17 @@ __global__ __launch_bounds__(NT) void k_inner_sgd(float* __restrict__ theta, con
 
 int coop_blocks(int items) { return items < 1024 ? items : 1024; }
 
-// The grid-barrier kernels (<= 1024 blocks of 256 threads, a few VGPRs, no LDS: 4 blocks per CU, all
-// co-resident) go through hipLaunchCooperativeKernel, whose launch-time check guarantees that
-// residency. SMAML_COOP=0 in the environment launches the same grid with a plain launch instead
-// (same kernels, same results; the profiler runs use it: rocprofv3 crashed in its exit handlers
-// after cooperative launches).
+// The grid-barrier kernels (<= 1024 blocks of 256 threads, a few VGPRs, no LDS: 4 blocks per CU) are
+// launched with a plain launch of that grid: every block becomes resident once the CU slots free up
+// (a plain launch has the same residency as a cooperative one; MI355X_MICROARCH "coop-launch"), and
+// blocks of another kernel never wait on ours, so a partially resident grid only waits. Cooperative
+// launches (SMAML_COOP=1) measured pathological with two processes on one GPU (the self-launched
+// 2-rank bench over gloo: 22.3 s per meta-step against 1.9 s in round 2, the launch serialising
+// against the other process's queue), and rocprofv3 crashed in its exit handlers after them.
 hipError_t launch_coop(const void* fn, int nb, void** args, hipStream_t s) {
   static const bool coop = [] {
     const char* e = std::getenv("SMAML_COOP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (coop) return hipLaunchCooperativeKernel(fn, dim3(nb), dim3(NT), args, 0, s);
   return hipLaunchKernel(fn, dim3(nb), dim3(NT), args, 0, s);
