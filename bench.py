@@ -11,6 +11,10 @@ meta-gradient and a replicated clip + AdamW. Tasks are sharded round-robin over 
 the meta-batch is fixed, so scaling is "strong". Inputs are synthetic ERA5-shaped
 feature streams (portable numpy seeds 1000+j) resident in HBM before the timed region;
 weights are random-init with the reference's distributions.
+
+At N=1, after the headline timed region (never inside it), the same line also carries
+BASELINE config 4 (``adaptation``: regional fine-tuning, ms per batch-1 sample-step) and one
+rank's share of config 5 (``config5_rank_share``: 8 of the 64 stress tasks, ms per meta-step).
 """
 from __future__ import annotations
 
@@ -57,6 +61,10 @@ def parse():
     p.add_argument("--adapt-epochs", type=int, default=2,
                    help="after the timed region (N=1 only): BASELINE config-4 adaptation epochs to time and "
                         "report under 'adaptation' (0 = skip)")
+    p.add_argument("--cfg5-share-tasks", type=int, default=8,
+                   help="after the timed region (N=1, config 2 only): time one second-order meta-step of this "
+                        "many BASELINE config-5 tasks (8 = one rank's share of the 64 tasks at 8 GPUs) and report "
+                        "it under 'config5_rank_share' (0 = skip)")
     p.add_argument("--task-group", default="auto",
                    help="tasks per pass of the C driver: an int, 'all', or 'auto' (default: groups small "
                         "enough that every inner step's primal stays resident for the second-order sweep)")
@@ -188,6 +196,59 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
         out["launches_per_sample_step"] = {k: v["launches"] / breakdown_steps for k, v in kern.items()
                                            if v["launches"] > 0}
     return out, feats
+
+
+def config5_share_bench(tasks, steps=1, warmup=1):
+    """BASELINE config 5 (stress: 64 tasks, N=1024 (32x32 grid), Hc=512, LSTM 4x128, K=10, second
+    order), the share one rank holds when the driver's 8-GPU run shards the 64 tasks round-robin:
+    ``tasks`` tasks on this GPU, ``warmup`` untimed + ``steps`` timed meta-steps on a fresh
+    MetaLearner, after (never inside) the headline timed region. The 8-GPU meta-step is this share
+    plus one all-reduce of the 606,304-float meta-gradient."""
+    import torch
+
+    from weatherforecast_stgcn_maml_amd import synth
+    from weatherforecast_stgcn_maml_amd.config import SEED, MamlConfig, ModelDims
+    from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
+    from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
+
+    d = ModelDims(num_nodes=1024, hidden_channels=512)
+    cfg = MamlConfig(inner_steps=10, batch=32, order=2)
+    lats, lons = synth.region_grid(n_lat=32, n_lon=32)
+    ei, _, _ = build_spatial_graph(lats, lons, 4)
+    P = synth.init_params(SEED, d)
+    names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
+    T_total = stream_len_for(cfg, d)
+    ids = list(range(tasks))
+    feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T_total) for j in ids]
+    ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
+                     ei, device=f"cuda:{torch.cuda.current_device()}", dropout_seed=SEED)
+    ml.set_tasks(feats, task_ids=ids)
+    for _ in range(warmup):
+        ml.meta_step(sync=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(steps):
+        res = ml.meta_step(sync=False)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    qmse = float(res.losses[-1].sum().item()) / tasks
+    kept = ml.ctx.so_kept_steps()
+    ml.ctx.close()
+    del ml
+    torch.cuda.empty_cache()
+    assert np.isfinite(qmse), qmse
+    flops = algorithmic_flops(d, tasks, cfg.inner_steps, cfg.batch, cfg.order)
+    ms = elapsed / steps * 1e3
+    return {
+        "metric": "config-5 rank share: ms per second-order meta-step of one rank's tasks",
+        "value": ms, "unit": "ms/meta-step", "higher_is_better": False, "steps": steps, "warmup": warmup,
+        "achieved_tflops_whole_step": flops / (elapsed / steps) / 1e12, "query_mse": qmse,
+        "config": {"workload": f"BASELINE config 5 share: {tasks} of 64 tasks x B={cfg.batch} x T={d.window_size} x "
+                               f"N={d.num_nodes} x C={d.input_channels}, Hc={d.hidden_channels}, LSTM "
+                               f"{d.lstm_num_layers}x{d.lstm_hidden_size}, K={cfg.inner_steps} inner steps",
+                   "tasks": tasks, "so_kept_steps": kept},
+    }
 
 
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
@@ -386,6 +447,12 @@ def main():
         torch.cuda.empty_cache()
         ad, _ = adaptation_bench(ModelDims(num_nodes=441, hidden_channels=256), P, ei, epochs=args.adapt_epochs)
         out["adaptation"] = ad
+    if world == 1 and args.cfg5_share_tasks > 0 and args.config == 2:
+        if "ml" in locals():
+            ml.ctx.close()
+            del ml
+            torch.cuda.empty_cache()
+        out["config5_rank_share"] = config5_share_bench(args.cfg5_share_tasks)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
