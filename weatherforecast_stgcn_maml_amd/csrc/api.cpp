@@ -238,11 +238,11 @@ struct smaml_ctx {
   // batch-1 adaptation: GCN features per window of task 0 (the frozen GCN stack without dropout
   // is a pure function of the window, F2), filled on first use and reused by later epochs.
   // Invalidated by smaml_set_graph / _set_gcn_params / _set_tasks.
-  char* gcn_wimg = nullptr;
+  char* gcn_wimg = nullptr;   // pre-split GCN weight images of the fused t >= 1 GCN (kernels_gcn.hip)
   char* gimg_buf = nullptr;   // pre-split gate-GEMM weight images (prep_gate_images)
   int64_t gimg_cap = 0;
   unsigned* bar = nullptr;    // grid-barrier arrival counter of the cooperative bookkeeping kernels
-  unsigned bar_count = 0;     // arrivals so far (host mirror: launches are stream-ordered)  // pre-split GCN weight images of the fused t >= 1 GCN (kernels_gcn.hip)
+  unsigned bar_count = 0;     // arrivals so far (host mirror: launches are stream-ordered)
   float* ad_F = nullptr;
   int64_t ad_cap = 0;              // windows the cache holds
   std::vector<uint8_t> ad_valid;   // per window start
