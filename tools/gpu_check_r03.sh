@@ -21,7 +21,7 @@ if [ -n "${AB_VARIANTS:-}" ]; then
   : > gpurun_out/${TAG}_ab.log
   for round in $(seq 1 ${AB_ROUNDS:-2}); do
     for v in libsmaml.so ${AB_VARIANTS}; do
-      SMAML_LIB=weatherforecast_stgcn_maml_amd/$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-sample-steps 0 --adapt-epochs 0 ${AB_BENCH_ARGS:-} > gpurun_out/ab_tmp.log 2>&1 || exit $?
+      SMAML_LIB=weatherforecast_stgcn_maml_amd/$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-sample-steps 0 --adapt-epochs 0 --cfg5-share-tasks 0 ${AB_BENCH_ARGS:-} > gpurun_out/ab_tmp.log 2>&1 || exit $?
       echo "$v $(tail -1 gpurun_out/ab_tmp.log)" >> gpurun_out/${TAG}_ab.log
     done
   done
