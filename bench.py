@@ -95,23 +95,45 @@ def algorithmic_flops(d, tasks, K, B, order):
     return fo
 
 
+def cpu_threads():
+    """(threads used, os.cpu_count(), CPUs this process may run on). The reference runs torch's
+    CPU path with torch's default thread pool; the port is timed with one thread per CPU the
+    process may use (sched_getaffinity), which equals os.cpu_count() unless the host pins the
+    process to a subset (then os.cpu_count() threads would oversubscribe the CPUs it has)."""
+    n_os = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = n_os
+    return max(1, min(n_os, n_aff)), n_os, n_aff
+
+
 def cpu_baseline(d, n_steps, P, ei, feats):
     """Reference CPU path restated op for op (oracle.refcpu.ReferencePort: per-node nn.LSTM
-    loop, batch 1, MKLDNN), timed on this host's cores over a bounded sample."""
+    loop, batch 1, MKLDNN), timed on this host's cores over a bounded sample. Returns
+    (seconds per sample-step, threads used, os.cpu_count(), affinity CPUs)."""
     import torch
     from oracle import refcpu
     from weatherforecast_stgcn_maml_amd import synth
 
-    port = refcpu.ReferencePort(P, d, ei)
-    x, y = synth.sample_xy(feats, 0)
-    x = torch.from_numpy(np.ascontiguousarray(x))
-    y = torch.from_numpy(np.ascontiguousarray(y))
-    port.step(x, y)  # warm
-    t0 = time.perf_counter()
-    for i in range(n_steps):
-        xi, yi = synth.sample_xy(feats, i % 8)
-        port.step(torch.from_numpy(np.ascontiguousarray(xi)), torch.from_numpy(np.ascontiguousarray(yi)))
-    return (time.perf_counter() - t0) / n_steps, torch.get_num_threads()
+    threads, n_os, n_aff = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        port = refcpu.ReferencePort(P, d, ei)
+        x, y = synth.sample_xy(feats, 0)
+        x = torch.from_numpy(np.ascontiguousarray(x))
+        y = torch.from_numpy(np.ascontiguousarray(y))
+        port.step(x, y)  # warm
+        t0 = time.perf_counter()
+        for i in range(n_steps):
+            xi, yi = synth.sample_xy(feats, i % 8)
+            port.step(torch.from_numpy(np.ascontiguousarray(xi)), torch.from_numpy(np.ascontiguousarray(yi)))
+        t = (time.perf_counter() - t0) / n_steps
+        used = torch.get_num_threads()
+    finally:
+        torch.set_num_threads(prev)
+    return t, used, n_os, n_aff
 
 
 def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", breakdown_steps=96, warmup=True):
@@ -260,21 +282,31 @@ KERNEL_SYMBOL = {"gcn_layer": "k_gcn_layer|k_gcn_mlp", "lstm_fwd_step": "k_lstm_
                  "wgrad_reduce": "k_wgrad_reduce"}
 
 
-def measured_traffic(category, workload, world):
-    """Per-launch HBM bytes of a timing category from the committed PMC profile
-    (tools/prof_summary.py output), only when it was taken on this exact workload. PMC
-    counters cannot be read from inside a timed run, so the figure comes from the separate
-    rocprofv3 --pmc passes of the same bench command (profiles/, tools/gpu_profile.sh)."""
-    if world != 1 or not os.path.exists(TRAFFIC_JSON):
+def rank_workload(d, cfg, rank_tasks, config=2):
+    """Key of a per-rank workload in profiles/traffic.json: what one rank runs per meta-step (its
+    task count sets the task groups and so the per-launch bytes; at N=1 it is the whole meta-batch,
+    at N>1 rank 0's round-robin share, the largest)."""
+    return (f"BASELINE config {config} rank workload: {rank_tasks} tasks x B={cfg.batch} x T={d.window_size} x "
+            f"N={d.num_nodes} x C={d.input_channels}, Hc={d.hidden_channels}, LSTM {d.lstm_num_layers}x"
+            f"{d.lstm_hidden_size}, K={cfg.inner_steps} inner steps, order {cfg.order}")
+
+
+def measured_traffic(category, rank_key):
+    """Per-launch HBM bytes of a timing category from the committed PMC profiles
+    (tools/prof_summary.py output), only when one was taken on this exact per-rank workload
+    (rank_workload). PMC counters cannot be read from inside a timed run, so the figure comes from
+    separate rocprofv3 --pmc passes of a one-GPU bench run with the same per-rank task count."""
+    if not os.path.exists(TRAFFIC_JSON):
         return None
     try:
         t = json.load(open(TRAFFIC_JSON))
     except (OSError, ValueError):
         return None
-    if t.get("workload") != workload or category not in t.get("categories", {}):
+    prof = t.get("profiles", {}).get(rank_key)
+    if not prof or category not in prof.get("categories", {}):
         return None
-    c = dict(t["categories"][category])
-    c["source"] = t.get("profile") or "profiles/traffic.json"
+    c = dict(prof["categories"][category])
+    c["source"] = prof.get("profile") or "profiles/traffic.json"
     return c
 
 
@@ -308,7 +340,7 @@ def main():
     from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, shard_tasks, stream_len_for
 
-    from weatherforecast_stgcn_maml_amd.distributed import env_rank, init_from_env, max_over_ranks
+    from weatherforecast_stgcn_maml_amd.distributed import env_rank, init_from_env, max_over_ranks, min_over_ranks
 
     from weatherforecast_stgcn_maml_amd import _capi
 
@@ -343,6 +375,7 @@ def main():
     if not args.no_timing:
         ml.ctx.timing_collect()  # drop warmup records
         ml.ctx.timing(True)
+    ml.comm_timing = world > 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -358,9 +391,18 @@ def main():
     if not args.no_timing:
         ml.ctx.timing(False)
         kern = ml.ctx.timing_collect()
-    qsum = float(res.losses[-1].sum().item())
+    qsum = float(res.losses[-1].sum().item()) if len(mine) else 0.0
     qmse = qsum / max(len(mine), 1)
+    comm = None
     if world > 1:
+        ar_ms, ar_n = ml.comm_time_collect()
+        ml.comm_timing = False
+        comm = {
+            "allreduce_ms": max_over_ranks(ar_ms / max(ar_n, 1), f"cuda:{local}"),
+            "allreduce_ms_min_rank": min_over_ranks(ar_ms / max(ar_n, 1), f"cuda:{local}"),
+            "elapsed_min_ms": min_over_ranks(elapsed, f"cuda:{local}") * 1e3,
+            "elapsed_max_ms": max_over_ranks(elapsed, f"cuda:{local}") * 1e3,
+        }
         elapsed = max_over_ranks(elapsed, f"cuda:{local}")
         q = torch.tensor([qsum], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(q)
@@ -397,6 +439,7 @@ def main():
             "dropout": list(args.dropout),
             "products": _capi.build_info(),
         },
+        "rank_workload": rank_workload(d, cfg, len(mine), args.config),
         "meta_step_tflop": flops_meta / 1e12,
         "achieved_tflops_whole_step": flops_meta / (elapsed / args.steps) / 1e12,
         "query_mse": qmse,
@@ -408,7 +451,7 @@ def main():
         dom = max((k for k in kern if k not in ("misc", "wgrad_reduce")), key=lambda k: kern[k]["ms"])
         kd = kern[dom]
         ach = kd["flops"] / (kd["ms"] * 1e-3) / 1e12 if kd["ms"] > 0 else 0.0
-        traffic = measured_traffic(dom, out["config"]["workload"], world)
+        traffic = measured_traffic(dom, out["rank_workload"])
         x6 = forms.get(CAT_FAMILY.get(dom, ""), 0) > 0
         peak = PEAK_X6_TFLOPS if x6 else PEAK_FP32_MFMA_TFLOPS
         out["roofline"] = {
@@ -427,12 +470,18 @@ def main():
                               "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                               "launches_per_step": v["launches"] / args.steps}
                           for k, v in kern.items()}
+    if comm is not None:
+        # the all-reduce's exposed time per meta-step (HIP events on the compute stream: end of this
+        # rank's meta-step work -> reduced buffer ready, incl. waiting for the slowest rank), max /
+        # min over ranks, and every rank's own elapsed time over the timed region
+        out["collective"] = dict(comm, what="one all_reduce(SUM) of [meta-gradient | query-loss sum], "
+                                            f"{(ml.theta.numel() + 64) * 4 / 1e6:.2f} MB, per meta-step")
     if rank == 0 and world == 1 and args.cpu_sample_steps > 0:
-        t_step, cores = cpu_baseline(d, args.cpu_sample_steps, P, ei, feats[0])
+        t_step, cores, n_os, n_aff = cpu_baseline(d, args.cpu_sample_steps, P, ei, feats[0])
         sample_steps = args.tasks * (cfg.inner_steps + 1) * cfg.batch
         out["cpu_baseline"] = {
             "value": 1.0 / (sample_steps * t_step), "unit": "meta-steps/s", "cores": cores,
-            "kind": "port",
+            "os_cpu_count": n_os, "affinity_cpus": n_aff, "kind": "port",
             "sample": f"{args.cpu_sample_steps} batch-1 sample-steps (fwd+bwd+clip+SGD) of the reference's "
                       f"per-node nn.LSTM CPU path at N={d.num_nodes}, {t_step:.3f} s each; meta-steps/s = "
                       f"1/({sample_steps} sample-steps x t); first-order work only (the reference has no "

@@ -206,6 +206,14 @@ int smaml_head_loss(smaml_ctx* ctx, void* stream, const float* theta, const floa
 int smaml_clip_sgd(smaml_ctx* ctx, void* stream, float* theta, const float* grad, int32_t ntasks, float lr,
                    float max_norm, float* norms);
 
+/* Synchronise `stream` and report device-side failures of this context's kernels: SMAML_EHIP if a
+ * grid-barrier bookkeeping kernel (the fused clip + SGD step above, the second-order sweep update)
+ * timed out waiting for a grid that was not co-resident (its results are then invalid; the barrier
+ * state is reset). Every compute entry point also checks the flag on entry, without syncing.
+ * Replaces the implicit error surfacing of torch's synchronous CPU ops at
+ * train_hybrid_maml_v5.py:135-139 (`loss.item()` after the inner step). */
+int smaml_sync(smaml_ctx* ctx, void* stream);
+
 /* inner_loop_v4 (train_hybrid_maml_v5.py:110-141) for every task of smaml_set_tasks:
  * `steps` support steps of `batch` windows (windows_host [steps+1][ntasks][batch], the last
  * row is the query batch, evaluated but not trained on) -> fast_out [ntasks][P]; losses /
@@ -262,7 +270,15 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "wgrad_wide":                  weight gradients whose column count is a multiple of 256 on
  *                                  256 x 256 tiles (1, the default) or 512 x 128 tiles (0);
  *   "wgrad_pair":                  the two passes of a tangent weight gradient (LSTM layers >= 1)
- *                                  as one split-K launch (1, the default) or two (0). */
+ *                                  as one split-K launch (1, the default) or two (0);
+ *   "grid_barrier":                the clip + SGD step and the sweep update as one grid-barrier
+ *                                  launch each (1, the default) or two launches each (0; bitwise
+ *                                  equal);
+ *   "barrier_timeout_us":          bound on a grid-barrier wait (default 4 s); on expiry the kernel
+ *                                  exits and the next call / smaml_sync returns SMAML_EHIP;
+ *   "barrier_oversize":            debug: > 0 launches the grid-barrier kernels with that many
+ *                                  times the resident capacity (+1 block), which can never be
+ *                                  co-resident, to exercise the bounded wait. */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -1,0 +1,53 @@
+"""Host-side caches of the module API: a reference-style training loop
+(train_hybrid_maml_v5.py:129-139) passes the same edge_index and unchanged weights every call, so the
+drop-in must not copy edge_index to the host (a sync) or re-pack the flat parameter vectors per call,
+and must notice every change (replaced tensors, in-place writes, optimizer steps)."""
+import torch
+
+from weatherforecast_stgcn_maml_amd.config import CONFIG2
+from weatherforecast_stgcn_maml_amd.hybrid_model import HybridSTGCN_LSTM
+from weatherforecast_stgcn_maml_amd.model import STGCN, _GraphMemo
+
+
+def test_graph_memo_identity_and_version():
+    m = _GraphMemo()
+    ei = torch.tensor([[0, 1], [1, 0]])
+    assert m.get(ei) is None
+    m.put(ei, 7)
+    assert m.get(ei) == 7
+    assert m.get(ei.clone()) is None        # another tensor with the same content: recomputed
+    ei[0, 0] = 1                            # in-place write bumps the version counter
+    assert m.get(ei) is None
+    m.put(ei, 8)
+    ei.view(-1)[3] = 0                      # a write through a view bumps the shared counter
+    assert m.get(ei) is None
+
+
+def _model():
+    d = CONFIG2
+    base = STGCN(d.input_channels, d.hidden_channels, d.output_channels, d.window_size, d.forecast_horizon, 0.0)
+    return HybridSTGCN_LSTM(base, d.lstm_hidden_size, d.lstm_num_layers, 0.0, d.output_channels,
+                            d.forecast_horizon), d
+
+
+def test_packed_parameters_cached_until_changed():
+    m, d = _model()
+    dev = torch.device("cpu")
+    th1, fresh1 = m._packed(0, m._trainable_params(), d, dev)
+    th2, fresh2 = m._packed(0, m._trainable_params(), d, dev)
+    assert fresh1 and not fresh2 and th2 is th1
+    w = m.lstm.weight_ih_l0
+    opt = torch.optim.SGD(m.get_trainable_parameters(), lr=0.1)
+    w.grad = torch.ones_like(w)
+    opt.step()                              # optimizer update in place: re-packed into the same buffer
+    th3, fresh3 = m._packed(0, m._trainable_params(), d, dev)
+    assert fresh3 and th3 is th1
+    assert torch.equal(th3[:w.numel()].view_as(w), w.detach())
+    m.load_state_dict(m.state_dict())       # load_state_dict copies in place: noticed
+    assert m._packed(0, m._trainable_params(), d, dev)[1]
+    m.output_layer.weight = torch.nn.Parameter(torch.zeros_like(m.output_layer.weight))  # replaced tensor
+    th4, fresh4 = m._packed(0, m._trainable_params(), d, dev)
+    assert fresh4
+    g1, f1 = m._packed(1, m._gcn_params(), d, dev)
+    g2, f2 = m._packed(1, m._gcn_params(), d, dev)
+    assert f1 and not f2 and g1 is g2

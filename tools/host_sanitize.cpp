@@ -53,7 +53,7 @@ static std::vector<int64_t> grid_edges(int side) {
 }
 
 int main() {
-  CHECK(smaml_abi_version() == 4);
+  CHECK(smaml_abi_version() == 5);
   CHECK(smaml_build_info() != nullptr && std::strlen(smaml_build_info()) > 0);
 
   // ---- parameter layout (hybrid_model.py state_dict order) ----
@@ -161,6 +161,8 @@ int main() {
   CHECK(smaml_set_task_ids(nullptr, ids, 2) == SMAML_EINVAL);
   CHECK(smaml_set_dropout(nullptr, 0.1f, 0.1f, 1) == SMAML_EINVAL);
   CHECK(smaml_set_option(nullptr, "keep", 1) == SMAML_EINVAL);
+  CHECK(smaml_sync(nullptr, nullptr) == SMAML_EINVAL);
+  CHECK(smaml_set_option(nullptr, "barrier_timeout_us", 1000) == SMAML_EINVAL);
   CHECK(smaml_meta_step(nullptr, nullptr, nullptr, 2, 1, 1, nullptr, 0.01f, 1.f, 0.5f, nullptr, nullptr, nullptr,
                         nullptr) == SMAML_EINVAL);
   CHECK(smaml_reserve(nullptr, 1, 1) == SMAML_EINVAL);

@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 run (kernel stats + FETCH_SIZE/WRITE_SIZE PMC passes) into markdown,
 and optionally write the per-launch HBM traffic of each bench timing category as JSON
-(``bench.py`` reads it into ``roofline.traffic`` when the workload matches).
+(``bench.py`` reads it into ``roofline.traffic`` when the per-rank workload matches: the file holds one
+entry per profiled rank workload, e.g. 15 tasks for N=1 and the 8/4/2-task rank shares for N=2/4/8).
 
 FETCH_SIZE on gfx950 reports half the bytes of wide coalesced streaming reads
 (MI355X_MICROARCH.md §HBM, 16 B/lane loads as all our operand loads are): the corrected
@@ -111,9 +112,18 @@ def main(d, title, traffic_out=None, profile_md=None):
         traffic[cat] = {"read_bytes": rd * per, "write_bytes": wt * per, "bytes_per_launch": (rd + wt) * per}
         print(f"| {cat} | {len(fr)} | {rd * per / 1e6:.1f} | {wt * per / 1e6:.1f} | {(rd + wt) * per / 1e6:.1f} |")
     if traffic_out:
+        # merge into {"profiles": {rank workload key (bench.py rank_workload): {...}}}
         b = bench_line(d)
-        json.dump({"workload": b["config"]["workload"] if b else None, "profile": profile_md, "unit": "bytes",
-                   "categories": traffic}, open(traffic_out, "w"), indent=1)
+        key = (b.get("rank_workload") or b["config"]["workload"]) if b else None
+        doc = {"unit": "bytes", "profiles": {}}
+        if os.path.exists(traffic_out):
+            try:
+                old = json.load(open(traffic_out))
+                doc["profiles"] = old.get("profiles", {})
+            except ValueError:
+                pass
+        doc["profiles"][key] = {"profile": profile_md, "categories": traffic}
+        json.dump(doc, open(traffic_out, "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -23,9 +23,9 @@ EXPORTS = (
     "smaml_backward", "smaml_gcn_forward", "smaml_lstm_forward", "smaml_lstm_backward", "smaml_head_loss",
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
     "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy", "smaml_variant_counts", "smaml_set_option",
-    "smaml_dropout",
+    "smaml_dropout", "smaml_sync",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
 VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kept", "fwd_dual_img", "bwd_big", "bwd_small", "bwd_split",
@@ -107,6 +107,7 @@ _SIGS = {
     "smaml_variant_counts": ([P, PI64, I32, PI32, I32], I32),
     "smaml_set_option": ([P, ctypes.c_char_p, I64], I32),
     "smaml_dropout": ([P, P, P, I64, F32, ctypes.c_uint32, I32], I32),
+    "smaml_sync": ([P, P], I32),
 }
 
 
@@ -293,6 +294,10 @@ class Context:
     def clip_sgd(self, stream, theta, grad, ntasks, lr, max_norm, norms=None):
         check(self._L.smaml_clip_sgd(self._h, stream, ptr(theta), ptr(grad), int(ntasks), float(lr),
                                      float(max_norm), ptr(norms) if norms is not None else None))
+
+    def sync(self, stream):
+        """Synchronise the stream; raises SmamlError if a grid-barrier kernel timed out."""
+        check(self._L.smaml_sync(self._h, stream))
 
     def inner_loop(self, stream, theta, steps, batch, windows: np.ndarray, inner_lr, max_norm, fast_out,
                    losses=None, norms=None):

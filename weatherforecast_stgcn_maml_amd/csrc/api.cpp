@@ -241,8 +241,15 @@ struct smaml_ctx {
   char* gcn_wimg = nullptr;   // pre-split GCN weight images of the fused t >= 1 GCN (kernels_gcn.hip)
   char* gimg_buf = nullptr;   // pre-split gate-GEMM weight images (prep_gate_images)
   int64_t gimg_cap = 0;
-  unsigned* bar = nullptr;    // grid-barrier arrival counter of the cooperative bookkeeping kernels
-  unsigned bar_count = 0;     // arrivals so far (host mirror: launches are stream-ordered)
+  // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
+  // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
+  unsigned* bar = nullptr;
+  int* bar_err_host = nullptr;
+  int* bar_err_dev = nullptr;
+  int64_t bar_timeout_us = 4000000;  // smaml_set_option("barrier_timeout_us")
+  int bar_fused = 1;                 // smaml_set_option("grid_barrier"): 0 = two launches per kernel
+  int bar_oversize = 0;              // smaml_set_option("barrier_oversize"): debug, never co-resident
+  uint64_t wall_khz = 0;             // wall_clock64 rate
   float* ad_F = nullptr;
   int64_t ad_cap = 0;              // windows the cache holds
   std::vector<uint8_t> ad_valid;   // per window start
@@ -575,14 +582,14 @@ void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t
 
 // Tangent weight gradient of one LSTM layer as ONE split-K launch + ONE reduce:
 //   R(dW) = R(dG)^T [x | h_{t-1}] + dG^T [Rx | Rh_{t-1}]   (both problems 4H x (cin + H)).
-void timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, const float* dG, int64_t a_zstride,
+bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, const float* dG, int64_t a_zstride,
                       int Mrows, const float* X, const float* RX, int64_t b1_zstride, int c1, const float* Hh,
                       const float* RHh, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                       int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, int drop_layer) {
   WgradPlan p;
   plan_wgrad(c->w, RdG, a_zstride, Mrows, X, b1_zstride, c1, Hh, b2_zstride, c2, K, Mshift, grad, P, off_w1, off_w2,
              off_b1, off_b2, true, false, p);
-  pair_wgrad(p, dG, RX, RHh);
+  if (!pair_wgrad(p, c->w, dG, RX, RHh)) return false;  // the caller runs the two accumulating passes
   p.drop = c->w.drop;
   p.drop_layer = drop_layer;
   count_variant(c->w, V_WGRAD);
@@ -590,6 +597,7 @@ void timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
   count_variant(c->w, V_WGRAD_PAIR);
   TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+  return true;
 }
 
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
@@ -803,12 +811,11 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
     const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
-    if (l > 0 && c->kn.wgrad_pair) {  // both passes 4H x (cin + H): one launch
-      timed_wgrad_pair(c, s, 2.0 * 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, dGl, TM * 4 * d.H, 4 * d.H, X, RX,
-                       TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M,
-                       HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, l - 1);
+    if (l > 0 && c->kn.wgrad_pair &&  // both passes 4H x (cin + H): one launch
+        timed_wgrad_pair(c, s, 2.0 * 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, dGl, TM * 4 * d.H, 4 * d.H, X,
+                         RX, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, w.RHs + (int64_t)l * lsz, TM * d.H, d.H,
+                         TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, l - 1))
       continue;
-    }
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
                        TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false, l - 1);
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
@@ -828,14 +835,43 @@ int require_ready(smaml_ctx* c) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// the cooperative bookkeeping kernels' barrier counter (zeroed once; only ever counts up)
+// the bookkeeping kernels' grid-barrier state (zeroed once; self-resetting, see kernels.h GridBar)
 int ensure_bar(smaml_ctx* c) {
   if (c->bar) return SMAML_OK;
-  HIP_TRY(hipMalloc((void**)&c->bar, sizeof(unsigned)));
-  HIP_TRY(hipMemset(c->bar, 0, sizeof(unsigned)));
+  int khz = 0;
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+  c->wall_khz = khz > 0 ? (uint64_t)khz : 100000;
+  HIP_TRY(hipHostMalloc((void**)&c->bar_err_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *(volatile int*)c->bar_err_host = 0;
+  HIP_TRY(hipHostGetDevicePointer((void**)&c->bar_err_dev, c->bar_err_host, 0));
+  HIP_TRY(hipMalloc((void**)&c->bar, 4 * sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->bar, 0, 4 * sizeof(unsigned)));
   HIP_TRY(hipDeviceSynchronize());
-  c->bar_count = 0;
   return SMAML_OK;
+}
+
+BarPlan bar_plan(const smaml_ctx* c) {
+  BarPlan bp{};
+  bp.gb.w = c->bar;
+  bp.gb.host_err = c->bar_err_dev;
+  bp.gb.timeout = (uint64_t)c->bar_timeout_us * c->wall_khz / 1000;
+  bp.fused = c->bar_fused;
+  bp.oversize = c->bar_oversize;
+  return bp;
+}
+
+// A grid-barrier wait that timed out (kernels.h grid_barrier) raised the pinned flag: drain the device,
+// reset the barrier state and report it. No host sync unless the flag is up.
+int check_device_error(smaml_ctx* c) {
+  if (!c->bar_err_host || *(volatile int*)c->bar_err_host == 0) return SMAML_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemset(c->bar, 0, 4 * sizeof(unsigned)));
+  HIP_TRY(hipDeviceSynchronize());
+  *(volatile int*)c->bar_err_host = 0;
+  return fail(SMAML_EHIP,
+              "a grid-barrier kernel (k_inner_sgd / k_sweep_update) timed out waiting for its grid: the grid was "
+              "not co-resident (another process holding the GPU, or the barrier_oversize debug knob); its "
+              "results are invalid");
 }
 
 }  // namespace
@@ -845,7 +881,7 @@ extern "C" {
 
 const char* smaml_last_error(void) { return g_err.c_str(); }
 
-int32_t smaml_abi_version(void) { return 4; }
+int32_t smaml_abi_version(void) { return 5; }
 
 const char* smaml_build_info(void) { return smaml::products_info(); }
 
@@ -950,6 +986,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->gcn_wimg) (void)hipFree(c->gcn_wimg);
   if (c->gimg_buf) (void)hipFree(c->gimg_buf);
   if (c->bar) (void)hipFree(c->bar);
+  if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
   for (auto& r : c->tm.recs) {
@@ -1087,6 +1124,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const int Z = (int)c->feats.size();
   const int B = batch;
   TRY(ensure_bar(c));
+  TRY(check_device_error(c));
   TRY(reserve(c, Z, B, order == 2));
   if (order == 2) TRY(ensure_so_store(c, std::max(steps, 1), Z, B));
   if (order == 2) TRY(ensure_keep(c, steps, Z, B));
@@ -1141,13 +1179,13 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       HIP_TRY(hipMemcpyAsync(c->so_grad + (int64_t)k * Z * P, c->grad, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
       TIMED(c, s, C_MISC, 0,
             HIP_TRY(launch_inner_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
-                                     c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z, c->bar, c->bar_count)));
+                                     c->so_norm + (int64_t)k * Z, c->so_coef + (int64_t)k * Z, bar_plan(c))));
       if (norms)
         HIP_TRY(hipMemcpyAsync(norms + (int64_t)k * Z, c->so_norm + (int64_t)k * Z, Z * 4, hipMemcpyDeviceToDevice, s));
     } else {
       TIMED(c, s, C_MISC, 0,
             HIP_TRY(launch_inner_sgd(s, c->fast, c->grad, P, Z, c->w.sqpart, inner_lr, max_norm,
-                                     norms ? norms + (int64_t)k * Z : nullptr, nullptr, c->bar, c->bar_count)));
+                                     norms ? norms + (int64_t)k * Z : nullptr, nullptr, bar_plan(c))));
     }
   }
   const float* const* xq = c->xtab + (int64_t)steps * Z * B;
@@ -1174,8 +1212,8 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       TIMED(c, s, C_MISC, 0,
             HIP_TRY(launch_sweep_update(s, V, nullptr, 0.f, c->so_grad + (int64_t)(steps - 1) * Z * P, P, Z,
                                         c->w.sqpart, c->so_norm + (int64_t)(steps - 1) * Z,
-                                        c->so_coef + (int64_t)(steps - 1) * Z, max_norm, c->so_u, c->bar,
-                                        c->bar_count)));
+                                        c->so_coef + (int64_t)(steps - 1) * Z, max_norm, c->so_u,
+                                        bar_plan(c))));
     for (int k = steps - 1; k >= 0; --k) {
       const float* th = c->so_theta + (int64_t)k * Z * P;
       const float* const* xt = c->xtab + (int64_t)k * Z * B;
@@ -1191,8 +1229,8 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
         TIMED(c, s, C_MISC, 0,
               HIP_TRY(launch_sweep_update(s, V, c->so_hu, -inner_lr, c->so_grad + (int64_t)(k - 1) * Z * P, P, Z,
                                           c->w.sqpart, c->so_norm + (int64_t)(k - 1) * Z,
-                                          c->so_coef + (int64_t)(k - 1) * Z, max_norm, c->so_u, c->bar,
-                                          c->bar_count)));
+                                          c->so_coef + (int64_t)(k - 1) * Z, max_norm, c->so_u,
+                                          bar_plan(c))));
       else
         TIMED(c, s, C_MISC, 0, launch_axpy(s, V, c->so_hu, (int64_t)Z * P, -inner_lr));
       c->w.primal_kept = 0;
@@ -1336,6 +1374,12 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_pair = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
+  } else if (k == "grid_barrier" && (value == 0 || value == 1)) {
+    c->bar_fused = (int)value;
+  } else if (k == "barrier_timeout_us" && value >= 1) {
+    c->bar_timeout_us = std::min<int64_t>(value, 600000000);
+  } else if (k == "barrier_oversize" && value >= 0 && value <= 64) {
+    c->bar_oversize = (int)value;
   } else if (k == "keep" && value >= -1) {
     c->keep_max = (int)std::min<int64_t>(value, 1 << 20);
     c->keep_tried_K = -1;  // re-plan the kept slots on the next second-order meta-step
@@ -1350,6 +1394,7 @@ int smaml_adamw_step(smaml_ctx* c, void* stream, float* theta, const float* grad
                      float* norm_out) {
   if (!c || !theta || !grad || !m || !v || n <= 0 || step < 1) return fail(SMAML_EINVAL, "bad adamw arguments");
   TRY(ensure_device(c));
+  TRY(check_device_error(c));
   TRY(reserve(c, 1, 1));
   hipStream_t s = (hipStream_t)stream;
   const double bc1 = 1.0 - std::pow((double)beta1, step);
@@ -1479,10 +1524,17 @@ int smaml_clip_sgd(smaml_ctx* c, void* stream, float* theta, const float* grad, 
   if (ntasks > c->z_cap) TRY(reserve(c, ntasks, 1));
   TRY(ensure_bar(c));
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(launch_inner_sgd(s, theta, grad, c->po.P, ntasks, c->w.sqpart, lr, max_norm, norms, nullptr, c->bar,
-                           c->bar_count));
+  TRY(check_device_error(c));
+  HIP_TRY(launch_inner_sgd(s, theta, grad, c->po.P, ntasks, c->w.sqpart, lr, max_norm, norms, nullptr, bar_plan(c)));
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
+}
+
+int smaml_sync(smaml_ctx* c, void* stream) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  TRY(ensure_device(c));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return check_device_error(c);
 }
 
 int smaml_inner_loop(smaml_ctx* c, void* stream, const float* theta, int32_t steps, int32_t batch,

@@ -82,11 +82,11 @@ enum Variant {
   V_FWDD,            // k_lstm_fwd_dual, primal recomputed
   V_FWDD_KEPT,       // k_lstm_fwd_dual, tangent only (primal kept)
   V_FWDD_IMG,        // k_lstm_fwd_dual with pre-split weight images (also counted as one of the above)
-  V_BWD_BIG,         // k_lstm_bwd_step, 64x128 tiles
+  V_BWD_BIG,         // k_lstm_bwd_step, big tiles (CfgBwd: SMAML_BWD_BM x 128, 128 x 128 in this build)
   V_BWD_SMALL,       // k_lstm_bwd_step, 64x64 tiles
   V_BWD_SPLIT,       // k_lstm_bwd_part + k_lstm_bwd_cell (small grids)
-  V_BWDD_BIG,        // k_lstm_bwd_dual, 64x128 tiles, primal recomputed
-  V_BWDD_BIG_KEPT,   // k_lstm_bwd_dual, 64x128 tiles, tangent only
+  V_BWDD_BIG,        // k_lstm_bwd_dual, big tiles (CfgBwdD, 128 x 128), primal recomputed
+  V_BWDD_BIG_KEPT,   // k_lstm_bwd_dual, big tiles (CfgBwdD, 128 x 128), tangent only
   V_BWDD_SMALL,      // k_lstm_bwd_dual, 64x64 tiles, primal recomputed
   V_BWDD_SMALL_KEPT, // k_lstm_bwd_dual, 64x64 tiles, tangent only
   V_WGRAD,           // k_wgrad launches (any tile)
@@ -97,7 +97,7 @@ enum Variant {
 
 // Build-time defaults of the run-time knobs below.
 #ifndef SMAML_BWD_BIG_MIN
-#define SMAML_BWD_BIG_MIN (3 * 256)  // BPTT launches with >= this many 64-row x 128 tiles' worth of rows use the big tiles
+#define SMAML_BWD_BIG_MIN (3 * 256)  // BPTT launches with >= this many 64-row x 128-unit tile units use the big tiles
 #endif
 #ifndef SMAML_BWDD_BIG_MIN
 #define SMAML_BWDD_BIG_MIN (3 * 256)
@@ -108,7 +108,8 @@ enum Variant {
 
 // Run-time tile-selection knobs (smaml_set_option; defaults = the build-time thresholds).
 struct Knobs {
-  int bwd_big_min;   // BPTT launches with >= this many 64x128 tiles use them (else 64x64 / split-K)
+  int bwd_big_min;   // BPTT launches with >= this many 64-row x 128-unit tile units (a 128 x 128 big tile counts
+                     // 2) use the big tiles (else 64x64 / split-K)
   int bwdd_big_min;  // same, tangent BPTT
   int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
   int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
@@ -184,21 +185,79 @@ inline void count_variant(const Work& w, Variant v) {
 
 constexpr int SQB = 64;  // blocks per task for squared-norm partials
 
-// Grid-wide barrier of a cooperative launch (every block co-resident): `bar` counts block arrivals
-// since the context was made (never reset); the launch passes the count its last arrival reaches.
+// Grid-wide barrier of the bookkeeping kernels (k_inner_sgd, k_sweep_update). A plain launch gives NO
+// co-residency guarantee, so the barrier relies on the launcher's grid sizing (grid_barrier_blocks: a
+// quarter of the device's resident capacity for the kernel, so up to four such grids from processes
+// sharing the GPU fit at once; blocks of ordinary kernels never wait on ours and free their slots) and
+// bounds every spin: a waiter that has not seen the barrier open within `timeout` wall-clock ticks, or
+// that sees another waiter's timeout, marks the error word, reports it through the pinned host flag
+// and returns false; the kernel then skips its second phase and exits, so a stranded grid drains and
+// the host turns the flag into SMAML_EHIP (api.cpp check_device_error) instead of hanging.
+// State w[0] = arrivals at the open barrier, w[1] = generation, w[2] = error; the last arrival resets
+// w[0] and bumps w[1], so nothing is mirrored on the host and a failed launch leaves no stale count.
+// One barrier state per context, used by that context's stream only (launches are stream-ordered).
 // Release: the block's stores are made visible before it arrives; acquire: the waiting lane's
 // agent-scope load invalidates this CU's L1, so the block then reads the other blocks' results.
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target) {
+struct GridBar {
+  unsigned* w;        // device words [3]
+  int* host_err;      // pinned, device-mapped flag (may be null)
+  uint64_t timeout;   // wall_clock64 ticks a waiter spins before giving up
+};
+__device__ __forceinline__ bool grid_barrier(const GridBar& gb, unsigned nb) {
+  __shared__ int ok_s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    while ((int)(__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
-      __builtin_amdgcn_s_sleep(2);
+    int ok = 1;
+    unsigned* cnt = gb.w;
+    unsigned* gen = gb.w + 1;
+    unsigned* err = gb.w + 2;
+    const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == nb - 1) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+            wall_clock64() - t0 > gb.timeout) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (gb.host_err) __hip_atomic_store(gb.host_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    ok_s = ok;
   }
   __syncthreads();
+  return ok_s != 0;
 }
-int coop_blocks(int items);  // blocks of a cooperative bookkeeping launch over `items` (task, chunk) items
-hipError_t launch_coop(const void* fn, int nb, void** args, hipStream_t s);  // NT threads per block
+// Launch plan of a bookkeeping kernel over `items` (task, chunk) items: `fused` = one launch with the
+// grid barrier (nb blocks, each looping over items), else the two phases as two launches of the same
+// kernel (same partition and summation order: bitwise-equal results).
+struct BarPlan {
+  GridBar gb;
+  int fused;     // 1: grid-barrier launch
+  int oversize;  // debug: > 0 launches oversize x the resident capacity + 1 blocks (never co-resident)
+};
+// Grid of a grid-barrier launch over `items` items given the kernel's resident capacity `cap` (blocks
+// the device holds at once): min(items, cap / 4) -- a quarter, so up to four processes sharing the GPU
+// each fit one such grid beside the others (ordinary kernels drain and free their slots); the kernels
+// loop over their items, so any grid size is correct. 0 = capacity unknown (the caller runs the
+// two-launch form). `oversize` > 0 (debug knob) returns cap * oversize + 1 blocks, a grid that can
+// never be co-resident, to exercise the bounded wait.
+inline int grid_barrier_grid(int cap, int items, int oversize) {
+  if (cap <= 0 || items <= 0) return 0;
+  if (oversize > 0) return cap * oversize + 1;
+  const int q = cap / 4 > 0 ? cap / 4 : 1;
+  return items < q ? items : q;
+}
+// grid_barrier_grid with the capacity of `fn` on the current device
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs at NT threads)
+int grid_barrier_blocks(const void* fn, int items, int oversize);
+int grid_barrier_capacity(const void* fn);  // resident blocks of fn on the current device (0: unknown)
 #ifndef SMAML_WGRAD_MAXSPLIT
 #define SMAML_WGRAD_MAXSPLIT 128  // split-K slices per weight gradient (partial-slab capacity)
 #endif
@@ -271,7 +330,7 @@ struct GcnMlpArgs {
   float* F;                  // [Z][T][B*N][Hc]
   int64_t R1, M;             // rows t >= 1 over all samples; B*N
   FastDiv rows_div, b_div, n_div;
-  int rows1, N, T, B, cin0, ks1;
+  int rows1, N, T, B, cin0;
   Drop dr;
 };
 bool gcn_mlp_supported(const Dims& d);
@@ -338,8 +397,9 @@ struct WgradPlan {
   int nsplit1 = 0;
 };
 // Turn a planned weight gradient into a pair with a second problem of the same shape (each problem
-// gets about half of the planned slices; one launch, one reduce, no accumulate pass).
-void pair_wgrad(WgradPlan& p, const float* A2, const float* B1s, const float* B2s);
+// gets about half of the planned slices; one launch, one reduce, no accumulate pass). Returns false
+// (plan unchanged) when the pair's slices would not fit the partial-slab buffer w.wpart.
+bool pair_wgrad(WgradPlan& p, const Work& w, const float* A2, const float* B1s, const float* B2s);
 void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, const float* B1, int64_t b1_zstride,
                 int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                 int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias, bool accumulate,
@@ -354,15 +414,15 @@ struct WgMulti {
 void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs);
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
-// clip_grad_norm_ + SGD of every task as one cooperative kernel (k_inner_sgd); bar_count: the
-// context's running barrier-arrival count (advanced here)
+// clip_grad_norm_ + SGD of every task as one grid-barrier kernel (k_inner_sgd), or its two phases as
+// two launches (BarPlan)
 hipError_t launch_inner_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, double* part, float lr,
-                            float max_norm, float* norm_out, float* coef_out, unsigned* bar, unsigned& bar_count);
-// second-order sweep bookkeeping as one cooperative kernel (k_sweep_update): v += alpha x (x may be
+                            float max_norm, float* norm_out, float* coef_out, const BarPlan& bp);
+// second-order sweep bookkeeping as one grid-barrier kernel (k_sweep_update): v += alpha x (x may be
 // null), U = clip-adjusted direction of (G, norms, coefs) at v
 hipError_t launch_sweep_update(hipStream_t s, float* V, const float* X, float alpha, const float* G, int64_t P, int Z,
                                double* part, const float* norms, const float* coefs, float max_norm, float* U,
-                               unsigned* bar, unsigned& bar_count);
+                               const BarPlan& bp);
 void launch_sum_tasks(hipStream_t s, const float* g, int64_t P, int Z, float* out);
 void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float* out);
 void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,

@@ -8,7 +8,7 @@
 //                      hybrid_model.py:105-115, train_hybrid_maml_v5.py:119,133
 //   k_lstm_bwd_step    BPTT of the cell (loss.backward through LSTM)   train_hybrid_maml_v5.py:134
 //   k_wgrad            dW_ih | dW_hh | db  as a split-K GEMM over B*N*T rows
-//   k_clip_sgd         clip_grad_norm_(1.0) + SGD(lr)   train_hybrid_maml_v5.py:135-139
+//   k_inner_sgd        clip_grad_norm_(1.0) + SGD(lr)   train_hybrid_maml_v5.py:135-139
 //   k_adamw            clip + AdamW (outer)             train_hybrid_maml_v5.py:174-179,245-249
 //
 // Every GEMM-shaped contraction takes f32 operands and accumulates in f32 through gemm_core.h:
@@ -16,6 +16,10 @@
 // into three bf16 pieces, six piece products per 16-k step; gemm_core.h mfma_x6), or with
 // -DSMAML_X6=0 on v_mfma_f32_32x32x2_f32. All reductions are in a fixed order (no float
 // atomics), so results are bitwise reproducible run to run and across ranks.
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "kernels.h"
 #include "loaders.h"
 
@@ -1904,15 +1908,21 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   p.wide = wide;
 }
 
-void pair_wgrad(WgradPlan& p, const float* A2, const float* B1s, const float* B2s) {
+bool pair_wgrad(WgradPlan& p, const Work& w, const float* A2, const float* B1s, const float* B2s) {
   const int64_t ktiles = (p.K + CfgTN::BK - 1) / CfgTN::BK;
   const int64_t n1 = std::max<int64_t>(1, p.nsplit / 2);
-  p.kchunk = ((ktiles + n1 - 1) / n1) * CfgTN::BK;
-  p.nsplit1 = (int)((p.K + p.kchunk - 1) / p.kchunk);
-  p.nsplit = 2 * p.nsplit1;  // <= the planned count: fits the partial-slab buffer
+  const int64_t kchunk = ((ktiles + n1 - 1) / n1) * CfgTN::BK;
+  const int64_t nsplit1 = (p.K + kchunk - 1) / kchunk;
+  // 2 * nsplit1 slices can exceed the planned count (a plan of one slice gives two); check them
+  // against the partial-slab buffer and leave the plan unpaired if they do not fit
+  if (2 * nsplit1 * p.Z * (int64_t)p.Mrows * p.ldp > w.wpart_floats) return false;
+  p.kchunk = kchunk;
+  p.nsplit1 = (int)nsplit1;
+  p.nsplit = 2 * p.nsplit1;
   p.A2 = A2;
   p.B1s = B1s;
   p.B2s = B2s;
+  return true;
 }
 
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
@@ -2032,28 +2042,31 @@ __device__ __forceinline__ float clip_coef_from(const double* part, float max_no
 // The inner SGD step as ONE kernel (train_hybrid_maml_v5.py:135-139: clip_grad_norm_ + SGD): every
 // block computes the fp64 squared-norm partials of its (task, chunk) items -- the partition and order
 // of k_sqsum -- then, after a grid barrier, each task's clip coefficient from its SQB partials in
-// order and the SGD update of the same chunks (still in L2). Bitwise equal to k_sqsum + k_clip_sgd.
-// Launched cooperatively (every block co-resident); `bar` counts arrivals since the context was
-// made and `target` is the count after this launch's.
+// order and the SGD update of the same chunks (still in L2). `phases`: 1 = partials only, 2 = update
+// only, 3 = both with the grid barrier between them (grid sized by grid_barrier_blocks; see
+// grid_barrier for the bounded wait). The two-launch form (1 then 2) is bitwise equal to the fused one.
 __global__ __launch_bounds__(NT) void k_inner_sgd(float* __restrict__ theta, const float* __restrict__ g, int64_t P,
                                                   int Z, double* __restrict__ part, float lr, float max_norm,
-                                                  float* norm_out, float* coef_out, unsigned* bar, unsigned target) {
+                                                  float* norm_out, float* coef_out, GridBar gb, int phases) {
   __shared__ double red[NT / 64];
   const int nit = SQB * Z;
   const int64_t per = (P + SQB - 1) / SQB;
-  for (int it = blockIdx.x; it < nit; it += gridDim.x) {
-    const int z = it / SQB, b = it - z * SQB;
-    const float* gz = g + (int64_t)z * P;
-    const int64_t beg = (int64_t)b * per, end = beg + per < P ? beg + per : P;
-    double acc = 0.0;
-    for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
-      const double v = gz[i];
-      acc += v * v;
+  if (phases & 1) {
+    for (int it = blockIdx.x; it < nit; it += gridDim.x) {
+      const int z = it / SQB, b = it - z * SQB;
+      const float* gz = g + (int64_t)z * P;
+      const int64_t beg = (int64_t)b * per, end = beg + per < P ? beg + per : P;
+      double acc = 0.0;
+      for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
+        const double v = gz[i];
+        acc += v * v;
+      }
+      const double sum = block_sum_d(acc, red);
+      if (threadIdx.x == 0) part[it] = sum;
     }
-    const double sum = block_sum_d(acc, red);
-    if (threadIdx.x == 0) part[it] = sum;
   }
-  grid_barrier(bar, target);
+  if (phases == 3 && !grid_barrier(gb, gridDim.x)) return;
+  if (!(phases & 2)) return;
   for (int it = blockIdx.x; it < nit; it += gridDim.x) {
     const int z = it / SQB, b = it - z * SQB;
     float total;
@@ -2069,31 +2082,38 @@ __global__ __launch_bounds__(NT) void k_inner_sgd(float* __restrict__ theta, con
   }
 }
 
-int coop_blocks(int items) { return items < 1024 ? items : 1024; }
+// (queried once per (kernel, device) and cached)
+int grid_barrier_capacity(const void* fn) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, int>, int>> cache;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& e : cache)
+    if (e.first.first == fn && e.first.second == dev) return e.second;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, 0) != hipSuccess) return 0;
+  const int cap = per_cu > 0 && cus > 0 ? per_cu * cus : 0;
+  cache.push_back({{fn, dev}, cap});
+  return cap;
+}
 
-// The grid-barrier kernels (<= 1024 blocks of 256 threads, a few VGPRs, no LDS: 4 blocks per CU) are
-// launched with a plain launch of that grid: every block becomes resident once the CU slots free up
-// (a plain launch has the same residency as a cooperative one; MI355X_MICROARCH "coop-launch"), and
-// blocks of another kernel never wait on ours, so a partially resident grid only waits. Cooperative
-// launches (SMAML_COOP=1) measured pathological with two processes on one GPU (the self-launched
-// 2-rank bench over gloo: 22.3 s per meta-step against 1.9 s in round 2, the launch serialising
-// against the other process's queue), and rocprofv3 crashed in its exit handlers after them.
-hipError_t launch_coop(const void* fn, int nb, void** args, hipStream_t s) {
-  static const bool coop = [] {
-    const char* e = std::getenv("SMAML_COOP");
-    return e && e[0] == '1';
-  }();
-  if (coop) return hipLaunchCooperativeKernel(fn, dim3(nb), dim3(NT), args, 0, s);
-  return hipLaunchKernel(fn, dim3(nb), dim3(NT), args, 0, s);
+int grid_barrier_blocks(const void* fn, int items, int oversize) {
+  return grid_barrier_grid(grid_barrier_capacity(fn), items, oversize);
 }
 
 hipError_t launch_inner_sgd(hipStream_t s, float* theta, const float* g, int64_t P, int Z, double* part, float lr,
-                            float max_norm, float* norm_out, float* coef_out, unsigned* bar, unsigned& bar_count) {
-  const int nb = coop_blocks(SQB * Z);
-  bar_count += (unsigned)nb;
-  unsigned target = bar_count;
-  void* args[] = {&theta, &g, &P, &Z, &part, &lr, &max_norm, &norm_out, &coef_out, &bar, &target};
-  return launch_coop((const void*)k_inner_sgd, nb, args, s);
+                            float max_norm, float* norm_out, float* coef_out, const BarPlan& bp) {
+  const int items = SQB * Z;
+  const int nb = bp.fused ? grid_barrier_blocks((const void*)k_inner_sgd, items, bp.oversize) : 0;
+  if (nb > 0) {
+    k_inner_sgd<<<nb, NT, 0, s>>>(theta, g, P, Z, part, lr, max_norm, norm_out, coef_out, bp.gb, 3);
+  } else {
+    const int n2 = items < 1024 ? items : 1024;
+    k_inner_sgd<<<n2, NT, 0, s>>>(theta, g, P, Z, part, lr, max_norm, norm_out, coef_out, bp.gb, 1);
+    k_inner_sgd<<<n2, NT, 0, s>>>(theta, g, P, Z, part, lr, max_norm, norm_out, coef_out, bp.gb, 2);
+  }
+  return hipGetLastError();
 }
 
 __global__ void k_sum_tasks(const float* __restrict__ g, int64_t P, int Z, float* __restrict__ out) {

@@ -788,17 +788,17 @@ __global__ void k_axpy(float* __restrict__ V, const float* __restrict__ X, int64
 //   fixed chunks per task, summed in chunk order), grid barrier, then
 //   U = c v - [c < 1] max_norm dot / (n (n + 1e-6)^2) g
 // with (g, n, c) those of the inner step the sweep visits next (round 2 ran this as two launches,
-// k_axpy_dot + k_so_dir, with the same partition and order). Cooperative launch; see k_inner_sgd
-// for the barrier counter.
+// k_axpy_dot + k_so_dir, with the same partition and order). `phases` as k_inner_sgd: 3 = one launch
+// with the grid barrier, 1 then 2 = the two-launch form (bitwise equal).
 __global__ __launch_bounds__(NT) void k_sweep_update(float* __restrict__ V, const float* __restrict__ X, float alpha,
                                                      const float* __restrict__ G, int64_t P, int Z,
                                                      double* __restrict__ part, const float* __restrict__ norms,
                                                      const float* __restrict__ coefs, float max_norm,
-                                                     float* __restrict__ Uo, unsigned* bar, unsigned target) {
+                                                     float* __restrict__ Uo, GridBar gb, int phases) {
   __shared__ double red[NT / 64];
   const int nit = SQB * Z;
   const int64_t per = (P + SQB - 1) / SQB;
-  for (int it = blockIdx.x; it < nit; it += gridDim.x) {
+  for (int it = blockIdx.x; (phases & 1) && it < nit; it += gridDim.x) {
     const int z = it / SQB, b = it - z * SQB;
     float* vz = V + (int64_t)z * P;
     const float* gz = G + (int64_t)z * P;
@@ -825,7 +825,8 @@ __global__ __launch_bounds__(NT) void k_sweep_update(float* __restrict__ V, cons
       part[it] = sum;
     }
   }
-  grid_barrier(bar, target);
+  if (phases == 3 && !grid_barrier(gb, gridDim.x)) return;
+  if (!(phases & 2)) return;
   for (int it = blockIdx.x; it < nit; it += gridDim.x) {
     const int z = it / SQB, b = it - z * SQB;
     double dot = 0.0;
@@ -846,17 +847,18 @@ __global__ __launch_bounds__(NT) void k_sweep_update(float* __restrict__ V, cons
 
 hipError_t launch_sweep_update(hipStream_t s, float* V, const float* X, float alpha, const float* G, int64_t P, int Z,
                                double* part, const float* norms, const float* coefs, float max_norm, float* U,
-                               unsigned* bar, unsigned& bar_count) {
-  const int nb = coop_blocks(SQB * Z);
-  bar_count += (unsigned)nb;
-  unsigned target = bar_count;
-  void* args[] = {&V, &X, &alpha, &G, &P, &Z, &part, &norms, &coefs, &max_norm, &U, &bar, &target};
-  return launch_coop((const void*)k_sweep_update, nb, args, s);
+                               const BarPlan& bp) {
+  const int items = SQB * Z;
+  const int nb = bp.fused ? grid_barrier_blocks((const void*)k_sweep_update, items, bp.oversize) : 0;
+  if (nb > 0) {
+    k_sweep_update<<<nb, NT, 0, s>>>(V, X, alpha, G, P, Z, part, norms, coefs, max_norm, U, bp.gb, 3);
+  } else {
+    const int n2 = items < 1024 ? items : 1024;
+    k_sweep_update<<<n2, NT, 0, s>>>(V, X, alpha, G, P, Z, part, norms, coefs, max_norm, U, bp.gb, 1);
+    k_sweep_update<<<n2, NT, 0, s>>>(V, X, alpha, G, P, Z, part, norms, coefs, max_norm, U, bp.gb, 2);
+  }
+  return hipGetLastError();
 }
-
-
-
-
 
 void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha) {
   int nb = (int)((n + NT - 1) / NT);

@@ -32,6 +32,7 @@ __host__ __device__ __forceinline__ int kperm(int kappa) {
 constexpr int GM_WAVES = 4;                        // waves (= 32-row groups) per workgroup
 constexpr int GM_ROWS = 32 * GM_WAVES;             // data rows per workgroup
 constexpr int GM_NSTG = 4;                         // W-image ring stages
+constexpr int GM_KS1 = 2;                          // 16-k steps of layer 1 (Cin0 <= 32, zero-padded to 32)
 __host__ __device__ constexpr int gm_step_bytes(int HC) { return 3 * HC * 32; }  // one 16-k step, 3 planes
 
 // W image of one 16-k step: [plane][HC rows][16 k] bf16, 16-B chunks XOR-swizzled by row
@@ -40,10 +41,11 @@ __device__ __forceinline__ int gm_img_off(int row, int k) {
   return row * 32 + 16 * ((k >> 3) ^ ((row >> 3) & 1)) + 2 * (k & 7);
 }
 
-// Pre-split images of W1..W4, steps in layer order: layer 1 (natural K order, zero-padded to
-// 16 * ks1), layers 2..4 (K order kperm). One thread per (step, row, 4 k).
-__global__ void k_gcn_wsplit(const float* __restrict__ gcn, GcnWOff wo, int HC, int cin0, int ks1,
-                             char* __restrict__ img) {
+// Pre-split images of W1..W4, steps in layer order: layer 1 (natural K order, always GM_KS1 steps,
+// zero-padded past Cin0: k_gcn_mlp walks two layer-1 steps whatever Cin0 <= 32 is), layers 2..4 (K
+// order kperm). One thread per (step, row, 4 k).
+__global__ void k_gcn_wsplit(const float* __restrict__ gcn, GcnWOff wo, int HC, int cin0, char* __restrict__ img) {
+  constexpr int ks1 = GM_KS1;
   const int nsteps = ks1 + 3 * (HC / 16);
   const int64_t total = (int64_t)nsteps * HC * 4;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
   static_assert(SB % 1024 == 0 && CHUNKS % GM_WAVES == 0, "whole chunks per wave");
   constexpr int CPW = CHUNKS / GM_WAVES;
   constexpr int KS = HC / 16;  // steps of layers 2..4
-  constexpr int NSTEPS = 2 + 3 * KS;  // layer 1: Cin0 <= 32, two steps
+  constexpr int NSTEPS = GM_KS1 + 3 * KS;
   __shared__ __attribute__((aligned(16))) char ring[GM_NSTG * SB];
   __shared__ __attribute__((aligned(16))) float bias_s[4][HC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
     return make_float4(act[ci][u], act[ci][u + 1], act[ci][u + 2], act[ci][u + 3]);
   };
   for (int layer = 1; layer < 4; ++layer) {
-    const int j0 = 2 + (layer - 1) * KS;
+    const int j0 = GM_KS1 + (layer - 1) * KS;
     b = split3(lo4(0), hi4(0));
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) step(j0 + ks, b, lo4(ks + 1 < KS ? ks + 1 : ks), hi4(ks + 1 < KS ? ks + 1 : ks));
@@ -208,13 +210,12 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
 }
 
 void launch_gcn_wsplit(hipStream_t s, const Dims& d, const float* gcn, const GcnWOff& wo, char* img) {
-  const int ks1 = (d.Cin0 + 15) / 16;
-  const int64_t total = (int64_t)(ks1 + 3 * (d.Hc / 16)) * d.Hc * 4;
-  k_gcn_wsplit<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(gcn, wo, d.Hc, d.Cin0, ks1, img);
+  const int64_t total = (int64_t)(GM_KS1 + 3 * (d.Hc / 16)) * d.Hc * 4;
+  k_gcn_wsplit<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(gcn, wo, d.Hc, d.Cin0, img);
 }
 
 int64_t gcn_wimg_bytes(const Dims& d) {
-  return (int64_t)((d.Cin0 + 15) / 16 + 3 * (d.Hc / 16)) * gm_step_bytes(d.Hc);
+  return (int64_t)(GM_KS1 + 3 * (d.Hc / 16)) * gm_step_bytes(d.Hc);
 }
 
 bool gcn_mlp_supported(const Dims& d) { return d.Hc == 256 && d.Cin0 <= 32 && d.Cin0 % 4 == 0 && d.T > 1; }
@@ -237,7 +238,6 @@ void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* co
   a.B = B;
   a.M = (int64_t)B * d.N;
   a.cin0 = d.Cin0;
-  a.ks1 = (d.Cin0 + 15) / 16;
   if (drop && drop->gcn()) a.dr = *drop;
   const unsigned blocks = (unsigned)((a.R1 + GM_ROWS - 1) / GM_ROWS);
   k_gcn_mlp<256><<<blocks, 64 * GM_WAVES, 0, s>>>(a);

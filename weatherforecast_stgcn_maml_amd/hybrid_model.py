@@ -167,10 +167,37 @@ class HybridSTGCN_LSTM(nn.Module):
         dims = self.dims(x.shape[0] // T)
         ctx = _context(dims, x.device)
         _set_graph(ctx, edge_index)
-        gflat = params.pack(self.named_gcn(), dims, which=1, device=x.device)
-        ctx.set_gcn_params(gflat)
-        theta = params.pack(self.named_trainable(), dims, which=0, device=x.device)
+        gflat, fresh = self._packed(1, self._gcn_params(), dims, x.device)
+        if fresh or getattr(ctx, "_gcn", None) is not gflat:  # another model may share the context
+            ctx.set_gcn_params(gflat)
+        theta, _ = self._packed(0, self._trainable_params(), dims, x.device)
         return ctx, dims, theta
+
+    def _gcn_params(self):
+        b = self.base_stgcn
+        out = []
+        for k in range(1, 5):
+            conv = getattr(b, f"conv{k}")
+            out += [(f"base_stgcn.conv{k}.bias", conv.bias), (f"base_stgcn.conv{k}.lin.weight", conv.lin.weight)]
+        return out
+
+    def _packed(self, which, named, dims, device):
+        """The flat (padded) parameter vector of `named` on `device`, cached: re-packed (in place, into the
+        same buffer) only when a parameter object was replaced or written (its version counter moved,
+        e.g. by an optimizer step or load_state_dict), so repeated forwards with unchanged weights do
+        no allocation and no copy. Returns (flat, re-packed?)."""
+        cache = self.__dict__.setdefault("_pack_cache", {})
+        objs = [p for _, p in named]
+        vers = [p._version for p in objs]
+        ent = cache.get(which)
+        if (ent is not None and ent["device"] == device and len(ent["objs"]) == len(objs)
+                and all(a is b for a, b in zip(ent["objs"], objs)) and ent["vers"] == vers):
+            return ent["flat"], False
+        total = (params.trainable_layout(dims) if which == 0 else params.gcn_layout(dims))[1]
+        reuse = ent["flat"] if ent is not None and ent["device"] == device and ent["flat"].numel() == total else None
+        flat = params.pack({n: p.detach() for n, p in named}, dims, which=which, device=device, out=reuse)
+        cache[which] = {"device": device, "objs": objs, "vers": vers, "flat": flat}
+        return flat, True
 
     # ------------------------------------------------------------------ module API
     def extract_base_features(self, x, edge_index):

@@ -21,7 +21,7 @@ import torch
 
 from . import _capi, params, synth
 from .config import MamlConfig, ModelDims
-from .distributed import reduce_meta, shard_tasks  # noqa: F401  (shard_tasks re-exported)
+from .distributed import active, reduce_meta, shard_tasks  # noqa: F401  (shard_tasks re-exported)
 
 
 def reference_query_start(n_samples: int) -> int:
@@ -154,6 +154,9 @@ class MetaLearner:
         self.pg = process_group
         self.tasks: List[torch.Tensor] = []
         self._groups = []
+        # HIP events around the per-meta-step all-reduce (bench: the collective's exposed time)
+        self.comm_timing = False
+        self._comm_ev = []
 
     # tasks are [t_total, N, 24] float32 feature streams resident in HBM
     def set_tasks(self, features: Sequence, task_ids: Optional[Sequence[int]] = None):
@@ -232,7 +235,15 @@ class MetaLearner:
         if Z:
             self._qsum.copy_((losses[K].sum() * cfg.query_loss_scale).reshape(1))
         # one all_reduce of [meta_grad | query-loss sum] (just the scalar in reference mode)
-        reduce_meta(self._reduce if cfg.order >= 1 else self._qsum, self.pg)
+        if self.comm_timing and active():
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            reduce_meta(self._reduce if cfg.order >= 1 else self._qsum, self.pg)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._comm_ev.append((e0, e1))
+        else:
+            reduce_meta(self._reduce if cfg.order >= 1 else self._qsum, self.pg)
         if cfg.order >= 1:
             self.step += 1
             norm_out = torch.empty(1, device=self.device)
@@ -243,8 +254,19 @@ class MetaLearner:
             norm_out = None
         if not sync:
             return StepResult(losses, norms, float("nan"), None)
+        self.ctx.sync(stream)  # surfaces a timed-out grid-barrier kernel as SmamlError
         return StepResult(losses, norms, float(self._qsum.item()),
                           float(norm_out.item()) if norm_out is not None else None)
+
+    def comm_time_collect(self):
+        """(summed ms, count) of the timed all-reduces since the last call: from the end of this rank's
+        meta-step work on the stream to the reduced buffer being ready, i.e. the collective plus the
+        wait for the slowest rank (synchronises)."""
+        torch.cuda.synchronize(self.device)
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in self._comm_ev)
+        n = len(self._comm_ev)
+        self._comm_ev = []
+        return ms, n
 
     def theta_named(self):
         return {k: v.detach().clone() for k, v in params.unpack(self.theta, self.dims, 0).items()}
