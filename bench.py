@@ -95,17 +95,42 @@ def algorithmic_flops(d, tasks, K, B, order):
     return fo
 
 
+def progress(msg):
+    """Progress on stderr (the driver reads only the JSON line on stdout)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cgroup_cpus():
+    """CPUs the process's cgroup quota grants (cgroup v2 cpu.max or v1 cfs quota), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_threads():
-    """(threads used, os.cpu_count(), CPUs this process may run on). The reference runs torch's
-    CPU path with torch's default thread pool; the port is timed with one thread per CPU the
-    process may use (sched_getaffinity), which equals os.cpu_count() unless the host pins the
-    process to a subset (then os.cpu_count() threads would oversubscribe the CPUs it has)."""
+    """(threads used, os.cpu_count(), CPUs this process may run on). The port is timed with one
+    thread per CPU the process can actually use: os.cpu_count() capped by the affinity mask and the
+    cgroup CPU quota (on the GPU box os.cpu_count() reports the whole machine, 256, while the quota
+    grants 16: 256 threads on 16 CPUs oversubscribe and stall)."""
     n_os = os.cpu_count() or 1
     try:
         n_aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         n_aff = n_os
-    return max(1, min(n_os, n_aff)), n_os, n_aff
+    quota = cgroup_cpus()
+    usable = min(n_os, n_aff, quota or n_os)
+    return max(1, usable), n_os, min(n_aff, quota or n_aff)
 
 
 def cpu_baseline(d, n_steps, P, ei, feats):
@@ -129,6 +154,7 @@ def cpu_baseline(d, n_steps, P, ei, feats):
         for i in range(n_steps):
             xi, yi = synth.sample_xy(feats, i % 8)
             port.step(torch.from_numpy(np.ascontiguousarray(xi)), torch.from_numpy(np.ascontiguousarray(yi)))
+            progress(f"cpu baseline sample-step {i + 1}/{n_steps} ({threads} threads)")
         t = (time.perf_counter() - t0) / n_steps
         used = torch.get_num_threads()
     finally:
@@ -370,6 +396,7 @@ def main():
     ml.set_tasks(feats, task_ids=mine)
     torch.cuda.synchronize()
 
+    progress(f"rank {rank}: {len(mine)} tasks, warmup")
     for _ in range(args.warmup):
         ml.meta_step(sync=False)
     if not args.no_timing:
@@ -386,6 +413,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    progress(f"rank {rank}: timed region done")
     elapsed = time.perf_counter() - t0
     kern = None
     if not args.no_timing:
@@ -494,6 +522,7 @@ def main():
         ml.ctx.close()
         del ml
         torch.cuda.empty_cache()
+        progress("config 4 adaptation")
         ad, _ = adaptation_bench(ModelDims(num_nodes=441, hidden_channels=256), P, ei, epochs=args.adapt_epochs)
         out["adaptation"] = ad
     if world == 1 and args.cfg5_share_tasks > 0 and args.config == 2:
@@ -501,6 +530,7 @@ def main():
             ml.ctx.close()
             del ml
             torch.cuda.empty_cache()
+        progress("config 5 rank share")
         out["config5_rank_share"] = config5_share_bench(args.cfg5_share_tasks)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -8,9 +8,10 @@ result's error against float64 (the oracle run in f64 on the same inputs) next t
 the reference's own precision (the oracle in f32 on the CPU, MKL) and requires the GPU to be no
 less accurate than that, up to a small factor for summation-order noise.
 
-Workload: BASELINE config-2 shapes (N=441, Hc=256, LSTM 4x128), one task, B=2, K=5 inner steps
+Workloads: BASELINE config-2 shapes (N=441, Hc=256, LSTM 4x128), one task, B=2, K=5 inner steps
 (the bench's depth: the error of five chained Hessian-vector steps), second order, clip active and
-inactive: forward, BPTT, weight gradients, the tangent sweep.
+inactive; and config-5 shapes (N=1024, Hc=512) at K=10 (ten chained steps): forward, BPTT, weight
+gradients, the tangent sweep.
 
 Special values (``test_bf16x6_special_values``): the split differs from an f32 MFMA only outside
 the finite bf16 range. An inf operand gives NaN, not inf (x1 = x - x0 = inf - inf), and a finite
@@ -24,7 +25,7 @@ import torch
 
 from oracle import refcpu
 from weatherforecast_stgcn_maml_amd import params, synth
-from weatherforecast_stgcn_maml_amd.config import CONFIG2, MamlConfig
+from weatherforecast_stgcn_maml_amd.config import CONFIG2, CONFIG5, MamlConfig
 from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
 from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
@@ -40,18 +41,21 @@ def rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-@pytest.mark.parametrize("max_norm", [1.0, 0.02])
-def test_f32_accuracy_against_float64(max_norm):
-    d = CONFIG2
-    cfg = MamlConfig(inner_steps=5, batch=2, order=2, max_norm=max_norm)
-    P = synth.init_params(21, d, gcn_bias_scale=0.1)
+@pytest.mark.parametrize("d,K,B,max_norm,seed", [(CONFIG2, 5, 2, 1.0, 21), (CONFIG2, 5, 2, 0.02, 21),
+                                                  (CONFIG5, 10, 1, 1.0, 27)],
+                         ids=["cfg2-k5-clip1", "cfg2-k5-clip0.02", "cfg5-k10-clip1"])
+def test_f32_accuracy_against_float64(d, K, B, max_norm, seed):
+    """cfg5-k10: BASELINE config-5 shapes (N=1024, Hc=512, LSTM 4x128) at config 5's depth, ten chained
+    Hessian-vector steps (the oracle takes ~1 min in f32 and ~2 min in f64 on the host)."""
+    cfg = MamlConfig(inner_steps=K, batch=B, order=2, max_norm=max_norm)
+    P = synth.init_params(seed, d, gcn_bias_scale=0.1)
     names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
     theta = {k: P[k] for k in names}
     gcn = {k: v for k, v in P.items() if k not in names}
     side = int(round(d.num_nodes ** 0.5))
     lats, lons = synth.region_grid(n_lat=side, n_lon=side)
     ei = build_spatial_graph(lats, lons, 4)[0]
-    feats = synth.make_features(1300, d.num_nodes, stream_len_for(cfg, d))
+    feats = synth.make_features(1300 if d is CONFIG2 else 1300 + seed, d.num_nodes, stream_len_for(cfg, d))
     ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
     ml.set_tasks([feats])
     fast = torch.zeros(1, ml.theta.numel(), device=DEV)
@@ -81,7 +85,7 @@ def test_f32_accuracy_against_float64(max_norm):
     rows.append(("query_mse", abs(ql - r64["query_losses"][0]) / r64["query_losses"][0],
                  abs(r32["query_losses"][0] - r64["query_losses"][0]) / r64["query_losses"][0]))
     worst = max(rows, key=lambda r: r[1] / max(r[2], 1e-7))
-    print(f"\nmax_norm={max_norm}: worst GPU/CPU-f32 error ratio {worst[0]}: gpu {worst[1]:.3e} cpu {worst[2]:.3e}; "
+    print(f"\nN={d.num_nodes} K={K} max_norm={max_norm}: worst GPU/CPU-f32 error ratio {worst[0]}: gpu {worst[1]:.3e} cpu {worst[2]:.3e}; "
           f"mean gpu {np.mean([r[1] for r in rows]):.3e} cpu {np.mean([r[2] for r in rows]):.3e}")
     for name, e_gpu, e_cpu in rows:
         assert e_gpu <= FACTOR * e_cpu + 1e-7, (name, e_gpu, e_cpu)

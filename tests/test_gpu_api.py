@@ -416,14 +416,17 @@ def test_gate_images_bitwise():
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("knob", ["wgrad_wide", "wgrad_pair"])
+@pytest.mark.parametrize("knob", ["wgrad_wide", "wgrad_pair", "wgrad_ws"])
 def test_wgrad_variants_match(knob):
-    """wgrad_wide: weight gradients with 256-column problems (LSTM layers >= 1 and their tangent
-    passes) run on 256 x 256 tiles by default (kernels.hip CfgTW); the 512 x 128 tiles give the same
-    weight sums (same split-K slices, same per-element MFMA order) and the bias column sums up to
-    summation order. wgrad_pair: the tangent weight gradient's two passes (R(dG)^T [x|h] and
-    dG^T [Rx|Rh]) as one split-K launch instead of two accumulating ones (summation order only).
-    Both second-order meta-steps agree with each other well inside the oracle tolerance."""
+    """wgrad_ws: the warp-specialised weight gradients (k_wgrad_ws: 4 MFMA waves + 4 producer waves,
+    256 x 128 tiles), the default where the shapes allow, against the staged 256 x 256 / 512 x 128
+    tiles (different split-K slices: summation order only). wgrad_wide (with wgrad_ws off): weight
+    gradients with 256-column problems (LSTM layers >= 1 and their tangent passes) on 256 x 256 tiles
+    (kernels.hip CfgTW); the 512 x 128 tiles give the same weight sums (same split-K slices, same
+    per-element MFMA order) and the bias column sums up to summation order. wgrad_pair: the tangent
+    weight gradient's two passes (R(dG)^T [x|h] and dG^T [Rx|Rh]) as one split-K launch instead of two
+    accumulating ones (summation order only). Both second-order meta-steps agree with each other well
+    inside the oracle tolerance."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
@@ -436,6 +439,8 @@ def test_wgrad_variants_match(knob):
     for on in (1, 0):
         ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
         ml.set_tasks(feats)
+        if knob == "wgrad_wide":
+            ml.ctx.set_option("wgrad_ws", 0)
         ml.ctx.set_option(knob, on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()

@@ -167,3 +167,39 @@ def test_bench_configuration_properties_and_determinism():
     for a, b in zip(runs[0][:4], runs[1][:4]):
         assert torch.equal(a, b)
     assert runs[0][4] == runs[1][4]
+
+
+def test_config5_share_properties_and_determinism():
+    """Config 5's per-rank share at 8 GPUs (8 of the 64 stress tasks x B=32 x T=24 x N=1024, Hc=512,
+    LSTM 4x128, K=10, second order), seeded as bench.py's config5_share_bench: every loss / norm /
+    meta-gradient entry finite, the query MSE near the unit target variance, theta moves, and the
+    whole meta-step (losses, norms, meta-gradient, post-AdamW theta) bitwise reproducible."""
+    d = CONFIG5
+    cfg = MamlConfig(inner_steps=10, batch=32, order=2)
+    P = synth.init_params(SEED, d)
+    theta, gcn, _ = split(P)
+    ei = grid_edges(d)
+    T = stream_len_for(cfg, d)
+    feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T) for j in range(8)]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, dropout_seed=SEED)
+    ml.set_tasks(feats, task_ids=list(range(8)))
+    theta0, m0, v0 = ml.theta.clone(), ml.m.clone(), ml.v.clone()
+    runs = []
+    for _ in range(2):
+        ml.theta.copy_(theta0)
+        ml.m.copy_(m0)
+        ml.v.copy_(v0)
+        ml.step = 0
+        res = ml.meta_step()
+        runs.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone(), ml.theta.cpu().clone(),
+                     res.meta_loss))
+    L, N, G, TH, ML = runs[0]
+    assert L.shape == (11, 8) and N.shape == (10, 8)
+    assert np.isfinite(L.numpy()).all() and np.isfinite(N.numpy()).all() and np.isfinite(G.numpy()).all()
+    assert 0.5 < float(L[-1].mean()) < 2.0
+    assert float(N.min()) > 0.0
+    assert float(G.norm()) > 0.0 and not torch.equal(TH, theta0.cpu())
+    assert np.isfinite(ML)
+    for a, b in zip(runs[0][:4], runs[1][:4]):
+        assert torch.equal(a, b)
+    assert runs[0][4] == runs[1][4]

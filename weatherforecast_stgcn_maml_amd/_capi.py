@@ -29,7 +29,8 @@ ABI_VERSION = 5
 
 # kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
 VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kept", "fwd_dual_img", "bwd_big", "bwd_small", "bwd_split",
-            "bwd_dual_big", "bwd_dual_big_kept", "bwd_dual_small", "bwd_dual_small_kept", "wgrad", "wgrad_wide", "wgrad_pair")
+            "bwd_dual_big", "bwd_dual_big_kept", "bwd_dual_small", "bwd_dual_small_kept", "wgrad", "wgrad_wide", "wgrad_pair",
+            "wgrad_ws")
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",
@@ -200,6 +201,10 @@ class Context:
         self._d = Dims.from_model(dims)
         check(self._L.smaml_create(ctypes.byref(self._d), int(device), ctypes.byref(self._h)))
         self.device = device
+        # A/B runs: SMAML_OPTIONS="key=value,key=value" applies smaml_set_option knobs to every context
+        for kv in filter(None, os.environ.get("SMAML_OPTIONS", "").split(",")):
+            k, _, v = kv.partition("=")
+            self.set_option(k.strip(), int(v))
         self._keep = []
         self.graph_key = None
 

@@ -92,6 +92,7 @@ enum Variant {
   V_WGRAD,           // k_wgrad launches (any tile)
   V_WGRAD_WIDE,      // k_wgrad with 256 x 256 tiles (also counted as V_WGRAD)
   V_WGRAD_PAIR,      // k_wgrad summing two problems (tangent weight gradient; also counted as V_WGRAD)
+  V_WGRAD_WS,        // k_wgrad_ws, warp-specialised (also counted as V_WGRAD)
   NVAR
 };
 
@@ -118,6 +119,7 @@ struct Knobs {
   int gate_img;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
   int wgrad_wide;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
   int wgrad_pair;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
+  int wgrad_ws;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -390,6 +392,7 @@ struct WgradPlan {
   Drop drop;       // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
   int drop_layer;
   bool wide;       // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
+  bool ws = false; // warp-specialised 256 x 128 tiles (k_wgrad_ws; dropout-free launches only)
   // pair (pair_wgrad): slices [nsplit1, nsplit) sum A2^T [B1s | B2s] (same shape and strides) into
   // the same gradient; A2 == nullptr: one problem
   const float* A2 = nullptr;
@@ -413,6 +416,7 @@ struct WgMulti {
 };
 void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs);
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
+bool wgrad_ws_ok(int Mrows, int c1, int c2);  // shapes the warp-specialised weight gradient takes
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
 // clip_grad_norm_ + SGD of every task as one grid-barrier kernel (k_inner_sgd), or its two phases as
 // two launches (BarPlan)

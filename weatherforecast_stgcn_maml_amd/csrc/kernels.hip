@@ -1774,6 +1774,212 @@ __global__ __launch_bounds__(C::NTH) void k_wgrad(const float* __restrict__ A, i
                     ngroups, part, ldp, with_bias, dr, drop_layer, smem, pr);
 }
 
+// ---- warp-specialised weight gradients (round 4) ---------------------------------------------
+// The staged mainloop above has every wave load, split and store its share of the next K-tile AFTER its
+// MFMAs, and the two waves of a SIMD belong to the same workgroup, so they reach that VALU phase
+// together and the MFMA pipe idles through it (MFMA busy 0.57; ~170 VALU per 48 MFMAs per wave).
+// Here one 8-wave workgroup per CU splits the roles: waves 0-3 (one per SIMD) only read bf16 fragments
+// and issue MFMAs -- a 256 x 128 output tile, 64 x 128 per wave, 48 v_mfma_f32_32x32x16_bf16 per K-tile,
+// back to back -- while waves 4-7 (the other wave of each SIMD) load the operand tiles two K-tiles
+// ahead into registers, split them into the bf16 planes and store them into a 3-stage LDS ring. The
+// producer's VALU issues in the 24 of every 32 cycles an MFMA leaves the SIMD's vector issue free. One
+// workgroup barrier per K-tile: stage kt % 3 is read by the MFMA waves in iteration kt while the
+// producers fill stage (kt + 2) % 3, last read in iteration kt - 1. The producers also form the bias
+// column sums (each producer thread always stages the same 4 gate rows). Same products in the same
+// per-accumulator order as k_wgrad: bitwise-identical weight sums, bias sums up to summation order.
+// Layout conditions (wgrad_ws_ok): 4H % 256 == 0 and both column segments multiples of 128.
+#ifndef SMAML_WGRAD_WS
+#define SMAML_WGRAD_WS 1
+#endif
+using CfgWS = GemmCfg<256, 128, 4, 1, false, false, 16, 2, 3, false>;  // consumer view: 4 waves of 64 x 128
+constexpr int WS_NST = 3;
+constexpr int WS_SA = CfgWS::AImg::BYTES, WS_SB = CfgWS::BImg::BYTES, WS_STAGE = WS_SA + WS_SB;
+constexpr int WS_NTH = 512;                  // 4 MFMA waves + 4 producer waves
+constexpr int WS_AF4 = 256 * 16 / 4 / 256;   // A float4s per producer thread per K-tile (4)
+constexpr int WS_BF4 = 128 * 16 / 4 / 256;   // B float4s (2)
+static_assert(WS_NST * WS_STAGE <= 160 * 1024 - 4096, "LDS ring");
+
+bool wgrad_ws_ok(int Mrows, int c1, int c2) {
+  return SMAML_WGRAD_WS && CfgTN::X6S && Mrows % 256 == 0 && c1 % 128 == 0 && c2 % 128 == 0 && c1 + c2 > 0;
+}
+
+struct WsRegs {
+  float4 a[WS_AF4], b[WS_BF4];
+};
+
+// Producer thread p (0..255): A float4 i covers k-row p/64 + 4i, gate rows 4(p%64) .. +3; B float4 i
+// covers k-row p/32 + 8i, columns 4(p%32) .. +3 of the tile. Rows k >= K (and the shifted h_{t-1}
+// rows before Mshift) are zeros: the load address is clamped to a valid row and the value selected
+// away, so the loads are branch-free.
+__device__ __forceinline__ float4 sel0(bool keep, const float4& v) {
+  return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
+}
+__device__ __forceinline__ void ws_fetch(const float* __restrict__ A, int Mrows, const WgB& b, int m0, int n0,
+                                         int64_t k0, int p, WsRegs& r) {
+  // A: uniform tile base + a loop-invariant 32-bit lane offset (global_load saddr + voffset)
+  const float* Ab = A + k0 * Mrows + m0;
+  const uint32_t ao = 4u * (uint32_t)((p / 64) * Mrows + 4 * (p % 64));
+  if (k0 + 16 <= b.K) {
+#pragma unroll
+    for (int i = 0; i < WS_AF4; ++i) r.a[i] = ldo(Ab, ao + 16u * (uint32_t)(i * Mrows));
+  } else {
+#pragma unroll
+    for (int i = 0; i < WS_AF4; ++i) {
+      const int64_t k = k0 + p / 64 + 4 * i;
+      const bool ok = k < b.K;
+      r.a[i] = sel0(ok, ld4(A + m0 + 4 * (p % 64) + (ok ? k : b.K - 1) * Mrows));
+    }
+  }
+  const bool seg1 = n0 < b.c1;  // tile inside one column segment (uniform)
+  const float* base = seg1 ? b.B1 : b.B2;
+  if (!base) {  // an absent segment (the tangent pass's Rx at layer 0): zeros
+#pragma unroll
+    for (int i = 0; i < WS_BF4; ++i) r.b[i] = f4zero();
+    return;
+  }
+  const int ld = seg1 ? b.c1 : b.c2, c0 = seg1 ? n0 : n0 - b.c1;
+  const int64_t shift = seg1 ? 0 : b.Mshift, kmax = b.K - 1 - shift;  // valid rows kk in [0, kmax]
+  const int64_t kb = k0 - shift;
+  if (kb >= 0 && kb + 15 <= kmax) {
+    const float* Bb = base + kb * ld + c0;
+    const uint32_t bo = 4u * (uint32_t)((p / 32) * ld + 4 * (p % 32));
+#pragma unroll
+    for (int i = 0; i < WS_BF4; ++i) r.b[i] = ldo(Bb, bo + 32u * (uint32_t)(i * ld));
+  } else {
+#pragma unroll
+    for (int i = 0; i < WS_BF4; ++i) {
+      const int64_t kk = kb + p / 32 + 8 * i;
+      const bool ok = kk >= 0 && kk <= kmax;
+      r.b[i] = sel0(ok, ld4(base + c0 + 4 * (p % 32) + (ok ? kk : 0) * ld));
+    }
+  }
+}
+
+__device__ __forceinline__ void ws_store(char* st, int p, const WsRegs& r, float4& cs) {
+  using IA = CfgWS::AImg;
+  using IB = CfgWS::BImg;
+#pragma unroll
+  for (int i = 0; i < WS_AF4; ++i) {
+    cs.x += r.a[i].x;
+    cs.y += r.a[i].y;
+    cs.z += r.a[i].z;
+    cs.w += r.a[i].w;
+    const int off = IA::mc(p / 64 + 4 * i, 8 * (p % 64));
+    uint2 p0, p1, p2;
+    split4(r.a[i], p0, p1, p2);
+    *reinterpret_cast<uint2*>(st + off) = p0;
+    *reinterpret_cast<uint2*>(st + IA::PLANE + off) = p1;
+    *reinterpret_cast<uint2*>(st + 2 * IA::PLANE + off) = p2;
+  }
+  char* sb = st + WS_SA;
+#pragma unroll
+  for (int i = 0; i < WS_BF4; ++i) {
+    const int off = IB::mc(p / 32 + 8 * i, 8 * (p % 32));
+    uint2 p0, p1, p2;
+    split4(r.b[i], p0, p1, p2);
+    *reinterpret_cast<uint2*>(sb + off) = p0;
+    *reinterpret_cast<uint2*>(sb + IB::PLANE + off) = p1;
+    *reinterpret_cast<uint2*>(sb + 2 * IB::PLANE + off) = p2;
+  }
+}
+
+__global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
+                                                     int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn,
+                                                     int ntile, int nsplit, int ngroups, float* __restrict__ part,
+                                                     int ldp, int with_bias, WgPair pr) {
+  __shared__ __attribute__((aligned(16))) char ring[WS_NST * WS_STAGE];
+  const int L = (int)blockIdx.x;
+  const int j = L >> 3;  // XCD-aware: the tiles of one (split, task) group 8 blocks apart (wgrad_block)
+  const int g = (j / ntile) * 8 + (L & 7), tile = j - (j / ntile) * ntile;
+  if (g >= ngroups) return;
+  const int z = g / nsplit, split = g - z * nsplit;
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const bool sec = pr.A2 != nullptr && split >= pr.nsplit1;
+  if (sec) {
+    A = pr.A2;
+    lb.B1 = pr.B1s;
+    lb.B2 = pr.B2s;
+    with_bias = 0;
+  }
+  const float* Az = A + (int64_t)z * a_zstride;
+  WgB b = lb;
+  if (b.B1) b.B1 += (int64_t)z * b1_zstride;
+  if (b.B2) b.B2 += (int64_t)z * b2_zstride;
+  const int64_t kbeg = (int64_t)(sec ? split - pr.nsplit1 : split) * kchunk;
+  const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
+  const int nkt = (int)((kend - kbeg + 15) / 16);
+  const int m0 = tm * 256, n0 = tn * 128;
+  const bool mfma_wave = threadIdx.x < 256;
+  float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
+  if (mfma_wave) {
+    Acc<CfgWS> acc;
+    acc.zero();
+    __syncthreads();  // stages 0 and 1 filled
+    for (int kt = 0; kt < nkt; ++kt) {
+      const char* st = ring + (kt % WS_NST) * WS_STAGE;
+#if SMAML_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+      mma_tile_x6s<CfgWS>(st, st + WS_SA, acc);
+#if SMAML_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      __syncthreads();
+    }
+    __syncthreads();  // (matches the producers' bias-reduce barrier)
+#pragma unroll
+    for (int i = 0; i < CfgWS::WTM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < CfgWS::WTN; ++jj) {
+        const int c = n0 + acc_col<CfgWS>(jj);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) P[(int64_t)(m0 + acc_row<CfgWS>(i, r)) * ldp + c] = acc.v[i][jj][r];
+      }
+    return;
+  }
+  // producers
+  const int p = (int)threadIdx.x - 256;
+  float4 cs = f4zero();
+  WsRegs r0, r1;
+  if (nkt > 0) ws_fetch(Az, Mrows, b, m0, n0, kbeg, p, r0);
+  if (nkt > 1) ws_fetch(Az, Mrows, b, m0, n0, kbeg + 16, p, r1);
+  if (nkt > 0) ws_store(ring, p, r0, cs);
+  if (nkt > 2) ws_fetch(Az, Mrows, b, m0, n0, kbeg + 32, p, r0);
+  if (nkt > 1) ws_store(ring + WS_STAGE, p, r1, cs);
+  if (nkt > 3) ws_fetch(Az, Mrows, b, m0, n0, kbeg + 48, p, r1);
+  __syncthreads();
+  // iteration kt: store tile kt + 2 (registers loaded two iterations earlier) into stage (kt + 2) % 3,
+  // then load tile kt + 4 into the freed registers; unrolled by two so each register set is static
+  for (int kt = 0; kt < nkt; kt += 2) {
+    if (kt + 2 < nkt) ws_store(ring + ((kt + 2) % WS_NST) * WS_STAGE, p, r0, cs);
+    if (kt + 4 < nkt) ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 4) * 16, p, r0);
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    if (kt + 3 < nkt) ws_store(ring + ((kt + 3) % WS_NST) * WS_STAGE, p, r1, cs);
+    if (kt + 5 < nkt) ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 5) * 16, p, r1);
+    __syncthreads();
+  }
+  // bias column sums: rows 4q .. 4q+3 (q = p % 64) over the four producer threads sharing q
+  float* red = reinterpret_cast<float*>(ring);
+  st4(red + 4 * p, cs);
+  __syncthreads();
+  if (tn == 0 && p < 64) {
+    float4 v = ld4(red + 4 * p);
+#pragma unroll
+    for (int t = 1; t < 4; ++t) {
+      const float4 u = ld4(red + 4 * (p + 64 * t));
+      v.x += u.x;
+      v.y += u.y;
+      v.z += u.z;
+      v.w += u.w;
+    }
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    const int ncols = lb.c1 + lb.c2;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) P[(int64_t)(m0 + 4 * p + c) * ldp + ncols] = with_bias ? e[c] : 0.f;
+  }
+}
+
 // Several weight gradients in ONE launch (the LSTM layers of a small-grid backward: at batch 1 each
 // layer alone fills too little of the chip and its K loop is short). Problem q owns blocks
 // [blk[q], blk[q+1]) and partial slabs from part + poff[q].
@@ -1862,9 +2068,12 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
                 WgradPlan& p, bool multi) {
   const int ncols = c1 + c2;
   const int ldp = ncols + 1;
-  const bool wide = !multi && SMAML_WGRAD_WIDE && w.kn.wgrad_wide && CfgTW::X6S && ncols % CfgTW::BN == 0 &&
+  // (no masked-B variant of k_wgrad_ws: with LSTM dropout on, the staged tiles below)
+  const bool ws = !multi && w.kn.wgrad_ws && !w.drop.lstm() && wgrad_ws_ok(Mrows, c1, c2);
+  const bool wide = !ws && !multi && SMAML_WGRAD_WIDE && w.kn.wgrad_wide && CfgTW::X6S && ncols % CfgTW::BN == 0 &&
                     Mrows % CfgTW::BM == 0;
-  const int BMc = wide ? CfgTW::BM : CfgTN::BM, BNc = wide ? CfgTW::BN : CfgTN::BN;
+  const int BMc = ws ? CfgWS::BM : wide ? CfgTW::BM : CfgTN::BM, BNc = ws ? CfgWS::BN : wide ? CfgTW::BN : CfgTN::BN;
+  static_assert(WS_NTH == CfgTN::NTH, "one split-K plan for every tile");
   static_assert(CfgTW::NTH == CfgTN::NTH && CfgTW::BK == CfgTN::BK, "one split-K plan for both tiles");
   const int ntm = (Mrows + BMc - 1) / BMc;
   const int ntn = (ncols + BNc - 1) / BNc;
@@ -1906,6 +2115,7 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   p.nsplit = (int)nsplit;
   p.kchunk = kchunk;
   p.wide = wide;
+  p.ws = ws;
 }
 
 bool pair_wgrad(WgradPlan& p, const Work& w, const float* A2, const float* B1s, const float* B2s) {
@@ -1941,7 +2151,11 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
   k_wgrad<CFG, D_><<<grid, CFG::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, \
                                              p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0, \
                                              p.drop, D_ ? p.drop_layer : -1, WgPair{p.A2, p.B1s, p.B2s, p.nsplit1})
-  if (p.wide) {
+  if (p.ws) {
+    k_wgrad_ws<<<grid, WS_NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn,
+                                       ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
+                                       WgPair{p.A2, p.B1s, p.B2s, p.nsplit1});
+  } else if (p.wide) {
     if (drop)
       SMAML_WGRAD_LAUNCH(CfgTW, true);
     else

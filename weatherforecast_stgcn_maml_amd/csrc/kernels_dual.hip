@@ -486,6 +486,18 @@ constexpr int bwdd_smem_floats() {
 // one row (16-B loads / stores); the primal cell backward is re-derived from the kept dh. Writes
 // R(dG) in place over R(G) (each item's elements are read before they are written) and both
 // cell-state carries.
+#ifndef SMAML_NT_BWDD
+#define SMAML_NT_BWDD 0  // tangent BPTT: streaming (nt) loads / stores for everything but the weights
+#endif
+template <bool NT>
+__device__ __forceinline__ float4 ld4_(const float* p) {
+  if constexpr (NT) return ld4_nt(p); else return ld4(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st4_(float* p, const float4& v) {
+  if constexpr (NT) st4_nt(p, v); else st4(p, v);
+}
+
 template <int H, class C, bool HEAD, bool CHECK>
 __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const float* Gz, float* RGz,
                                                     const float* __restrict__ dhz, const float* __restrict__ Cz,
@@ -520,15 +532,15 @@ __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const flo
     const float* rp = RGz + row * G4 + j;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      v.g[g] = ld4(gp + g * H);
-      v.rg[g] = ld4(rp + g * H);
+      v.g[g] = ld4_<SMAML_NT_BWDD != 0>(gp + g * H);
+      v.rg[g] = ld4_<SMAML_NT_BWDD != 0>(rp + g * H);
     }
-    v.dh = ld4(dhz + row * H + j);
-    v.cp = ld4(Cz + row * H - pM + j);
-    v.rcp = ld4(RCz + row * H - pM + j);
-    v.dc = ld4(dcz + (int64_t)m * H + j);
-    v.rdc = ld4(rdcz + (int64_t)m * H + j);
-    if (HEAD) v.rhd = ld4(RdHz + (int64_t)m * H + j);
+    v.dh = ld4_<SMAML_NT_BWDD != 0>(dhz + row * H + j);
+    v.cp = ld4_<SMAML_NT_BWDD != 0>(Cz + row * H - pM + j);
+    v.rcp = ld4_<SMAML_NT_BWDD != 0>(RCz + row * H - pM + j);
+    v.dc = ld4_<SMAML_NT_BWDD != 0>(dcz + (int64_t)m * H + j);
+    v.rdc = ld4_<SMAML_NT_BWDD != 0>(rdcz + (int64_t)m * H + j);
+    if (HEAD) v.rhd = ld4_<SMAML_NT_BWDD != 0>(RdHz + (int64_t)m * H + j);
   };
   auto step = [&](int k, const V& v) {
     int r, m, j;
@@ -563,9 +575,9 @@ __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const flo
     }
     float* rp = RGz + (tM + m) * G4 + j;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) st4(rp + g * H, o[g]);
-    st4(dcz + (int64_t)m * H + j, odc);
-    st4(rdcz + (int64_t)m * H + j, ordc);
+    for (int g = 0; g < 4; ++g) st4_<SMAML_NT_BWDD != 0>(rp + g * H, o[g]);
+    st4_<SMAML_NT_BWDD != 0>(dcz + (int64_t)m * H + j, odc);
+    st4_<SMAML_NT_BWDD != 0>(rdcz + (int64_t)m * H + j, ordc);
   };
   V v;
 #pragma unroll 1
@@ -647,8 +659,8 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
       const float* a0 = up ? dGAll + oa : dGz + on;
       const float* r0 = up ? RGsAll + oa : RGz + on;
       const int64_t w0o = up ? wih_up : lo.whh;
-      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2>{{a0, dGz + on}, {G4, G4}, M},
-                                        SegKCt<2>{{r0, RGz + on}, {G4, G4}, M},
+      gemm_dual_mainloop<CfgNND, !KEPT>(SegKCt<2, SMAML_NT_BWDD != 0>{{a0, dGz + on}, {G4, G4}, M},
+                                        SegKCt<2, SMAML_NT_BWDD != 0>{{r0, RGz + on}, {G4, G4}, M},
                                         SegMCt<2>{{th + w0o, th + lo.whh}, {G4, G4}, H},
                                         SegMCt<2>{{u + w0o, u + lo.whh}, {G4, G4}, H}, m0, n0, ns * G4, 0, ap, at,
                                         smem);

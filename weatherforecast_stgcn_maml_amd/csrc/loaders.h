@@ -231,6 +231,28 @@ struct WgB {
 __device__ __forceinline__ float4 ldo(const float* base, uint32_t byteoff) {
   return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byteoff);
 }
+// Non-temporal (streaming) 16-B load / store: `nt` cache policy, so data read or written once per
+// launch does not evict what the launch re-reads from L2 (the per-task weight operands).
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+  const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4_nt(float* p, const float4& v) {
+  f32x4v w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
+}
+template <bool NT>
+__device__ __forceinline__ float4 ldo_(const float* base, uint32_t byteoff) {
+  if constexpr (NT)
+    return ld4_nt(reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + byteoff));
+  else
+    return ldo(base, byteoff);
+}
 
 // The segment holding K index k0 (segment widths w[], k-concatenated): its base pointer, width and
 // the offset inside it. Every member is read unconditionally and the choice is made on the values:
@@ -250,8 +272,8 @@ __device__ __forceinline__ void seg_pick(const P (&p)[NS], const int (&w)[NS], i
   ws = s == 0 ? w0 : s == 1 ? w1 : s == 2 ? w2 : w[NS - 1];
 }
 
-// KC operand [rows][w_s] per segment (row stride = width), k-concatenated.
-template <int NS>
+// KC operand [rows][w_s] per segment (row stride = width), k-concatenated. NT: streaming loads.
+template <int NS, bool NT = false>
 struct SegKCt {
   static constexpr bool kTileFetch = true;
   const float* p[NS];
@@ -268,7 +290,7 @@ struct SegKCt {
     for (int i = 0; i < F4; ++i) {
       const int f = (int)threadIdx.x + NTH * i;
       const int dr = min(row0 + f / (BK / 4), rows - 1) - row0;
-      r[i] = ldo(b, 4u * (uint32_t)(dr * ws + 4 * (f % (BK / 4))));
+      r[i] = ldo_<NT>(b, 4u * (uint32_t)(dr * ws + 4 * (f % (BK / 4))));
     }
   }
 };
