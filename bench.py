@@ -414,6 +414,8 @@ def main():
     if world > 1:
         dist.barrier()
     progress(f"rank {rank}: timed region done")
+    from weatherforecast_stgcn_maml_amd import _capi as _c
+    ml.ctx.sync(_c.stream_ptr(torch))  # a timed-out grid-barrier kernel would have invalidated the run: raise
     elapsed = time.perf_counter() - t0
     kern = None
     if not args.no_timing:

@@ -1791,10 +1791,15 @@ __global__ __launch_bounds__(C::NTH) void k_wgrad(const float* __restrict__ A, i
 #ifndef SMAML_WGRAD_WS
 #define SMAML_WGRAD_WS 1
 #endif
-using CfgWS = GemmCfg<256, 128, 4, 1, false, false, 16, 2, 3, false>;  // consumer view: 4 waves of 64 x 128
+#ifndef SMAML_WS_MW
+#define SMAML_WS_MW 8  // MFMA waves of k_wgrad_ws: 4 (64 x 128 each, one per SIMD) or 8 (32 x 128, two per SIMD)
+#endif
+template <int MW>
+using CfgWSm = GemmCfg<256, 128, MW, 1, false, false, 16, 2, 3, false>;  // the MFMA waves' view of the tile
+using CfgWS = CfgWSm<SMAML_WS_MW>;
 constexpr int WS_NST = 3;
 constexpr int WS_SA = CfgWS::AImg::BYTES, WS_SB = CfgWS::BImg::BYTES, WS_STAGE = WS_SA + WS_SB;
-constexpr int WS_NTH = 512;                  // 4 MFMA waves + 4 producer waves
+constexpr int WS_NTH = 64 * SMAML_WS_MW + 256;  // MFMA waves + 4 producer waves
 constexpr int WS_AF4 = 256 * 16 / 4 / 256;   // A float4s per producer thread per K-tile (4)
 constexpr int WS_BF4 = 128 * 16 / 4 / 256;   // B float4s (2)
 static_assert(WS_NST * WS_STAGE <= 160 * 1024 - 4096, "LDS ring");
@@ -1909,7 +1914,7 @@ __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A
   const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
   const int nkt = (int)((kend - kbeg + 15) / 16);
   const int m0 = tm * 256, n0 = tn * 128;
-  const bool mfma_wave = threadIdx.x < 256;
+  const bool mfma_wave = threadIdx.x < 64 * SMAML_WS_MW;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
   if (mfma_wave) {
     Acc<CfgWS> acc;
@@ -1938,7 +1943,7 @@ __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A
     return;
   }
   // producers
-  const int p = (int)threadIdx.x - 256;
+  const int p = (int)threadIdx.x - 64 * SMAML_WS_MW;
   float4 cs = f4zero();
   WsRegs r0, r1;
   if (nkt > 0) ws_fetch(Az, Mrows, b, m0, n0, kbeg, p, r0);
@@ -2073,7 +2078,7 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   const bool wide = !ws && !multi && SMAML_WGRAD_WIDE && w.kn.wgrad_wide && CfgTW::X6S && ncols % CfgTW::BN == 0 &&
                     Mrows % CfgTW::BM == 0;
   const int BMc = ws ? CfgWS::BM : wide ? CfgTW::BM : CfgTN::BM, BNc = ws ? CfgWS::BN : wide ? CfgTW::BN : CfgTN::BN;
-  static_assert(WS_NTH == CfgTN::NTH, "one split-K plan for every tile");
+
   static_assert(CfgTW::NTH == CfgTN::NTH && CfgTW::BK == CfgTN::BK, "one split-K plan for both tiles");
   const int ntm = (Mrows + BMc - 1) / BMc;
   const int ntn = (ncols + BNc - 1) / BNc;
