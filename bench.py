@@ -390,9 +390,11 @@ def main():
     mine = shard_tasks(args.tasks, rank, world)
     T_total = stream_len_for(cfg, d)
     feats = [synth.make_features(synth.task_seed(j), d.num_nodes, T_total) for j in mine]
+    # ranks sharing one GPU (the N>1 rehearsal on a one-GPU box) each plan task groups for their share of HBM
+    per_dev = -(-world // max(1, torch.cuda.device_count()))
     ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
                      ei, device=f"cuda:{local}", task_group=args.task_group, dropout=tuple(args.dropout),
-                     dropout_seed=SEED)
+                     dropout_seed=SEED, mem_share=1.0 / per_dev)
     ml.set_tasks(feats, task_ids=mine)
     torch.cuda.synchronize()
 

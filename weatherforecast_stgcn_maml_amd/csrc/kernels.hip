@@ -1791,6 +1791,9 @@ __global__ __launch_bounds__(C::NTH) void k_wgrad(const float* __restrict__ A, i
 #ifndef SMAML_WGRAD_WS
 #define SMAML_WGRAD_WS 1
 #endif
+#ifndef SMAML_WS_PRIO
+#define SMAML_WS_PRIO 1  // 1: MFMA waves at raised priority over their MFMA phase; 2: producer waves raised instead
+#endif
 #ifndef SMAML_WS_MW
 #define SMAML_WS_MW 8  // MFMA waves of k_wgrad_ws: 4 (64 x 128 each, one per SIMD) or 8 (32 x 128, two per SIMD)
 #endif
@@ -1819,44 +1822,37 @@ struct WsRegs {
 __device__ __forceinline__ float4 sel0(bool keep, const float4& v) {
   return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
 }
+__device__ __forceinline__ int iclamp(int64_t v, int lo, int hi) {
+  return (int)(v < lo ? lo : v > hi ? hi : v);
+}
 __device__ __forceinline__ void ws_fetch(const float* __restrict__ A, int Mrows, const WgB& b, int m0, int n0,
                                          int64_t k0, int p, WsRegs& r) {
-  // A: uniform tile base + a loop-invariant 32-bit lane offset (global_load saddr + voffset)
-  const float* Ab = A + k0 * Mrows + m0;
-  const uint32_t ao = 4u * (uint32_t)((p / 64) * Mrows + 4 * (p % 64));
-  if (k0 + 16 <= b.K) {
+  // Branch-free (no control flow between a load and its use, so the waitcnt pass keeps the two K-tiles
+  // of prefetch in flight) and register-light: a uniform tile base plus a 32-bit lane offset whose row is
+  // clamped into the matrix; out-of-range rows are selected to zero. A: rows k0 + rr < K.
+  const int alast = iclamp(b.K - 1 - k0, -1, 15);  // last valid tile row (uniform)
+  const float* Ab = A + k0 * Mrows + m0 + 4 * (p % 64);
 #pragma unroll
-    for (int i = 0; i < WS_AF4; ++i) r.a[i] = ldo(Ab, ao + 16u * (uint32_t)(i * Mrows));
-  } else {
-#pragma unroll
-    for (int i = 0; i < WS_AF4; ++i) {
-      const int64_t k = k0 + p / 64 + 4 * i;
-      const bool ok = k < b.K;
-      r.a[i] = sel0(ok, ld4(A + m0 + 4 * (p % 64) + (ok ? k : b.K - 1) * Mrows));
-    }
+  for (int i = 0; i < WS_AF4; ++i) {
+    const int rr = p / 64 + 4 * i;
+    r.a[i] = sel0(rr <= alast, ldo(Ab, 4u * (uint32_t)(min(rr, max(alast, 0)) * Mrows)));
   }
+  // B: source rows kk = k0 + rr - shift in [0, kmax] of the tile's column segment (h_{t-1} rows before
+  // Mshift and rows k >= K are zeros; an absent segment, the tangent pass's Rx at layer 0, is zeros)
   const bool seg1 = n0 < b.c1;  // tile inside one column segment (uniform)
   const float* base = seg1 ? b.B1 : b.B2;
-  if (!base) {  // an absent segment (the tangent pass's Rx at layer 0): zeros
+  const bool present = base != nullptr;
+  const int ld = seg1 ? b.c1 : b.c2;
+  const int64_t shift = seg1 ? 0 : b.Mshift, kmax = b.K - 1 - shift, kb = k0 - shift;
+  const int64_t kbase = present ? (kb < 0 ? 0 : kb > kmax ? kmax : kb) : 0;  // a valid row (uniform)
+  const int lo = iclamp(-kb, 0, 16), hi = iclamp(kmax - kb, -1, 15);       // valid tile rows [lo, hi]
+  const int dr = iclamp(kb - kbase, -(1 << 20), 0);                        // tile row rr -> kbase + rr + dr
+  const float* Bb = (present ? base + kbase * ld : A) + (seg1 ? n0 : n0 - b.c1) + 4 * (p % 32);
 #pragma unroll
-    for (int i = 0; i < WS_BF4; ++i) r.b[i] = f4zero();
-    return;
-  }
-  const int ld = seg1 ? b.c1 : b.c2, c0 = seg1 ? n0 : n0 - b.c1;
-  const int64_t shift = seg1 ? 0 : b.Mshift, kmax = b.K - 1 - shift;  // valid rows kk in [0, kmax]
-  const int64_t kb = k0 - shift;
-  if (kb >= 0 && kb + 15 <= kmax) {
-    const float* Bb = base + kb * ld + c0;
-    const uint32_t bo = 4u * (uint32_t)((p / 32) * ld + 4 * (p % 32));
-#pragma unroll
-    for (int i = 0; i < WS_BF4; ++i) r.b[i] = ldo(Bb, bo + 32u * (uint32_t)(i * ld));
-  } else {
-#pragma unroll
-    for (int i = 0; i < WS_BF4; ++i) {
-      const int64_t kk = kb + p / 32 + 8 * i;
-      const bool ok = kk >= 0 && kk <= kmax;
-      r.b[i] = sel0(ok, ld4(base + c0 + 4 * (p % 32) + (ok ? kk : 0) * ld));
-    }
+  for (int i = 0; i < WS_BF4; ++i) {
+    const int rr = p / 32 + 8 * i;
+    const bool ok = present && rr >= lo && rr <= hi;
+    r.b[i] = sel0(ok, ldo(Bb, 4u * (uint32_t)(ok ? (rr + dr) * ld : 0)));
   }
 }
 
@@ -1888,6 +1884,11 @@ __device__ __forceinline__ void ws_store(char* st, int p, const WsRegs& r, float
   }
 }
 
+// Ring barrier: LDS stores retired (lgkmcnt), then s_barrier -- NOT __syncthreads, whose workgroup
+// release fence also drains vmcnt, i.e. would wait for the producers' prefetch loads issued two K-tiles
+// ahead and expose their full latency every K-tile.
+__device__ __forceinline__ void ws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
                                                      int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn,
                                                      int ntile, int nsplit, int ngroups, float* __restrict__ part,
@@ -1913,23 +1914,26 @@ __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A
   const int64_t kbeg = (int64_t)(sec ? split - pr.nsplit1 : split) * kchunk;
   const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
   const int nkt = (int)((kend - kbeg + 15) / 16);
+  // an even K-tile count (ws plans use 32-row-multiple slices, so only the last slice can be odd; its
+  // padding tile lies past K and is zeros)
+  const int nkt2 = (nkt + 1) & ~1;
   const int m0 = tm * 256, n0 = tn * 128;
   const bool mfma_wave = threadIdx.x < 64 * SMAML_WS_MW;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
   if (mfma_wave) {
     Acc<CfgWS> acc;
     acc.zero();
-    __syncthreads();  // stages 0 and 1 filled
-    for (int kt = 0; kt < nkt; ++kt) {
+    ws_barrier();  // stages 0 and 1 filled
+    for (int kt = 0; kt < nkt2; ++kt) {
       const char* st = ring + (kt % WS_NST) * WS_STAGE;
-#if SMAML_PRIO
+#if SMAML_WS_PRIO == 1
       __builtin_amdgcn_s_setprio(1);
 #endif
       mma_tile_x6s<CfgWS>(st, st + WS_SA, acc);
-#if SMAML_PRIO
+#if SMAML_WS_PRIO == 1
       __builtin_amdgcn_s_setprio(0);
 #endif
-      __syncthreads();
+      ws_barrier();
     }
     __syncthreads();  // (matches the producers' bias-reduce barrier)
 #pragma unroll
@@ -1944,25 +1948,32 @@ __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A
   }
   // producers
   const int p = (int)threadIdx.x - 64 * SMAML_WS_MW;
+#if SMAML_WS_PRIO == 2
+  __builtin_amdgcn_s_setprio(1);
+#endif
   float4 cs = f4zero();
   WsRegs r0, r1;
-  if (nkt > 0) ws_fetch(Az, Mrows, b, m0, n0, kbeg, p, r0);
-  if (nkt > 1) ws_fetch(Az, Mrows, b, m0, n0, kbeg + 16, p, r1);
-  if (nkt > 0) ws_store(ring, p, r0, cs);
-  if (nkt > 2) ws_fetch(Az, Mrows, b, m0, n0, kbeg + 32, p, r0);
-  if (nkt > 1) ws_store(ring + WS_STAGE, p, r1, cs);
-  if (nkt > 3) ws_fetch(Az, Mrows, b, m0, n0, kbeg + 48, p, r1);
-  __syncthreads();
+  // prologue: tiles 0 and 1 into stages 0 and 1, tiles 2 and 3 in flight (a tile past the slice is
+  // loaded but never stored into a stage the MFMA waves read: its rows are zeros (k >= K) or are
+  // another slice's, unread)
+  ws_fetch(Az, Mrows, b, m0, n0, kbeg, p, r0);
+  ws_fetch(Az, Mrows, b, m0, n0, kbeg + 16, p, r1);
+  float4 nocs = f4zero();
+  ws_store(ring, p, r0, cs);
+  ws_fetch(Az, Mrows, b, m0, n0, kbeg + 32, p, r0);
+  ws_store(ring + WS_STAGE, p, r1, nkt > 1 ? cs : nocs);
+  ws_fetch(Az, Mrows, b, m0, n0, kbeg + 48, p, r1);
+  ws_barrier();
   // iteration kt: store tile kt + 2 (registers loaded two iterations earlier) into stage (kt + 2) % 3,
-  // then load tile kt + 4 into the freed registers; unrolled by two so each register set is static
-  for (int kt = 0; kt < nkt; kt += 2) {
-    if (kt + 2 < nkt) ws_store(ring + ((kt + 2) % WS_NST) * WS_STAGE, p, r0, cs);
-    if (kt + 4 < nkt) ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 4) * 16, p, r0);
-    __syncthreads();
-    if (kt + 1 >= nkt) break;
-    if (kt + 3 < nkt) ws_store(ring + ((kt + 3) % WS_NST) * WS_STAGE, p, r1, cs);
-    if (kt + 5 < nkt) ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 5) * 16, p, r1);
-    __syncthreads();
+  // then load tile kt + 4 into the freed registers; unrolled by two (nkt2 is even) so each register
+  // set is static and no load sits under a branch
+  for (int kt = 0; kt < nkt2; kt += 2) {
+    ws_store(ring + ((kt + 2) % WS_NST) * WS_STAGE, p, r0, kt + 2 < nkt ? cs : nocs);
+    ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 4) * 16, p, r0);
+    ws_barrier();
+    ws_store(ring + ((kt + 3) % WS_NST) * WS_STAGE, p, r1, kt + 3 < nkt ? cs : nocs);
+    ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 5) * 16, p, r1);
+    ws_barrier();
   }
   // bias column sums: rows 4q .. 4q+3 (q = p % 64) over the four producer threads sharing q
   float* red = reinterpret_cast<float*>(ring);
@@ -2091,7 +2102,9 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   const int64_t per_split = (int64_t)w.Z * Mrows * ldp;
   if (nsplit * per_split > w.wpart_floats) nsplit = w.wpart_floats / per_split;
   if (nsplit < 1) nsplit = 1;
-  const int64_t kchunk = ((ktiles + nsplit - 1) / nsplit) * CfgTN::BK;
+  int64_t kt_per = (ktiles + nsplit - 1) / nsplit;
+  if (ws) kt_per += kt_per & 1;  // k_wgrad_ws runs K-tiles in pairs: every slice but the last even
+  const int64_t kchunk = kt_per * CfgTN::BK;
   nsplit = (K + kchunk - 1) / kchunk;
   p.A = A;
   p.a_zstride = a_zstride;
@@ -2126,7 +2139,9 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
 bool pair_wgrad(WgradPlan& p, const Work& w, const float* A2, const float* B1s, const float* B2s) {
   const int64_t ktiles = (p.K + CfgTN::BK - 1) / CfgTN::BK;
   const int64_t n1 = std::max<int64_t>(1, p.nsplit / 2);
-  const int64_t kchunk = ((ktiles + n1 - 1) / n1) * CfgTN::BK;
+  int64_t kt_per = (ktiles + n1 - 1) / n1;
+  if (p.ws) kt_per += kt_per & 1;  // (k_wgrad_ws: even slices)
+  const int64_t kchunk = kt_per * CfgTN::BK;
   const int64_t nsplit1 = (p.K + kchunk - 1) / kchunk;
   // 2 * nsplit1 slices can exceed the planned count (a plan of one slice gives two); check them
   // against the partial-slab buffer and leave the plan unpaired if they do not fit

@@ -474,11 +474,15 @@ using CfgBwdD = GemmCfg<SMAML_BWD_BM, 128, SMAML_BWD_WM, SMAML_BWD_WN, true, fal
 #ifndef SMAML_BWDD_HALFEPI
 #define SMAML_BWDD_HALFEPI (SMAML_X6 ? 1 : 0)
 #endif
+#ifndef SMAML_BWDD_MIN_LDS
+#define SMAML_BWDD_MIN_LDS 0  // A/B: pad the tangent BPTT's LDS to at least this many bytes (e.g. 56 KB: 2 WGs per CU)
+#endif
 template <class C>
 constexpr int bwdd_smem_floats() {
   constexpr int E = (SMAML_BWDD_HALFEPI && C::WAVES_M == 2) ? C::BM * C::BN / 2 : C::BM * C::BN;
   constexpr int S = C::X6S ? DualStage<C>::X6S_FLOATS : DualStage<C>::FLOATS;
-  return S > E ? S : E;
+  constexpr int F = S > E ? S : E;
+  return F > SMAML_BWDD_MIN_LDS / 4 ? F : SMAML_BWDD_MIN_LDS / 4;
 }
 
 // Tangent-only cell backward of a kept step (see kernels.hip bwd_cell_): R(dh) = the GEMM

@@ -120,7 +120,7 @@ class MetaLearner:
 
     def __init__(self, dims: ModelDims, cfg: MamlConfig, gcn_params: dict, theta: dict,
                  edge_index: np.ndarray, device=None, process_group=None, task_group="auto",
-                 dropout=(0.0, 0.0), dropout_seed: int = 0):
+                 dropout=(0.0, 0.0), dropout_seed: int = 0, mem_share: float = 1.0):
         """``task_group``: tasks batched into one pass of the C driver. ``None`` = all of this
         rank's tasks at once; ``"auto"`` (default) = plan_task_group: second-order meta-steps run
         in groups small enough that every inner step's primal stays resident for the sweep.
@@ -130,7 +130,11 @@ class MetaLearner:
         inner loop (STGCN ``dropout_rate`` after conv1-3, ``lstm_dropout`` between LSTM layers
         and on the head input), with counter-based masks keyed by
         (``dropout_seed``, meta-step, global task id, inner step, element). (0, 0) = off: the
-        reference parity setting."""
+        reference parity setting.
+
+        ``mem_share``: the fraction of the device's free HBM the "auto" task-group plan may use (several
+        processes sharing one GPU, e.g. a multi-rank rehearsal on one device, each plan for their share)."""
+        self.mem_share = float(mem_share)
         self.dims = dims
         self.cfg = cfg
         self.task_group = task_group
@@ -174,7 +178,7 @@ class MetaLearner:
         tg = self.task_group
         if tg == "auto":
             free, _ = torch.cuda.mem_get_info(self.device)
-            tg = plan_task_group(self.dims, self.cfg, len(feats), free)
+            tg = plan_task_group(self.dims, self.cfg, len(feats), int(free * self.mem_share))
         G = min(tg or len(feats), len(feats))
         self._groups = [(z0, feats[z0:z0 + G]) for z0 in range(0, len(feats), G)]
         self.ctx.set_tasks(self._groups[0][1])
