@@ -450,3 +450,32 @@ def test_wgrad_variants_match(knob):
         del ml
     np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-6)
     assert rel(out[0][1], out[1][1]) < 1e-6
+
+
+@pytest.mark.parametrize("knob", ["bwdd_remap"])
+def test_order_only_knobs_bitwise(knob):
+    """Knobs that only reorder work between workgroups (bwdd_remap: the tangent BPTT's pair-segment
+    tile order per XCD) leave every tile's arithmetic unchanged: a second-order meta-step (big tangent
+    BPTT tiles forced, every primal kept) is bitwise equal with the knob on and off."""
+    from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
+
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=4, order=2)
+    P = synth.init_params(47, d, gcn_bias_scale=0.1)
+    Ptr, Pg, _ = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(4700 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(3)]
+    out = []
+    for on in (1, 0):
+        ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
+        ml.set_tasks(feats)
+        ml.ctx.set_option("bwdd_big_min", 0)
+        ml.ctx.set_option(knob, on)
+        ml.ctx.variant_counts(reset=True)
+        res = ml.meta_step()
+        vc = ml.ctx.variant_counts()
+        assert vc["bwd_dual_big_kept"] > 0, vc
+        out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
+        del ml
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)

@@ -510,6 +510,63 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   }
 }
 
+// The staged mainloop with the global loads issued TWO K-tiles ahead (two register sets): a K-tile's
+// loads are issued before the MFMA phase of the tile before the one they feed, so they have two MFMA
+// phases (not one) to land before the split + LDS store needs them. Two LDS stages, one barrier per
+// K-tile; unrolled by two so each register set is static. The fetch and the store run unconditionally
+// (a fetch past the slice reads rows the loaders return as zeros or rows of another slice; its store
+// goes to the idle stage nobody reads), so no load sits under a branch and the waitcnt pass keeps the
+// next tile's loads in flight across the barrier. Same products in the same order as
+// gemm_mainloop_x6s: bitwise-identical results.
+template <class C, int IG, class LA, class LB, class Hook>
+__device__ __forceinline__ void gemm_mainloop_x6s_pf2(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
+                                                      Acc<C>& acc, float* smem, Hook& hook) {
+  static_assert(C::X6S && C::X6S_NST == 2 && !has_dma_image<LB>::value, "pf2: staged, two stages, f32 B");
+  constexpr int BKc = C::BK;
+  constexpr int SA = C::AImg::BYTES;
+  char* st0 = reinterpret_cast<char*>(smem);
+  const int nkt = (kend - kbeg + BKc - 1) / BKc;
+  if (nkt <= 0) return;
+  float4 ra0[C::A_F4], ra1[C::A_F4];
+  BStage<C, LB> rb0, rb1;
+  auto fetch = [&](float4 (&ra)[C::A_F4], BStage<C, LB>& rb, int k0) {
+    fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, k0, ra);
+    rb.fetch(lb, n0, k0, nullptr);
+  };
+  auto store = [&](char* st, const float4 (&ra)[C::A_F4], const BStage<C, LB>& rb, bool sum) {
+    if constexpr (has_stage_a<Hook>::value)
+      if (sum) hook.template stage_a<C::A_F4>(ra);
+    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc, C::MSW>(st, ra);
+    rb.store(st + SA);
+  };
+  auto mma = [&](int kt) {
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+    mma_tile_x6s<C, IG>(st0 + (kt & 1) * C::X6S_STAGE, st0 + (kt & 1) * C::X6S_STAGE + SA, acc);
+#if SMAML_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  };
+  fetch(ra0, rb0, kbeg);
+  fetch(ra1, rb1, kbeg + BKc);
+  store(st0, ra0, rb0, true);
+  __syncthreads();
+  // iteration kt: tile kt in stage kt & 1, tile kt + 1 in the other register set; load tile kt + 2
+  // into this set, MFMAs of tile kt, store tile kt + 1 into the idle stage, barrier
+  for (int kt = 0; kt < nkt; kt += 2) {
+    fetch(ra0, rb0, kbeg + (kt + 2) * BKc);
+    mma(kt);
+    store(st0 + ((kt + 1) & 1) * C::X6S_STAGE, ra1, rb1, kt + 1 < nkt);
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    fetch(ra1, rb1, kbeg + (kt + 3) * BKc);
+    mma(kt + 1);
+    store(st0 + (kt & 1) * C::X6S_STAGE, ra0, rb0, kt + 2 < nkt);
+    __syncthreads();
+  }
+}
+
 // acc += sum_{k in [kbeg,kend)} A[m0+., k] * B[n0+., k]
 // IG >= 0: ask LLVM for iglp_opt strategy IG in the MFMA phase (set per call site by A/B).
 template <class C, int IG = -1, class LA, class LB, class Hook>

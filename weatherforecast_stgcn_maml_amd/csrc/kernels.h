@@ -120,6 +120,7 @@ struct Knobs {
   int wgrad_wide;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
   int wgrad_pair;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
   int wgrad_ws;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
+  int bwdd_remap;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1

@@ -1684,6 +1684,18 @@ constexpr int wgrad_smem_floats() {
 // Pair (A2 != null): slices [nsplit1, nsplit) of each task sum a second problem of the same shape,
 // A2^T [B1s | B2s] (the tangent weight gradient's dG^T [Rx | Rh] beside R(dG)^T [x | h]), into the
 // same partial slabs; its slices carry no bias column (zeros).
+#ifndef SMAML_WGRAD_PF2
+#define SMAML_WGRAD_PF2 0  // weight-gradient staged mainloop with loads two K-tiles ahead (gemm_mainloop_x6s_pf2)
+#endif
+template <class C, class LA, class LB, class Hook>
+__device__ __forceinline__ void wgrad_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
+                                               Acc<C>& acc, float* smem, Hook& hook) {
+  if constexpr (SMAML_WGRAD_PF2 && C::X6S && C::X6S_NST == 2)
+    gemm_mainloop_x6s_pf2<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
+  else
+    gemm_mainloop<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
+}
+
 struct WgPair {
   const float* A2;
   const float *B1s, *B2s;
@@ -1724,9 +1736,10 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
     const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
                               (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
     if (tn == 0 && with_bias) {
-      gemm_mainloop<C, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+      wgrad_mainloop<C>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     } else {
-      gemm_mainloop<C, kWgradIG>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem);
+      NoHook nh;
+      wgrad_mainloop<C>(la, bd, m0, n0, (int)kbeg, (int)kend, acc, smem, nh);
     }
   } else if (std::is_same<C, CfgTN>::value && SMAML_WGRAD_GLDS && kWgradGldsShape && Mrows == CfgTN::BM && lb.c1 % CfgTN::BN == 0 &&
              lb.c2 % CfgTN::BN == 0) {
@@ -1743,9 +1756,10 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
     // (branch-free tile loaders for both operands measured slower here twice: with the f32 MFMA,
     // wgrad 723 -> 820 ms per meta-step, profiles/r02_ab_wgrad_gcn_tile_loaders.log; with the staged
     // bf16x6 split and 256 x 256 tiles, 498 -> 552 ms, profiles/r03_ab_wgrad_tile_loaders.log)
-    gemm_mainloop<C, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    wgrad_mainloop<C>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
   } else {
-    gemm_mainloop<C, kWgradIG>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem);
+    NoHook nh;
+    wgrad_mainloop<C>(la, b, m0, n0, (int)kbeg, (int)kend, acc, smem, nh);
   }
   const int ncols = lb.c1 + lb.c2;
   float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
@@ -1802,86 +1816,73 @@ using CfgWSm = GemmCfg<256, 128, MW, 1, false, false, 16, 2, 3, false>;  // the 
 using CfgWS = CfgWSm<SMAML_WS_MW>;
 constexpr int WS_NST = 3;
 constexpr int WS_SA = CfgWS::AImg::BYTES, WS_SB = CfgWS::BImg::BYTES, WS_STAGE = WS_SA + WS_SB;
-constexpr int WS_NTH = 64 * SMAML_WS_MW + 256;  // MFMA waves + 4 producer waves
-constexpr int WS_AF4 = 256 * 16 / 4 / 256;   // A float4s per producer thread per K-tile (4)
-constexpr int WS_BF4 = 128 * 16 / 4 / 256;   // B float4s (2)
-static_assert(WS_NST * WS_STAGE <= 160 * 1024 - 4096, "LDS ring");
+constexpr int WS_NP = 8;                          // producer waves
+constexpr int WS_NTH = 64 * (SMAML_WS_MW + WS_NP);  // MFMA waves + producer waves
+constexpr int WS_NPT = 64 * WS_NP;                 // producer threads (512)
+static_assert(WS_NPT == 256 * 16 / 8, "one 8-row A chunk per producer thread per K-tile");
+static_assert(WS_NST * WS_STAGE <= 160 * 1024 - 8192, "LDS ring");
 
 bool wgrad_ws_ok(int Mrows, int c1, int c2) {
   return SMAML_WGRAD_WS && CfgTN::X6S && Mrows % 256 == 0 && c1 % 128 == 0 && c2 % 128 == 0 && c1 + c2 > 0;
 }
 
+// A producer thread's share of one K-tile: one 8-row chunk of A (k-row p / 32, gate rows 8 (p % 32)
+// .. +7) and, for the first 256 producer threads (uniform per wave), one 8-row chunk of B (k-row
+// p / 16, tile columns 8 (p % 16) .. +7). 8 rows = 16 B per bf16 plane: one ds_write_b128 per plane
+// (the wide store runs at full rate from one wave per SIMD; ds_write_b64 needs ~4).
 struct WsRegs {
-  float4 a[WS_AF4], b[WS_BF4];
+  float4 a[2], b[2];
 };
 
-// Producer thread p (0..255): A float4 i covers k-row p/64 + 4i, gate rows 4(p%64) .. +3; B float4 i
-// covers k-row p/32 + 8i, columns 4(p%32) .. +3 of the tile. Rows k >= K (and the shifted h_{t-1}
-// rows before Mshift) are zeros: the load address is clamped to a valid row and the value selected
-// away, so the loads are branch-free.
 __device__ __forceinline__ float4 sel0(bool keep, const float4& v) {
   return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
-}
-__device__ __forceinline__ int iclamp(int64_t v, int lo, int hi) {
-  return (int)(v < lo ? lo : v > hi ? hi : v);
 }
 __device__ __forceinline__ void ws_fetch(const float* __restrict__ A, int Mrows, const WgB& b, int m0, int n0,
                                          int64_t k0, int p, WsRegs& r) {
   // Branch-free (no control flow between a load and its use, so the waitcnt pass keeps the two K-tiles
-  // of prefetch in flight) and register-light: a uniform tile base plus a 32-bit lane offset whose row is
-  // clamped into the matrix; out-of-range rows are selected to zero. A: rows k0 + rr < K.
-  const int alast = iclamp(b.K - 1 - k0, -1, 15);  // last valid tile row (uniform)
-  const float* Ab = A + k0 * Mrows + m0 + 4 * (p % 64);
-#pragma unroll
-  for (int i = 0; i < WS_AF4; ++i) {
-    const int rr = p / 64 + 4 * i;
-    r.a[i] = sel0(rr <= alast, ldo(Ab, 4u * (uint32_t)(min(rr, max(alast, 0)) * Mrows)));
+  // of prefetch in flight): rows are clamped into the matrix and out-of-range ones selected to zero.
+  // A: rows k < K.
+  {
+    const int64_t k = k0 + p / 32;
+    const bool ok = k < b.K;
+    const float* src = A + (ok ? k : b.K - 1) * Mrows + m0 + 8 * (p % 32);
+    r.a[0] = sel0(ok, ld4(src));
+    r.a[1] = sel0(ok, ld4(src + 4));
   }
-  // B: source rows kk = k0 + rr - shift in [0, kmax] of the tile's column segment (h_{t-1} rows before
+  // B: source rows kk = k - shift in [0, kmax] of the tile's column segment (h_{t-1} rows before
   // Mshift and rows k >= K are zeros; an absent segment, the tangent pass's Rx at layer 0, is zeros)
   const bool seg1 = n0 < b.c1;  // tile inside one column segment (uniform)
   const float* base = seg1 ? b.B1 : b.B2;
-  const bool present = base != nullptr;
   const int ld = seg1 ? b.c1 : b.c2;
-  const int64_t shift = seg1 ? 0 : b.Mshift, kmax = b.K - 1 - shift, kb = k0 - shift;
-  const int64_t kbase = present ? (kb < 0 ? 0 : kb > kmax ? kmax : kb) : 0;  // a valid row (uniform)
-  const int lo = iclamp(-kb, 0, 16), hi = iclamp(kmax - kb, -1, 15);       // valid tile rows [lo, hi]
-  const int dr = iclamp(kb - kbase, -(1 << 20), 0);                        // tile row rr -> kbase + rr + dr
-  const float* Bb = (present ? base + kbase * ld : A) + (seg1 ? n0 : n0 - b.c1) + 4 * (p % 32);
-#pragma unroll
-  for (int i = 0; i < WS_BF4; ++i) {
-    const int rr = p / 32 + 8 * i;
-    const bool ok = present && rr >= lo && rr <= hi;
-    r.b[i] = sel0(ok, ldo(Bb, 4u * (uint32_t)(ok ? (rr + dr) * ld : 0)));
-  }
+  const int64_t shift = seg1 ? 0 : b.Mshift, kmax = b.K - 1 - shift;
+  const int64_t kk = k0 + (p & 255) / 16 - shift;
+  const bool ok = base != nullptr && kk >= 0 && kk <= kmax && p < 256;
+  const float* src = (base ? base : A) + (ok ? kk * ld : 0) + (seg1 ? n0 : n0 - b.c1) + 8 * (p % 16);
+  r.b[0] = sel0(ok, ld4(src));
+  r.b[1] = sel0(ok, ld4(src + 4));
 }
 
-__device__ __forceinline__ void ws_store(char* st, int p, const WsRegs& r, float4& cs) {
+__device__ __forceinline__ void split8_store(char* img, int plane, int off, const float4& lo, const float4& hi) {
+  uint2 a0, a1, a2, b0, b1, b2;
+  split4(lo, a0, a1, a2);
+  split4(hi, b0, b1, b2);
+  *reinterpret_cast<uint4*>(img + off) = make_uint4(a0.x, a0.y, b0.x, b0.y);
+  *reinterpret_cast<uint4*>(img + plane + off) = make_uint4(a1.x, a1.y, b1.x, b1.y);
+  *reinterpret_cast<uint4*>(img + 2 * plane + off) = make_uint4(a2.x, a2.y, b2.x, b2.y);
+}
+
+__device__ __forceinline__ void ws_store(char* st, int p, const WsRegs& r, float4 (&cs)[2]) {
   using IA = CfgWS::AImg;
   using IB = CfgWS::BImg;
 #pragma unroll
-  for (int i = 0; i < WS_AF4; ++i) {
-    cs.x += r.a[i].x;
-    cs.y += r.a[i].y;
-    cs.z += r.a[i].z;
-    cs.w += r.a[i].w;
-    const int off = IA::mc(p / 64 + 4 * i, 8 * (p % 64));
-    uint2 p0, p1, p2;
-    split4(r.a[i], p0, p1, p2);
-    *reinterpret_cast<uint2*>(st + off) = p0;
-    *reinterpret_cast<uint2*>(st + IA::PLANE + off) = p1;
-    *reinterpret_cast<uint2*>(st + 2 * IA::PLANE + off) = p2;
+  for (int h = 0; h < 2; ++h) {
+    cs[h].x += r.a[h].x;
+    cs[h].y += r.a[h].y;
+    cs[h].z += r.a[h].z;
+    cs[h].w += r.a[h].w;
   }
-  char* sb = st + WS_SA;
-#pragma unroll
-  for (int i = 0; i < WS_BF4; ++i) {
-    const int off = IB::mc(p / 32 + 8 * i, 8 * (p % 32));
-    uint2 p0, p1, p2;
-    split4(r.b[i], p0, p1, p2);
-    *reinterpret_cast<uint2*>(sb + off) = p0;
-    *reinterpret_cast<uint2*>(sb + IB::PLANE + off) = p1;
-    *reinterpret_cast<uint2*>(sb + 2 * IB::PLANE + off) = p2;
-  }
+  split8_store(st, IA::PLANE, IA::mc(p / 32, 16 * (p % 32)), r.a[0], r.a[1]);
+  if (p < 256) split8_store(st + WS_SA, IB::PLANE, IB::mc(p / 16, 16 * (p % 16)), r.b[0], r.b[1]);
 }
 
 // Ring barrier: LDS stores retired (lgkmcnt), then s_barrier -- NOT __syncthreads, whose workgroup
@@ -1951,14 +1952,13 @@ __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A
 #if SMAML_WS_PRIO == 2
   __builtin_amdgcn_s_setprio(1);
 #endif
-  float4 cs = f4zero();
+  float4 cs[2] = {f4zero(), f4zero()}, nocs[2] = {f4zero(), f4zero()};
   WsRegs r0, r1;
   // prologue: tiles 0 and 1 into stages 0 and 1, tiles 2 and 3 in flight (a tile past the slice is
   // loaded but never stored into a stage the MFMA waves read: its rows are zeros (k >= K) or are
-  // another slice's, unread)
+  // another slice's, unread, and its column sums go to nocs)
   ws_fetch(Az, Mrows, b, m0, n0, kbeg, p, r0);
   ws_fetch(Az, Mrows, b, m0, n0, kbeg + 16, p, r1);
-  float4 nocs = f4zero();
   ws_store(ring, p, r0, cs);
   ws_fetch(Az, Mrows, b, m0, n0, kbeg + 32, p, r0);
   ws_store(ring + WS_STAGE, p, r1, nkt > 1 ? cs : nocs);
@@ -1975,15 +1975,17 @@ __global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A
     ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 5) * 16, p, r1);
     ws_barrier();
   }
-  // bias column sums: rows 4q .. 4q+3 (q = p % 64) over the four producer threads sharing q
+  // bias column sums: gate rows 8q .. 8q+7 (q = p % 32) over the 16 producer threads sharing q
   float* red = reinterpret_cast<float*>(ring);
-  st4(red + 4 * p, cs);
+  st4(red + 8 * p, cs[0]);
+  st4(red + 8 * p + 4, cs[1]);
   __syncthreads();
-  if (tn == 0 && p < 64) {
-    float4 v = ld4(red + 4 * p);
+  if (tn == 0 && p < 64) {  // thread p: gate rows 4p .. 4p+3 = half (p & 1) of chunk q = p / 2
+    const int q = p >> 1, hh = p & 1;
+    float4 v = ld4(red + 8 * q + 4 * hh);
 #pragma unroll
-    for (int t = 1; t < 4; ++t) {
-      const float4 u = ld4(red + 4 * (p + 64 * t));
+    for (int t = 1; t < 16; ++t) {
+      const float4 u = ld4(red + 8 * (q + 32 * t) + 4 * hh);
       v.x += u.x;
       v.y += u.y;
       v.z += u.z;

@@ -601,6 +601,29 @@ __device__ __forceinline__ void bwd_dual_kept_cell_(const float* smem, const flo
 // re-derived elementwise from the kept dh, and only R(dG) and the carries are written.
 // Otherwise dGAll == GsAll (dG written in place over the gates) and dhAll is unused.
 // DROP: as k_lstm_bwd_step (the layer-above segment masked by drop(h_l) before the recurrent one).
+// Pair-segment tile order (knob bwdd_remap): the weight operands [W_ih(l+1); W_hh(l)] and U of a
+// tile depend on its (task, problem) pair (per-task fast weights: 1 MB of f32 per pair), and in the
+// hardware order every XCD holds tiles of ~7 pairs at once (3 workgroups x 32 CUs = 96 tiles per
+// XCD, 111 row tiles per pair), more than its 4 MB L2 keeps. Here each pair's row tiles are cut in
+// two segments, the segments are ordered problem-major and dealt to the XCDs round-robin, and XCD x
+// (hardware id L % 8, in the order L / 8 it receives them) runs its segments one after another: ~2
+// pairs' weights per XCD at a time, every XCD a similar mix of problems. 1-D grid; ids past the
+// segments or past a short segment exit at once.
+struct PairRemap {
+  int on;
+  int Z, R, seg, NS;  // tasks, row tiles per pair, tiles per segment, segments (= problems x Z x 2)
+};
+__device__ __forceinline__ bool remap_pair(const PairRemap& rm, int Lid, int& p, int& z, int& mb) {
+  const int x = Lid & 7, j = Lid >> 3;
+  const int slot = j / rm.seg, rin = j - slot * rm.seg;
+  const int g = x + 8 * slot;
+  if (g >= rm.NS) return false;
+  p = g / (2 * rm.Z);
+  z = (g >> 1) % rm.Z;
+  mb = (g & 1) * rm.seg + rin;
+  return mb < rm.R;
+}
+
 template <int H, class CfgNND, bool KEPT, bool DROP>
 __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(const float* GsAll, float* dGAll,
                                                       const float* __restrict__ dhAll, float* __restrict__ RGsAll,
@@ -609,17 +632,24 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
                                                       float* __restrict__ dcAll, float* __restrict__ RdcAll,
                                                       int64_t lsz, const float* __restrict__ theta,
                                                       const float* __restrict__ U, int64_t tstride, BwdWave wv, int L,
-                                                      int T, int M, Drop dr) {
+                                                      int T, int M, Drop dr, PairRemap rm) {
   __shared__ float smem[bwdd_smem_floats<CfgNND>()];
   constexpr int G4 = 4 * H;
-  const Blk bk = xcd_block();
-  int mb;
-  const int p = bwd_block(wv, bk.x, mb);
+  int mb, p, z, ny;
+  if (rm.on) {  // 1-D grid, one column tile (H == BN)
+    if (!remap_pair(rm, (int)blockIdx.x, p, z, mb)) return;
+    ny = 0;
+  } else {
+    const Blk bk = xcd_block();
+    p = bwd_block(wv, bk.x, mb);
+    z = bk.z;
+    ny = bk.y;
+  }
+  const int Zt = rm.on ? rm.Z : (int)gridDim.z;
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
-  const int z = bk.z;
-  const int m0 = mb * CfgNND::BM, n0 = bk.y * CfgNND::BN;
+  const int m0 = mb * CfgNND::BM, n0 = ny * CfgNND::BN;
   const int64_t slab = (int64_t)z * T * M;
   const float* th = theta + (int64_t)z * tstride;
   const float* u = U + (int64_t)z * tstride;
@@ -629,8 +659,8 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   const float* dhz = dhAll + (int64_t)l * lsz + slab * H;
   const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
   const float* RCz = RCsAll + (int64_t)l * lsz + slab * H;
-  float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
-  float* rdcz = RdcAll + ((int64_t)l * gridDim.z + z) * M * H;
+  float* dcz = dcAll + ((int64_t)l * Zt + z) * M * H;
+  float* rdcz = RdcAll + ((int64_t)l * Zt + z) * M * H;
   Acc<CfgNND> ap, at;
   ap.zero();
   at.zero();
@@ -754,15 +784,25 @@ static void bwd_dual_grid(hipStream_t s, const Dims& d, const Work& w, const Bwd
                           const float* U, int64_t tstride) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   dim3 grid(wv.off[wv.n], ntn, w.Z);
+  PairRemap rm{};
+  const int R = wv.n > 0 ? wv.off[1] - wv.off[0] : 0;  // row tiles per problem
+  if (w.kn.bwdd_remap && ntn == 1 && R >= 2) {
+    rm.on = 1;
+    rm.Z = w.Z;
+    rm.R = R;
+    rm.seg = (R + 1) / 2;
+    rm.NS = wv.n * w.Z * 2;
+    grid = dim3((unsigned)(8 * ((rm.NS + 7) / 8) * rm.seg), 1, 1);
+  }
   const float* dh = KEPT ? w.dh : w.Gs;  // unread unless KEPT
   if (w.drop.lstm()) {
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, Cfg, KEPT, true><<<grid, Cfg::NTH, 0, s>>>(
                               w.Gs, w.dG, dh, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride,
-                              wv, d.L, d.T, w.M, w.drop));
+                              wv, d.L, d.T, w.M, w.drop, rm));
   } else {
     SMAML_DISPATCH_H(d.H, k_lstm_bwd_dual<HT, Cfg, KEPT, false><<<grid, Cfg::NTH, 0, s>>>(
                               w.Gs, w.dG, dh, w.RGs, w.Cs, w.RCs, w.dH, w.RdH, w.dc, w.Rdc, lsz, theta, U, tstride,
-                              wv, d.L, d.T, w.M, w.drop));
+                              wv, d.L, d.T, w.M, w.drop, rm));
   }
 }
 
