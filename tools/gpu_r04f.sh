@@ -2,9 +2,14 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu "tests/test_gpu_api.py::test_wgrad_variants_match" > gpurun_out/r04f_pytest.log 2>&1 || { tail -30 gpurun_out/r04f_pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu "tests/test_gpu_api.py::test_wgrad_variants_match" "tests/test_gpu_api.py::test_order_only_knobs_bitwise" > gpurun_out/r04f_pytest.log 2>&1 || { tail -30 gpurun_out/r04f_pytest.log; exit 1; }
 tail -1 gpurun_out/r04f_pytest.log
-timeout -k 10 900 python -u tools/ab_run.py gpurun_out/r04f_ab.log 1 ws=libsmaml.so wsoff=libsmaml.so:SMAML_OPTIONS=wgrad_ws=0 || exit 1
+timeout -k 10 900 python -u tools/ab_run.py gpurun_out/r04f_ab.log 1 ws=libsmaml.so wsoff=libsmaml.so:SMAML_OPTIONS=wgrad_ws=0 remap=libsmaml.so:SMAML_OPTIONS=wgrad_ws=0,bwdd_remap=1 || exit 1
 BA="--steps 1 --warmup 0 --cpu-sample-steps 0 --no-timing --adapt-epochs 0 --cfg5-share-tasks 0"
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA --kernel-include-regex "k_wgrad" -f csv -d gpurun_out/r04f_pmc_ws -o run -- python bench.py $BA > gpurun_out/r04f_pmc_ws.log 2>&1
 echo "pmc rc=$?"
+for v in off:bwdd_remap=0 on:bwdd_remap=1; do
+  n=${v%%:*}; o=${v#*:}
+  SMAML_OPTIONS=wgrad_ws=0,$o timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_lstm_bwd_dual" -f csv -d gpurun_out/r04f_fetch_$n -o run -- python bench.py $BA > gpurun_out/r04f_fetch_$n.log 2>&1
+  echo "fetch $n rc=$?"
+done
