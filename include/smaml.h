@@ -112,6 +112,23 @@ int smaml_set_task_ids(smaml_ctx* ctx, const int32_t* ids_host, int32_t n);
 int smaml_gcn_conv(smaml_ctx* ctx, void* stream, const float* x, int32_t rows, int32_t cin,
                    const float* weight, const float* bias, int32_t cout, float* out);
 
+/* GCNConv / Linear forward and backward for the module API's autograd (model.py:7-52: STGCN trained on
+ * its own; the hybrid path keeps the GCN frozen, F2). flags: SMAML_GCN_RELU applies ReLU to the output,
+ * SMAML_GCN_PLAIN skips the graph aggregation (a plain x W^T + b, e.g. STGCN.output_layer). */
+#define SMAML_GCN_RELU 1
+#define SMAML_GCN_PLAIN 2
+int smaml_gcn_conv_ex(smaml_ctx* ctx, void* stream, const float* x, int32_t rows, int32_t cin,
+                      const float* weight, const float* bias, int32_t cout, int32_t flags, float* out);
+
+/* Backward of z = A_hat x W^T + b (SMAML_GCN_PLAIN: A_hat = I) given dz = dL/dz [rows][cout]:
+ * dx = A_hat^T dz W [rows][cin] (optional), dwb = [dL/dW (cout x cin, row-major) | dL/db (cout)]
+ * (optional). Deterministic (fixed-order sums). Replaces autograd through PyG GCNConv / nn.Linear. */
+int smaml_gcn_conv_backward(smaml_ctx* ctx, void* stream, const float* x, int32_t rows, int32_t cin,
+                            const float* weight, int32_t cout, const float* dz, int32_t flags, float* dx, float* dwb);
+
+/* g *= (h > 0) over n elements: the ReLU derivative from the post-activation h (F.relu's backward). */
+int smaml_relu_mask(smaml_ctx* ctx, void* stream, float* g, const float* h, int64_t n);
+
 /* HybridSTGCN_LSTM.forward(x, edge_index) (hybrid_model.py:80-117) for `nsamples` samples:
  * x_host[s] = device pointer to sample s's x [T*N, input_channels] (time-major rows);
  * pred [nsamples][N*Hf][C] (rows n*Hf + h); feats (optional) [nsamples][T*N][Hc] = the

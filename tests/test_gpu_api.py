@@ -314,12 +314,12 @@ def test_stgcn_forward_matches_reference(golden_dir, i):
     x, _ = synth.sample_xy(synth.make_features(int(z["feat_seed"]), d.num_nodes, synth.t_total_for(1)), 0)
     xg = torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
     eig = torch.from_numpy(z[f"d{i}/edge_index"]).to("cuda:0")
-    out = base(xg, eig).cpu().numpy()
+    out = base(xg, eig).detach().cpu().numpy()
     assert out.shape == z[f"d{i}/out"].shape
     assert rel(out, z[f"d{i}/out"]) < 1e-5
     base.train()
     torch.manual_seed(3)
-    out_t = base(xg, eig).cpu()
+    out_t = base(xg, eig).detach().cpu()
     torch.manual_seed(3)
     drop = refcpu.Dropout(draw_dropout_seed(), 0.2, 0.0, 0, 0)
     ref = refcpu.stgcn_forward(torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(z[f"d{i}/edge_index"]),
@@ -450,6 +450,48 @@ def test_wgrad_variants_match(knob):
         del ml
     np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-6)
     assert rel(out[0][1], out[1][1]) < 1e-6
+
+
+@pytest.mark.parametrize("d", [CONFIG1, CONFIG2], ids=["cfg1", "cfg2"])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_stgcn_autograd_matches_oracle(d, p):
+    """STGCN trained on its own (model.py:30-52 as an ordinary differentiable module): the HIP path's
+    forward and backward (_STGCNFn: conv + ReLU x4 with train-mode dropout, the head; backward through
+    smaml_gcn_conv_backward / smaml_relu_mask / the replayed masks) against torch autograd through the
+    oracle's STGCN (refcpu.stgcn_forward, PyG gcn_norm restated) with the same masks: loss, the output,
+    the gradient of every parameter and of the input x."""
+    from weatherforecast_stgcn_maml_amd.hybrid_model import draw_dropout_seed
+    from weatherforecast_stgcn_maml_amd.model import STGCN
+
+    P = synth.init_params(53, d, gcn_bias_scale=0.1)
+    base = STGCN(d.input_channels, d.hidden_channels, d.output_channels, d.window_size, d.forecast_horizon,
+                 dropout_rate=p)
+    base.load_state_dict({k[len("base_stgcn."):]: torch.from_numpy(v) for k, v in P.items()
+                          if k.startswith("base_stgcn.")})
+    base = base.to(DEV).train()
+    x, _ = synth.sample_xy(synth.make_features(5300, d.num_nodes, synth.t_total_for(1)), 0)
+    ei = grid_edges(d)
+    rng = np.random.default_rng(7)
+    R = rng.standard_normal((d.num_nodes * d.forecast_horizon, d.output_channels)).astype(np.float32)
+    xg = torch.from_numpy(np.ascontiguousarray(x)).to(DEV).requires_grad_(True)
+    torch.manual_seed(11)
+    out = base(xg, torch.from_numpy(ei).to(DEV))
+    assert out.grad_fn is not None
+    (out * torch.from_numpy(R).to(DEV)).sum().backward()
+    # oracle: the same masks (the module draws its seed from torch's RNG)
+    torch.manual_seed(11)
+    drop = refcpu.Dropout(draw_dropout_seed(), p, 0.0, 0, 0) if p > 0.0 else None
+    Pt = {k: v.clone().requires_grad_(True) for k, v in refcpu.to_torch(P).items() if k.startswith("base_stgcn.")}
+    xt = torch.from_numpy(np.ascontiguousarray(x)).clone().requires_grad_(True)
+    ref = refcpu.stgcn_forward(xt, torch.from_numpy(ei).long(), Pt, d, drop)
+    (ref * torch.from_numpy(R)).sum().backward()
+    assert rel(out.detach().cpu(), ref.detach()) < 1e-5
+    sd = dict(base.named_parameters())
+    for k, v in Pt.items():
+        g = sd[k[len("base_stgcn."):]].grad
+        assert g is not None, k
+        assert rel(g.cpu(), v.grad) < 1e-4, (k, rel(g.cpu(), v.grad))
+    assert rel(xg.grad.cpu(), xt.grad) < 1e-4
 
 
 @pytest.mark.parametrize("knob", ["bwdd_remap"])

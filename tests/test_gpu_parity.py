@@ -80,6 +80,8 @@ def test_forward_matches_reference(golden_dir, d, name):
 
 
 def test_gcnconv_dropin_matches_oracle():
+    """PyG GCNConv drop-in, forward and (round 4) backward, against the oracle's restatement run through
+    torch autograd (the t = 0 block aggregates, later rows see only their self loop, F3)."""
     from weatherforecast_stgcn_maml_amd.model import GCNConv
 
     torch.manual_seed(0)
@@ -90,9 +92,21 @@ def test_gcnconv_dropin_matches_oracle():
         with torch.no_grad():
             conv.bias.uniform_(-0.1, 0.1)
         x = torch.randn(rows, cin)
-        ref = refcpu.gcn_conv(x, torch.from_numpy(ei), conv.lin.weight.detach(), conv.bias.detach())
-        out = conv.to(DEV)(x.to(DEV), torch.from_numpy(ei).to(DEV)).cpu()
-        assert rel(out.numpy(), ref.numpy()) < 1e-5
+        W = conv.lin.weight.detach().clone().requires_grad_(True)
+        b = conv.bias.detach().clone().requires_grad_(True)
+        xr = x.clone().requires_grad_(True)
+        ref = refcpu.gcn_conv(xr, torch.from_numpy(ei), W, b)
+        R = torch.randn(rows, cout)
+        (ref * R).sum().backward()
+        conv = conv.to(DEV)
+        xg = x.to(DEV).requires_grad_(True)
+        out = conv(xg, torch.from_numpy(ei).to(DEV))
+        assert rel(out.detach().cpu().numpy(), ref.detach().numpy()) < 1e-5
+        # backward on the HIP path (smaml_gcn_conv_backward: A_hat^T dz W, dz^T A_hat x, sum dz)
+        (out * R.to(DEV)).sum().backward()
+        assert rel(conv.lin.weight.grad.cpu(), W.grad) < 1e-5
+        assert rel(conv.bias.grad.cpu(), b.grad) < 1e-5
+        assert rel(xg.grad.cpu(), xr.grad) < 1e-5
 
 
 # ----------------------------------------------------------------------------- reference mode

@@ -53,7 +53,7 @@ static std::vector<int64_t> grid_edges(int side) {
 }
 
 int main() {
-  CHECK(smaml_abi_version() == 5);
+  CHECK(smaml_abi_version() == 6);
   CHECK(smaml_build_info() != nullptr && std::strlen(smaml_build_info()) > 0);
 
   // ---- parameter layout (hybrid_model.py state_dict order) ----

@@ -23,9 +23,10 @@ EXPORTS = (
     "smaml_backward", "smaml_gcn_forward", "smaml_lstm_forward", "smaml_lstm_backward", "smaml_head_loss",
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
     "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy", "smaml_variant_counts", "smaml_set_option",
-    "smaml_dropout", "smaml_sync",
+    "smaml_dropout", "smaml_sync", "smaml_gcn_conv_ex", "smaml_gcn_conv_backward", "smaml_relu_mask",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
+GCN_RELU, GCN_PLAIN = 1, 2  # smaml_gcn_conv_ex / _backward flags
 
 # kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
 VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kept", "fwd_dual_img", "bwd_big", "bwd_small", "bwd_split",
@@ -109,6 +110,9 @@ _SIGS = {
     "smaml_set_option": ([P, ctypes.c_char_p, I64], I32),
     "smaml_dropout": ([P, P, P, I64, F32, ctypes.c_uint32, I32], I32),
     "smaml_sync": ([P, P], I32),
+    "smaml_gcn_conv_ex": ([P, P, P, I32, I32, P, P, I32, I32, P], I32),
+    "smaml_gcn_conv_backward": ([P, P, P, I32, I32, P, I32, P, I32, P, P], I32),
+    "smaml_relu_mask": ([P, P, P, P, I64], I32),
 }
 
 
@@ -249,6 +253,19 @@ class Context:
     def gcn_conv(self, stream, x, weight, bias, out):
         check(self._L.smaml_gcn_conv(self._h, stream, ptr(x), x.shape[0], x.shape[1], ptr(weight),
                                      ptr(bias), weight.shape[0], ptr(out)))
+
+    def gcn_conv_ex(self, stream, x, weight, bias, out, flags=0):
+        check(self._L.smaml_gcn_conv_ex(self._h, stream, ptr(x), x.shape[0], x.shape[1], ptr(weight), ptr(bias),
+                                        weight.shape[0], int(flags), ptr(out)))
+
+    def gcn_conv_backward(self, stream, x, weight, dz, dx=None, dwb=None, flags=0):
+        check(self._L.smaml_gcn_conv_backward(self._h, stream, ptr(x), x.shape[0], x.shape[1], ptr(weight),
+                                              weight.shape[0], ptr(dz), int(flags),
+                                              ptr(dx) if dx is not None else None,
+                                              ptr(dwb) if dwb is not None else None))
+
+    def relu_mask(self, stream, g, h):
+        check(self._L.smaml_relu_mask(self._h, stream, ptr(g), ptr(h), g.numel()))
 
     def forward(self, stream, theta, xs, pred, feats=None):
         arr = (P * len(xs))(*[ptr(x) for x in xs])

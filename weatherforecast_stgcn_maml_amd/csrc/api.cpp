@@ -204,6 +204,12 @@ struct smaml_ctx {
   int device = 0;
   int32_t* ell_c = nullptr;
   float* ell_v = nullptr;
+  // A_hat^T as CSR (GCNConv backward's aggregation of the t = 0 rows; built with the ELL)
+  int32_t *tr_p = nullptr, *tr_c = nullptr;
+  float* tr_v = nullptr;
+  int64_t tr_nnz_cap = 0;
+  float* bw_scratch = nullptr;  // GCNConv backward: [rows][max(cin, cout)] x 2
+  int64_t bw_scratch_cap = 0;
   const float* gcn = nullptr;
   // workspace
   char* arena = nullptr;
@@ -883,7 +889,7 @@ extern "C" {
 
 const char* smaml_last_error(void) { return g_err.c_str(); }
 
-int32_t smaml_abi_version(void) { return 5; }
+int32_t smaml_abi_version(void) { return 6; }
 
 const char* smaml_build_info(void) { return smaml::products_info(); }
 
@@ -977,6 +983,10 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->arena) (void)hipFree(c->arena);
   if (c->ell_c) (void)hipFree(c->ell_c);
   if (c->ell_v) (void)hipFree(c->ell_v);
+  if (c->tr_p) (void)hipFree(c->tr_p);
+  if (c->tr_c) (void)hipFree(c->tr_c);
+  if (c->tr_v) (void)hipFree(c->tr_v);
+  if (c->bw_scratch) (void)hipFree(c->bw_scratch);
   if (c->xtab) (void)hipFree((void*)c->xtab);
   (void)c->stage.release();
   if (c->scratch_loss) (void)hipFree(c->scratch_loss);
@@ -1014,6 +1024,40 @@ int smaml_set_graph(smaml_ctx* c, const int64_t* edge_index_host, int64_t num_ed
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(c->ell_c, cols.data(), cols.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->ell_v, vals.data(), vals.size() * 4, hipMemcpyHostToDevice));
+  // A_hat^T as CSR: entry (t, e) of the ELL (row t gathers column cols[t][e] with weight vals[t][e])
+  // becomes row cols[t][e] of the transpose, in ascending t (fixed order)
+  const int N = c->d.N;
+  std::vector<int32_t> tp(N + 1, 0), tc;
+  std::vector<float> tv;
+  for (int t = 0; t < N; ++t)
+    for (int e = 0; e < ELLW; ++e)
+      if (vals[(size_t)t * ELLW + e] != 0.f) ++tp[cols[(size_t)t * ELLW + e] + 1];
+  for (int i = 0; i < N; ++i) tp[i + 1] += tp[i];
+  tc.resize(tp[N]);
+  tv.resize(tp[N]);
+  std::vector<int32_t> pos(tp.begin(), tp.end() - 1);
+  for (int t = 0; t < N; ++t)
+    for (int e = 0; e < ELLW; ++e) {
+      const float v = vals[(size_t)t * ELLW + e];
+      if (v == 0.f) continue;
+      const int j = cols[(size_t)t * ELLW + e];
+      tc[pos[j]] = t;
+      tv[pos[j]] = v;
+      ++pos[j];
+    }
+  if (!c->tr_p) HIP_TRY(hipMalloc((void**)&c->tr_p, (size_t)(N + 1) * 4));
+  if ((int64_t)tc.size() > c->tr_nnz_cap) {
+    if (c->tr_c) HIP_TRY(hipFree(c->tr_c));
+    if (c->tr_v) HIP_TRY(hipFree(c->tr_v));
+    c->tr_nnz_cap = std::max<int64_t>((int64_t)tc.size(), 1);
+    HIP_TRY(hipMalloc((void**)&c->tr_c, c->tr_nnz_cap * 4));
+    HIP_TRY(hipMalloc((void**)&c->tr_v, c->tr_nnz_cap * 4));
+  }
+  HIP_TRY(hipMemcpy(c->tr_p, tp.data(), tp.size() * 4, hipMemcpyHostToDevice));
+  if (!tc.empty()) {
+    HIP_TRY(hipMemcpy(c->tr_c, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->tr_v, tv.data(), tv.size() * 4, hipMemcpyHostToDevice));
+  }
   return SMAML_OK;
 }
 
@@ -1063,6 +1107,81 @@ int smaml_gcn_conv(smaml_ctx* c, void* stream, const float* x, int32_t rows, int
   hipStream_t s = (hipStream_t)stream;
   launch_gcn_layer(s, c->d, 0, 1, 1, nullptr, x, out, false, false, weight, bias, cin, cout, c->ell_c, c->ell_v,
                    rows, std::min(rows, c->d.N));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_gcn_conv_ex(smaml_ctx* c, void* stream, const float* x, int32_t rows, int32_t cin, const float* weight,
+                      const float* bias, int32_t cout, int32_t flags, float* out) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  const bool plain = (flags & SMAML_GCN_PLAIN) != 0, relu = (flags & SMAML_GCN_RELU) != 0;
+  if (!plain && !c->ell_c) return fail(SMAML_ESTATE, "smaml_set_graph not called");
+  if (!x || !weight || !bias || !out || rows <= 0 || cin <= 0 || cout <= 0 || (flags & ~3))
+    return fail(SMAML_EINVAL, "bad gcn_conv_ex arguments");
+  if (cin % 4) return fail(SMAML_EINVAL, "cin must be a multiple of 4");
+  if (!aligned16(x) || !aligned16(weight)) return fail(SMAML_EINVAL, "x / weight must be 16-byte aligned");
+  TRY(ensure_device(c));
+  TRY(check_device_error(c));
+  hipStream_t s = (hipStream_t)stream;
+  launch_gcn_layer(s, c->d, 0, 1, 1, nullptr, x, out, false, relu, weight, bias, cin, cout, c->ell_c, c->ell_v, rows,
+                   plain ? 0 : std::min(rows, c->d.N));
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_gcn_conv_backward(smaml_ctx* c, void* stream, const float* x, int32_t rows, int32_t cin,
+                            const float* weight, int32_t cout, const float* dz, int32_t flags, float* dx, float* dwb) {
+  if (!c) return fail(SMAML_EINVAL, "ctx is NULL");
+  const bool plain = (flags & SMAML_GCN_PLAIN) != 0;
+  if (!plain && !c->ell_c) return fail(SMAML_ESTATE, "smaml_set_graph not called");
+  if (!x || !weight || !dz || rows <= 0 || cin <= 0 || cout <= 0 || (flags & ~SMAML_GCN_PLAIN) || (!dx && !dwb))
+    return fail(SMAML_EINVAL, "bad gcn_conv_backward arguments");
+  if (cin % 4 || cout % 4) return fail(SMAML_EINVAL, "cin and cout must be multiples of 4");
+  if (!aligned16(x) || !aligned16(weight) || !aligned16(dz) || (dx && !aligned16(dx)))
+    return fail(SMAML_EINVAL, "x / weight / dz / dx must be 16-byte aligned");
+  TRY(ensure_device(c));
+  TRY(check_device_error(c));
+  TRY(reserve(c, 1, 1));  // the split-K partial slabs of the weight gradient
+  hipStream_t s = (hipStream_t)stream;
+  const int ng = plain ? 0 : std::min(rows, c->d.N);
+  const int64_t need = 2 * (int64_t)rows * std::max(cin, cout);
+  if (need > c->bw_scratch_cap) {
+    if (c->bw_scratch) HIP_TRY(hipFree(c->bw_scratch));
+    HIP_TRY(hipMalloc((void**)&c->bw_scratch, need * 4));
+    c->bw_scratch_cap = need;
+  }
+  float* t0 = c->bw_scratch;
+  float* t1 = c->bw_scratch + (int64_t)rows * std::max(cin, cout);
+  if (dwb) {
+    // dW = dz^T (A_hat x), db = sum_rows dz: the split-K weight-gradient GEMM with its bias column
+    const float* ax = x;
+    if (ng > 0) {
+      launch_gather_rows(s, x, t0, rows, cin, ng, c->ell_c, c->ell_v, nullptr, nullptr, nullptr);
+      ax = t0;
+    }
+    Work w = c->w;
+    w.Z = 1;
+    w.drop = Drop{};
+    launch_wgrad(s, c->d, w, dz, 0, cout, ax, 0, cin, nullptr, 0, 0, rows, 0, dwb, 0, 0, 0,
+                 (int64_t)cout * cin, -1, true, false);
+  }
+  if (dx) {
+    // dx = A_hat^T (dz W): the rows past the graph's nodes see only their self loop
+    if (ng > 0) {
+      launch_gemm_nn_plain(s, dz, rows, cout, weight, cin, t1);
+      launch_gather_rows(s, t1, dx, rows, cin, ng, nullptr, nullptr, c->tr_p, c->tr_c, c->tr_v);
+    } else {
+      launch_gemm_nn_plain(s, dz, rows, cout, weight, cin, dx);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_relu_mask(smaml_ctx* c, void* stream, float* g, const float* h, int64_t n) {
+  if (!c || !g || !h || n <= 0) return fail(SMAML_EINVAL, "bad relu_mask arguments");
+  TRY(ensure_device(c));
+  launch_relu_mask((hipStream_t)stream, g, h, n);
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }

@@ -428,6 +428,12 @@ hipError_t launch_inner_sgd(hipStream_t s, float* theta, const float* g, int64_t
 hipError_t launch_sweep_update(hipStream_t s, float* V, const float* X, float alpha, const float* G, int64_t P, int Z,
                                double* part, const float* norms, const float* coefs, float max_norm, float* U,
                                const BarPlan& bp);
+// ---- GCNConv backward helpers (module API autograd; kernels.hip) ----
+// out[r] = sum_adj w * src[col] for r < n_gather (ELL when csr_p is null, else CSR), src[r] otherwise
+void launch_gather_rows(hipStream_t s, const float* src, float* out, int rows, int cols, int n_gather, const int* ell_c,
+                        const float* ell_v, const int* csr_p, const int* csr_c, const float* csr_v);
+void launch_relu_mask(hipStream_t s, float* g, const float* h, int64_t n);  // g *= (h > 0)
+void launch_gemm_nn_plain(hipStream_t s, const float* A, int rows, int K, const float* W, int ncols, float* out);
 void launch_sum_tasks(hipStream_t s, const float* g, int64_t P, int Z, float* out);
 void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float* out);
 void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,

@@ -2247,6 +2247,63 @@ void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int 
 }
 
 // ====================================================================================
+// GCNConv backward helpers (the module API's STGCN / GCNConv autograd, model.py:7-52; off the hybrid
+// hot path, where the GCN is frozen). Row gather: out[r] = sum over the adjacency list of row r of
+// w * src[col] for r < n_gather (the ELL of A_hat for the forward aggregation, or the CSR of A_hat^T
+// for the backward one), out[r] = src[r] for the other rows. One float4 of one row per thread, fixed
+// summation order (deterministic).
+__global__ void k_gather_rows(const float* __restrict__ src, float* __restrict__ out, int rows, int cols,
+                              int n_gather, const int* __restrict__ ell_c, const float* __restrict__ ell_v,
+                              const int* __restrict__ csr_p, const int* __restrict__ csr_c,
+                              const float* __restrict__ csr_v) {
+  const int q4 = cols / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * q4) return;
+  const int r = (int)(i / q4), k = 4 * (int)(i - (int64_t)r * q4);
+  float4 v;
+  if (r < n_gather) {
+    v = f4zero();
+    if (csr_p) {
+      for (int e = csr_p[r]; e < csr_p[r + 1]; ++e) v = fma4(csr_v[e], ld4(src + (int64_t)csr_c[e] * cols + k), v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < ELLW; ++e) {
+        const float wv = ell_v[r * ELLW + e];
+        if (wv != 0.f) v = fma4(wv, ld4(src + (int64_t)ell_c[r * ELLW + e] * cols + k), v);
+      }
+    }
+  } else {
+    v = ld4(src + (int64_t)r * cols + k);
+  }
+  st4(out + (int64_t)r * cols + k, v);
+}
+
+void launch_gather_rows(hipStream_t s, const float* src, float* out, int rows, int cols, int n_gather, const int* ell_c,
+                        const float* ell_v, const int* csr_p, const int* csr_c, const float* csr_v) {
+  const int64_t n = (int64_t)rows * (cols / 4);
+  k_gather_rows<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, out, rows, cols, n_gather, ell_c, ell_v, csr_p,
+                                                            csr_c, csr_v);
+}
+
+// g *= (h > 0): the ReLU derivative taken from the (post-ReLU, post-dropout) activation h
+__global__ void k_relu_mask(float* __restrict__ g, const float* __restrict__ h, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    g[i] = h[i] > 0.f ? g[i] : 0.f;
+}
+
+void launch_relu_mask(hipStream_t s, float* g, const float* h, int64_t n) {
+  int nb = (int)((n + 255) / 256);
+  if (nb > 4096) nb = 4096;
+  k_relu_mask<<<nb, 256, 0, s>>>(g, h, n);
+}
+
+// out = A . W  (A [rows][K] row-major, W [K][ncols] row-major): k_gemm_nn on one problem
+void launch_gemm_nn_plain(hipStream_t s, const float* A, int rows, int K, const float* W, int ncols, float* out) {
+  dim3 grid((rows + CfgNN::BM - 1) / CfgNN::BM, (ncols + CfgNN::BN - 1) / CfgNN::BN, 1);
+  k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(A, 0, rows, K, W, 0, 0, ncols, out, 0);
+}
+
+// ====================================================================================
 // clip_grad_norm_ + SGD, per task z. Squared norm accumulated in fp64, fixed order.
 __global__ void k_sqsum(const float* __restrict__ g, int64_t P, double* __restrict__ part) {
   __shared__ double red[NT / 64];

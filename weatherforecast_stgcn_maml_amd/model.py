@@ -94,7 +94,8 @@ class GCNConv(nn.Module):
         self.lin = _Linear(in_channels, out_channels)
         self.bias = nn.Parameter(torch.zeros(out_channels))
 
-    def forward(self, x, edge_index):
+    def graph_context(self, x, edge_index):
+        """The library context this conv runs in for ``edge_index`` (graph uploaded once per tensor)."""
         memo = self.__dict__.setdefault("_ei_memo", _GraphMemo())
         n_graph = memo.get(edge_index)
         if n_graph is None:  # first call with this edge_index (or it changed): one host sync
@@ -105,7 +106,13 @@ class GCNConv(nn.Module):
                          lstm_num_layers=1, forecast_horizon=1, output_channels=1)
         ctx = _context(dims, x.device)
         _set_graph(ctx, edge_index)
+        return ctx
+
+    def forward(self, x, edge_index):
+        ctx = self.graph_context(x, edge_index)
         x = x.contiguous().float()
+        if torch.is_grad_enabled() and (x.requires_grad or self.lin.weight.requires_grad or self.bias.requires_grad):
+            return _GCNConvFn.apply(x, ctx, self.lin.weight, self.bias)
         out = torch.empty(x.shape[0], self.out_channels, device=x.device, dtype=torch.float32)
         ctx.gcn_conv(_capi.stream_ptr(torch), x, self.lin.weight.detach().contiguous(),
                      self.bias.detach().contiguous(), out)
@@ -113,6 +120,88 @@ class GCNConv(nn.Module):
 
     def __repr__(self):
         return f"GCNConv({self.in_channels}, {self.out_channels})"
+
+
+class _GCNConvFn(torch.autograd.Function):
+    """out = A_hat x W^T + b with its backward on the HIP path (smaml_gcn_conv_backward): dx = A_hat^T dz W,
+    dW = dz^T (A_hat x), db = sum dz (PyG GCNConv's autograd, model.py:23-26)."""
+
+    @staticmethod
+    def forward(fctx, x, lib_ctx, weight, bias):
+        w = weight.detach().contiguous()
+        out = torch.empty(x.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
+        lib_ctx.gcn_conv(_capi.stream_ptr(torch), x, w, bias.detach().contiguous(), out)
+        fctx.save_for_backward(x, w)
+        fctx.lib_ctx = lib_ctx
+        return out
+
+    @staticmethod
+    def backward(fctx, gout):
+        x, w = fctx.saved_tensors
+        dz = gout.contiguous().float()
+        need_x = fctx.needs_input_grad[0]
+        dx = torch.empty_like(x) if need_x else None
+        dwb = torch.empty(w.numel() + w.shape[0], device=x.device, dtype=torch.float32)
+        fctx.lib_ctx.gcn_conv_backward(_capi.stream_ptr(torch), x, w, dz, dx=dx, dwb=dwb)
+        return dx, None, dwb[:w.numel()].view_as(w), dwb[w.numel():]
+
+
+class _STGCNFn(torch.autograd.Function):
+    """STGCN.forward (model.py:30-52) on the HIP path with its backward: conv1..conv4 + ReLU
+    (smaml_gcn_conv_ex), train-mode dropout after each (smaml_dropout, counter-based masks), the last
+    time block through output_layer (smaml_gcn_conv_ex without aggregation). The backward replays the
+    masks on the gradient, applies the ReLU derivative from the saved activations (smaml_relu_mask) and
+    runs smaml_gcn_conv_backward per layer."""
+
+    @staticmethod
+    def forward(fctx, x, convs, ctxs, dctx, p, seed, num_nodes, *params):
+        st = _capi.stream_ptr(torch)
+        hs = [x]
+        h = x
+        for k in range(4):
+            w, b = params[2 * k].detach().contiguous(), params[2 * k + 1].detach().contiguous()
+            out = torch.empty(h.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
+            ctxs[k].gcn_conv_ex(st, h, w, b, out, flags=_capi.GCN_RELU)
+            if p > 0.0:
+                dctx.dropout(st, out, p, seed, k)
+            hs.append(out)
+            h = out
+        wo, bo = params[8].detach().contiguous(), params[9].detach().contiguous()
+        last = h[-num_nodes:]
+        out = torch.empty(num_nodes, wo.shape[0], device=x.device, dtype=torch.float32)
+        ctxs[3].gcn_conv_ex(st, last, wo, bo, out, flags=_capi.GCN_PLAIN)
+        fctx.save_for_backward(*hs)
+        fctx.ctxs, fctx.dctx, fctx.p, fctx.seed, fctx.num_nodes = ctxs, dctx, p, seed, num_nodes
+        fctx.ws = [params[2 * k].detach().contiguous() for k in range(4)] + [wo]
+        return out
+
+    @staticmethod
+    def backward(fctx, gout):
+        st = _capi.stream_ptr(torch)
+        hs = fctx.saved_tensors
+        N, ctxs, ws = fctx.num_nodes, fctx.ctxs, fctx.ws
+        grads = [None] * 10
+        h4 = hs[4]
+        wo = ws[4]
+        dwb = torch.empty(wo.numel() + wo.shape[0], device=h4.device, dtype=torch.float32)
+        dlast = torch.empty(N, h4.shape[1], device=h4.device, dtype=torch.float32)
+        ctxs[3].gcn_conv_backward(st, h4[-N:], wo, gout.contiguous().float(), dx=dlast, dwb=dwb,
+                                  flags=_capi.GCN_PLAIN)
+        grads[8], grads[9] = dwb[:wo.numel()].view_as(wo), dwb[wo.numel():]
+        g = torch.zeros_like(h4)
+        g[-N:] = dlast
+        need_x = fctx.needs_input_grad[0]
+        for k in range(3, -1, -1):
+            if fctx.p > 0.0:
+                fctx.dctx.dropout(st, g, fctx.p, fctx.seed, k)  # same masks: d dropout(y) = dropout(d)
+            ctxs[k].relu_mask(st, g, hs[k + 1])
+            w = ws[k]
+            dwb = torch.empty(w.numel() + w.shape[0], device=h4.device, dtype=torch.float32)
+            dx = torch.empty_like(hs[k]) if (k > 0 or need_x) else None
+            ctxs[k].gcn_conv_backward(st, hs[k], w, g, dx=dx, dwb=dwb)
+            grads[2 * k], grads[2 * k + 1] = dwb[:w.numel()].view_as(w), dwb[w.numel():]
+            g = dx
+        return (g if need_x else None, None, None, None, None, None, None, *grads)
 
 
 def _any_context(device):
@@ -126,7 +215,9 @@ class STGCN(nn.Module):
     node features through ``output_layer`` as the reference does (model.py:44-52); in
     ``train()`` mode it applies ``self.dropout`` after each of the four conv + ReLU layers
     (model.py:33,36,39,42) with the library's counter-based masks, a fresh seed per call drawn
-    from the global torch RNG. Forward only (no autograd through the HIP GCN)."""
+    from the global torch RNG. With grad enabled it is differentiable (``_STGCNFn``: every conv, the
+    ReLUs, the dropout masks and the head run forward and backward in libsmaml), so STGCN trains on
+    its own as the reference module does; under no_grad the forward-only path runs."""
 
     def __init__(self, in_channels, hidden_channels, out_channels=12, window_size=6,
                  forecast_horizon=1, dropout_rate=0.3):
@@ -142,12 +233,27 @@ class STGCN(nn.Module):
         self.dropout = nn.Dropout(p=dropout_rate)
         self.output_layer = nn.Linear(hidden_channels, out_channels * forecast_horizon)
 
+    def _params(self):
+        out = []
+        for conv in (self.conv1, self.conv2, self.conv3, self.conv4):
+            out += [conv.lin.weight, conv.bias]
+        return out + [self.output_layer.weight, self.output_layer.bias]
+
     def forward(self, x, edge_index):
         p = float(self.dropout.p) if self.training else 0.0
         if p > 0.0:
             from .hybrid_model import draw_dropout_seed
             seed = draw_dropout_seed()
             dctx = _any_context(x.device)
+        params = self._params()
+        if torch.is_grad_enabled() and (x.requires_grad or any(q.requires_grad for q in params)):
+            x = x.contiguous().float()
+            convs = (self.conv1, self.conv2, self.conv3, self.conv4)
+            ctxs = [cv.graph_context(x, edge_index) for cv in convs]
+            num_nodes = x.shape[0] // self.window_size
+            out = _STGCNFn.apply(x, convs, ctxs, dctx if p > 0.0 else None, p, seed if p > 0.0 else 0, num_nodes,
+                                 *params)
+            return out.view(num_nodes, self.forecast_horizon, self.out_channels).reshape(-1, self.out_channels)
         with torch.no_grad():
             h = x
             for k, conv in enumerate((self.conv1, self.conv2, self.conv3, self.conv4)):
