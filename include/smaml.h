@@ -266,10 +266,11 @@ int smaml_timing(smaml_ctx* ctx, int32_t enable);
 int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* count, int32_t cap);
 
 /* Launch counts per kernel variant (tile configuration) since the last reset, in the order of
- * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_dual, fwd_dual_kept,
- * bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept, bwd_dual_small,
- * bwd_dual_small_kept. Writes min(cap, count) entries, *count = number of variants; reset != 0
- * zeroes them. Host-side counters: no synchronisation. Lets tests assert which configurations ran. */
+ * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
+ * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
+ * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw.
+ * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
+ * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
 
 /* Run-time knobs (tests / A-B; defaults = build-time values):
@@ -295,7 +296,14 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  exits and the next call / smaml_sync returns SMAML_EHIP;
  *   "barrier_oversize":            debug: > 0 launches the grid-barrier kernels with that many
  *                                  times the resident capacity (+1 block), which can never be
- *                                  co-resident, to exercise the bounded wait. */
+ *                                  co-resident, to exercise the bounded wait;
+ *   "wgrad_ws":                    warp-specialised weight-gradient kernel where the shapes allow
+ *                                  (1) or the staged one (0);
+ *   "bwdd_remap":                  tangent BPTT tiles dealt in pair-segment order per XCD (1) or in
+ *                                  hardware order (0; bitwise equal);
+ *   "small_kw":                    small-grid (batch-1) LSTM forward / BPTT diagonals as one launch
+ *                                  with the K reduction split over the waves of a workgroup (1), or
+ *                                  as the split-K part + cell launch pair (0). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -83,11 +83,13 @@ def test_adaptation_matches_reference_adapt_model(golden_dir, region):
         assert rel(got[k].cpu().numpy(), z[f"{tag}/adapted/{k}"]) < 1e-5, k
 
 
-def test_adaptation_n441_matches_oracle():
+@pytest.mark.parametrize("small_kw", [0, 1], ids=["split-k", "kw"])
+def test_adaptation_n441_matches_oracle(small_kw):
     """BASELINE config 4 shapes (N=441, Hc=256, LSTM 4x128, batch-1 steps): 2 epochs over 16
     shuffled training windows + the 4-window validation, against the oracle. Runs the
-    small-grid split-K forward / BPTT steps and the per-window GCN feature cache (the second
-    epoch reads every window's features from it)."""
+    small-grid forward / BPTT steps -- the split-K part + cell launch pairs (small_kw 0) or the
+    one-launch K-split-over-waves kernels (kernels_small.hip, small_kw 1) -- and the per-window GCN
+    feature cache (the second epoch reads every window's features from it)."""
     from weatherforecast_stgcn_maml_amd import _capi
     from weatherforecast_stgcn_maml_amd.config import CONFIG2
 
@@ -98,12 +100,16 @@ def test_adaptation_n441_matches_oracle():
     ei = build_spatial_graph(lats, lons, 4)[0]
     feats = synth.make_features(3200, d.num_nodes, synth.t_total_for(20))
     ctx = _capi.Context(d, 0)
+    ctx.set_option("small_kw", small_kw)
     ctx.variant_counts(reset=True)
     torch.manual_seed(5)
     res = adapt(d, feats, ei, {k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, tr, "Moscow",
                 epochs=2, device="cuda:0", ctx=ctx)
     vc = ctx.variant_counts()
-    assert vc["fwd_split"] > 0 and vc["bwd_split"] > 0, vc
+    if small_kw:
+        assert vc["fwd_kw"] > 0 and vc["bwd_kw"] > 0 and vc["fwd_split"] == 0 and vc["bwd_split"] == 0, vc
+    else:
+        assert vc["fwd_split"] > 0 and vc["bwd_split"] > 0 and vc["fwd_kw"] == 0 and vc["bwd_kw"] == 0, vc
     torch.manual_seed(5)
     PT = refcpu.to_torch(P)
     tr_t, gcn_t = _split(PT)

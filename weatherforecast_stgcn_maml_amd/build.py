@@ -9,7 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = [os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "kernels_dual.hip"),
-           os.path.join(CSRC, "kernels_gcn.hip"), os.path.join(CSRC, "api.cpp")]
+           os.path.join(CSRC, "kernels_gcn.hip"), os.path.join(CSRC, "kernels_small.hip"),
+           os.path.join(CSRC, "api.cpp")]
 HEADERS = [os.path.join(CSRC, "gemm_core.h"), os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "loaders.h"),
            os.path.join(REPO, "include", "smaml.h")]
 OUT = os.path.join(HERE, "libsmaml.so")

@@ -227,7 +227,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, 1, 0};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, 1, 0, SMAML_SMALL_KW};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -1497,6 +1497,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_ws = (int)value;
   } else if (k == "bwdd_remap" && (value == 0 || value == 1)) {
     c->kn.bwdd_remap = (int)value;
+  } else if (k == "small_kw" && (value == 0 || value == 1)) {
+    c->kn.small_kw = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "grid_barrier" && (value == 0 || value == 1)) {

@@ -93,6 +93,8 @@ enum Variant {
   V_WGRAD_WIDE,      // k_wgrad with 256 x 256 tiles (also counted as V_WGRAD)
   V_WGRAD_PAIR,      // k_wgrad summing two problems (tangent weight gradient; also counted as V_WGRAD)
   V_WGRAD_WS,        // k_wgrad_ws, warp-specialised (also counted as V_WGRAD)
+  V_FWD_KW,          // k_lstm_fwd_kw (small grids: K split over the waves of one workgroup)
+  V_BWD_KW,          // k_lstm_bwd_kw (same, BPTT)
   NVAR
 };
 
@@ -121,12 +123,16 @@ struct Knobs {
   int wgrad_pair;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
   int wgrad_ws;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
   int bwdd_remap;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
+  int small_kw;              // 1: small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip)
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
 #endif
 #ifndef SMAML_GCN_FUSED
 #define SMAML_GCN_FUSED 1
+#endif
+#ifndef SMAML_SMALL_KW
+#define SMAML_SMALL_KW 0
 #endif
 #ifndef SMAML_WGRAD_PAIR
 #define SMAML_WGRAD_PAIR 1
@@ -368,6 +374,13 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
                     const ParamOff& po);
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
                           const ParamOff& po);
+// kernels_small.hip: the small-grid (batch-1) forward / BPTT diagonal as one launch with the K
+// reduction split over the waves of a workgroup (used where the split-K pair would run)
+bool small_kw_ok(const Dims& d, const Work& w);
+void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta, int64_t tstride,
+                        const ParamOff& po);
+void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
+                        const ParamOff& po);
 void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, int64_t a_zstride,
                   int Mrows, const float* B1, int64_t b1_zstride, int c1, const float* B2,
                   int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,

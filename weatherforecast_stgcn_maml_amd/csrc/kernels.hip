@@ -677,6 +677,10 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     const int64_t per = (int64_t)gridP.x * gridP.z * CfgGateP::NTH * CfgGateP::WTM * CfgGateP::WTN * 16;
     const int S = small_grid_splits((int64_t)wvP.n * ntmP * ngrpP * w.Z, kmax, CfgGateP::BK, per, w.wpart_floats,
                                     w.kn.split_max);
+    if (S > 1 && small_kw_ok(d, w)) {
+      launch_lstm_fwd_kw(s, d, w, diag, theta, tstride, po);
+      return;
+    }
     if (S > 1) {
       count_variant(w, V_FWD_SPLIT);
       dim3 gp(gridP.x, S, gridP.z);
@@ -1444,6 +1448,10 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
       constexpr int64_t PER = CfgNNs::WTM * CfgNNs::WTN * 16 * CfgNNs::NTH;
       const int S = small_grid_splits((int64_t)grid.x * ntns * w.Z, 8 * d.H, CfgNNs::BK,
                                       (int64_t)grid.x * ntns * w.Z * PER, w.wpart_floats, w.kn.split_max);
+      if (S > 1 && small_kw_ok(d, w)) {
+        launch_lstm_bwd_kw(s, d, w, e, theta, tstride, po);
+        return;
+      }
       if (S > 1) {
         count_variant(w, V_BWD_SPLIT);
         dim3 gp(grid.x, S * ntns, w.Z);

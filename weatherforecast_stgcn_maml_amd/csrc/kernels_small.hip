@@ -1,0 +1,384 @@
+// Batch-1 wavefront steps (config 4's regional adaptation, adapt_hybrid_v5.py:186-208; eval and any
+// launch too small to fill the chip): the LSTM forward step (hybrid_model.py:93-102, nn.LSTM gates
+// [i,f,g,o]) and the BPTT step of one anti-diagonal, each ONE launch with the K reduction split over
+// the waves of a workgroup.
+//
+// At M = 441 sequences a diagonal holds <= 4 problems x 14 row tiles x 4 unit groups of work, and
+// its time is one tile's latency chain, not throughput. The split-K pair it replaces
+// (k_lstm_*_part + k_lstm_*_cell_q, kernels.hip) spreads a tile's K over S workgroups on S CUs and
+// pays a second launch plus a partial-slab round trip through L2 per diagonal. Here one workgroup of
+// KW_W waves owns a 32-row tile; wave w accumulates the w-th contiguous K-tile range with its operands
+// loaded from global memory straight into MFMA fragments (no wave shares an operand with another,
+// so there is no LDS staging and no barrier in the K loop), the KW_W partial tiles meet in LDS and
+// are summed in wave order (deterministic), and the workgroup runs the cell epilogue. The
+// epilogue's own operands (bias sums, c_{t-1}; gates, carry, head dh in the BPTT) are loaded before
+// the K loop, so their latency hides under it.
+//
+// Products: bf16x6 (gemm_core.h mfma_x6, f32-accurate). Forward B operand: the pre-split gate
+// images (launch_split_gate) read straight into fragments, or the f32 weights split in registers.
+#include "kernels.h"
+#include "loaders.h"
+
+namespace smaml {
+
+constexpr int KW_W = 8;   // waves per workgroup (two per SIMD)
+constexpr int KW_CH = 2;  // K-tiles per wave whose loads are in flight together (forward)
+constexpr int KW_BCH = 8; // same, BPTT (a K-tile's fragments are 16 VGPRs against the forward's 56)
+
+// Accumulator register r of lane (.., hl) holds tile row (r & 3) + 8 (r >> 2) + 4 hl; the inverse:
+__device__ __forceinline__ int kw_row(int r, int hl) { return (r & 3) + 8 * (r >> 2) + 4 * hl; }
+
+// One gate fragment (8 bf16 per plane) of a pre-split gate image: image row n = g * 32 + jj, chunk h
+// (k = 8h .. 8h + 7), XOR-swizzled by (n >> 3) & 1 (k_split_gate / X6Img<128, KC, 16>).
+__device__ __forceinline__ void img_frag(const char* img, int n, int h, uint4& p0, uint4& p1, uint4& p2) {
+  constexpr int PLANE = 128 * 32;
+  const char* q = img + n * 32 + 16 * (h ^ ((n >> 3) & 1));
+  p0 = *reinterpret_cast<const uint4*>(q);
+  p1 = *reinterpret_cast<const uint4*>(q + PLANE);
+  p2 = *reinterpret_cast<const uint4*>(q + 2 * PLANE);
+}
+
+// Operands of one forward tile's K loop (this lane's row / unit, the two K segments [x | h_{t-1}]).
+struct FwdKw {
+  const float* x;    // x row ar (segment 0, width cin)
+  const float* hp;   // h_{t-1} row ar (segment 1, width H)
+  const float* wih;  // W_ih row (g * H + j) for g = 0 (f32 weights; + g * H * cin per gate)
+  const float* whh;
+  const char* img0;  // gate images of (layer, W_ih), unit group ug (IMG)
+  const char* img1;  // ... W_hh
+  int cin, hl, jj;
+};
+
+// N K-tiles from kt0 on: every load first (no branch between them, so all are in flight together),
+// then the splits and MFMAs in K order.
+template <int H, bool IMG, int N>
+__device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, f32x16 (&acc)[4]) {
+  float4 a[N][2];
+  uint4 bi[N][4][3];
+  float4 bf[N][4][2];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int k = 16 * (kt0 + i);
+    const bool sx = k < o.cin;
+    const int kk = sx ? k : k - o.cin;
+    const float* ap = (sx ? o.x : o.hp) + kk + 8 * o.hl;
+    a[i][0] = ld4(ap);
+    a[i][1] = ld4(ap + 4);
+    if constexpr (IMG) {
+      const char* img = sx ? o.img0 + (int64_t)(kk / 16) * GATE_IMG_BYTES : o.img1 + (int64_t)(kk / 16) * GATE_IMG_BYTES;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) img_frag(img, g * 32 + o.jj, o.hl, bi[i][g][0], bi[i][g][1], bi[i][g][2]);
+    } else {
+      const int ws = sx ? o.cin : H;
+      const float* wb = (sx ? o.wih : o.whh) + kk + 8 * o.hl;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float* wr = wb + (int64_t)g * H * ws;
+        bf[i][g][0] = ld4(wr);
+        bf[i][g][1] = ld4(wr + 4);
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // (keeps the scheduler from interleaving the loads with the MFMAs)
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const Split3 as = split3(a[i][0], a[i][1]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Split3 b;
+      if constexpr (IMG) {
+        b.p0 = __builtin_bit_cast(bf16x8_t, bi[i][g][0]);
+        b.p1 = __builtin_bit_cast(bf16x8_t, bi[i][g][1]);
+        b.p2 = __builtin_bit_cast(bf16x8_t, bi[i][g][2]);
+      } else {
+        b = split3(bf[i][g][0], bf[i][g][1]);
+      }
+      acc[g] = mfma_x6(as, b, acc[g]);
+    }
+  }
+}
+
+// Contiguous K-tile range [kb, ke) of wave `wave` out of KW_W (deterministic partition).
+__device__ __forceinline__ void kw_range(int nkt, int wave, int& kb, int& ke) {
+  const int per = (nkt + KW_W - 1) / KW_W;
+  kb = min(nkt, wave * per);
+  ke = min(nkt, kb + per);
+}
+
+// ---- forward: tile = 32 rows x 32 units (the 4 gates: 128 gate columns) ------------------------
+template <int H, bool IMG>
+__global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restrict__ F, float* __restrict__ HsAll,
+                                                          float* __restrict__ CsAll, float* __restrict__ GsAll,
+                                                          int64_t lsz, const float* __restrict__ theta,
+                                                          int64_t tstride, FwdWave wv, int T, int M, GateImgs gi) {
+  static_assert(H % 32 == 0, "32-unit groups");
+  __shared__ float red[KW_W * 64 * 64];  // [wave][gate*16 + r][lane]
+  int l, t, b0;
+  LayerOff lo;
+  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  const int ntm = (M + 31) / 32;
+  const int bl = (int)blockIdx.x - b0;
+  const int tm = bl % ntm, ug = bl / ntm;  // row tiles fastest (all XCDs see every unit group)
+  const int z = blockIdx.z;
+  const float* th = theta + (int64_t)z * tstride;
+  const int cin = lo.cin;
+  const int64_t slab = (int64_t)z * T * M;
+  const float* X = (l == 0 ? F : HsAll + (int64_t)(l - 1) * lsz) + (slab + (int64_t)t * M) * cin;
+  float* Hz = HsAll + (int64_t)l * lsz + slab * H;
+  float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * (4 * H);
+  const float* Hp = Hz + (int64_t)(t > 0 ? t - 1 : 0) * M * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane >> 5, jj = lane & 31;
+  const int m0 = tm * 32, j = ug * 32 + jj;
+
+  // epilogue operands: this thread's elements are rows kw_row(2 wave + q, hl), unit j
+  float bs[4], cp[2];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bs[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int m = min(m0 + kw_row(2 * wave + q, hl), M - 1);
+    const float v = Cz[((int64_t)(t > 0 ? t - 1 : 0) * M + m) * H + j];  // (t = 0: a valid address, selected out)
+    cp[q] = t > 0 ? v : 0.f;
+  }
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[g][r] = 0.f;
+  {
+    const int ar = min(m0 + jj, M - 1);  // this lane's A row (clamped: rows past M are not stored)
+    FwdKw o;
+    o.x = X + (int64_t)ar * cin;
+    o.hp = Hp + (int64_t)ar * H;
+    o.wih = th + lo.wih + (int64_t)j * cin;
+    o.whh = th + lo.whh + (int64_t)j * H;
+    o.img0 = o.img1 = nullptr;
+    if constexpr (IMG) {
+      int64_t io0 = 0, io1 = 0;
+#pragma unroll
+      for (int q = 0; q < MAX_LAYERS; ++q)
+        if (q == l) {
+          io0 = gi.off[q][0];
+          io1 = gi.off[q][1];
+        }
+      const char* ib = gi.th + (int64_t)z * gi.tstride;
+      o.img0 = ib + io0 + (int64_t)ug * (cin / 16) * GATE_IMG_BYTES;
+      o.img1 = ib + io1 + (int64_t)ug * (H / 16) * GATE_IMG_BYTES;
+    }
+    o.cin = cin;
+    o.hl = hl;
+    o.jj = jj;
+    int kb, ke;
+    kw_range((cin + (t > 0 ? H : 0)) / 16, wave, kb, ke);
+    // (uniform branches between straight-line chunks)
+    while (ke - kb >= KW_CH) {
+      fwd_kw_chunk<H, IMG, KW_CH>(o, kb, acc);
+      kb += KW_CH;
+    }
+    for (; kb < ke; ++kb) fwd_kw_chunk<H, IMG, 1>(o, kb, acc);
+  }
+
+  // partial tiles -> LDS (lane-contiguous: conflict-free), summed in wave order
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(wave * 64 + g * 16 + r) * 64 + lane] = acc[g][r];
+  __syncthreads();
+  const uint32_t tM = (uint32_t)t * (uint32_t)M;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 2 * wave + q;
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < KW_W; ++w) s += red[(w * 64 + g * 16 + r) * 64 + lane];
+      pre[g] = s + bs[g];
+    }
+    const int m = m0 + kw_row(r, hl);
+    if (m >= M) continue;
+    const float gi_ = sigmoidf_(pre[0]), gf = sigmoidf_(pre[1]), gg = tanhf_(pre[2]), go = sigmoidf_(pre[3]);
+    const float c = lstm_cell_c(gi_, gf, gg, cp[q]);
+    const float h = go * tanhf_(c);
+    const uint32_t row = tM + (uint32_t)m;
+    const uint32_t og = row * (4 * H) + j, oh = row * H + j;
+    stb(Gz, 4u * og, gi_);
+    stb(Gz, 4u * (og + H), gf);
+    stb(Gz, 4u * (og + 2 * H), gg);
+    stb(Gz, 4u * (og + 3 * H), go);
+    stb(Cz, 4u * oh, c);
+    stb(Hz, 4u * oh, h);
+  }
+}
+
+// Operands of one BPTT tile's K loop: this lane's rows of the two dG segments and weight columns.
+struct BwdKw {
+  const float* a0;  // segment 0 (dG above, or dG next when there is no layer above): row ar, k = 8 hl
+  const float* a1;  // segment 1 (dG next)
+  const float* w0;  // W (k = 8 hl, unit j) of segment 0: W_ih(l+1) or W_hh(l), [4H][H]
+  const float* w1;  // ... segment 1: W_hh(l)
+};
+
+template <int H, int N>
+__device__ __forceinline__ void bwd_kw_chunk(const BwdKw& o, int kt0, f32x16& acc) {
+  constexpr int G4 = 4 * H;
+  float4 a[N][2];
+  float b[N][8];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int k = 16 * (kt0 + i);
+    const bool s1 = k >= G4;
+    const int kk = s1 ? k - G4 : k;
+    const float* ap = (s1 ? o.a1 : o.a0) + kk;
+    a[i][0] = ld4(ap);
+    a[i][1] = ld4(ap + 4);
+    const float* wp = (s1 ? o.w1 : o.w0) + (int64_t)kk * H;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[i][e] = wp[e * H];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const Split3 as = split3(a[i][0], a[i][1]);
+    const Split3 bs = split3(make_float4(b[i][0], b[i][1], b[i][2], b[i][3]), make_float4(b[i][4], b[i][5], b[i][6], b[i][7]));
+    acc = mfma_x6(as, bs, acc);
+  }
+}
+
+// ---- BPTT: tile = 32 rows x 32 units of dh = [dG(l+1,t) | dG(l,t+1)] . [W_ih(l+1) ; W_hh(l)] -----
+template <int H>
+__global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, float* dGAll, float* __restrict__ dhAll,
+                                                          const float* __restrict__ CsAll,
+                                                          const float* __restrict__ dHhead, float* __restrict__ dcAll,
+                                                          int64_t lsz, const float* __restrict__ theta,
+                                                          int64_t tstride, BwdWave wv, int L, int T, int M) {
+  static_assert(H % 32 == 0, "32-unit tiles");
+  constexpr int G4 = 4 * H;
+  __shared__ float red[KW_W * 16 * 64];  // [wave][r][lane]
+  const int p = wave_index(wv, (int)blockIdx.x);
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const LayerOff lo = wave_sel(wv.lo, p);
+  const int64_t wih_up = wave_sel(wv.wih_up, p);
+  const int ntm = (M + 31) / 32;
+  const int bl = (int)blockIdx.x - b0;
+  const int tm = bl % ntm, tn = bl / ntm;
+  const int z = blockIdx.z;
+  const int64_t slab = (int64_t)z * T * M;
+  const float* th = theta + (int64_t)z * tstride;
+  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dhz = dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr;
+  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* dcz = dcAll + ((int64_t)l * gridDim.z + z) * M * H;
+  const float* dHz = dHhead + (int64_t)z * M * H;
+  const bool up = l + 1 < L, nx = t + 1 < T, first = t == T - 1, past = t > 0, head = first && l == L - 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane >> 5, jj = lane & 31;
+  const int m0 = tm * 32, j = tn * 32 + jj;
+
+  // epilogue operands of this thread's elements (rows kw_row(2 wave + q, hl), unit j), loaded first;
+  // uniform conditions select after loads from valid addresses (no branch around a load)
+  float g[2][4], cp[2], dc[2], hd[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int m = min(m0 + kw_row(2 * wave + q, hl), M - 1);
+    const int64_t row = (int64_t)t * M + m;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[q][k] = Gz[row * G4 + k * H + j];
+    const float c = Cz[(past ? row - M : row) * H + j];
+    const float d = dcz[(int64_t)m * H + j];
+    const float h = dHz[(int64_t)m * H + j];
+    cp[q] = past ? c : 0.f;
+    dc[q] = first ? 0.f : d;
+    hd[q] = head ? h : 0.f;
+  }
+
+  // segments [above | next] compacted (as k_lstm_bwd_step): K = ns * 4H
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  {
+    const float* pa = dGAll + (int64_t)(l + 1) * lsz * 4 + (slab + (int64_t)t * M) * G4;
+    const float* pn = dGz + (int64_t)(t + 1) * M * G4;
+    const int ar = min(m0 + jj, M - 1);
+    BwdKw o;
+    o.a0 = (up ? pa : pn) + (int64_t)ar * G4 + 8 * hl;
+    o.a1 = pn + (int64_t)ar * G4 + 8 * hl;
+    o.w0 = (up ? th + wih_up : th + lo.whh) + (int64_t)(8 * hl) * H + j;
+    o.w1 = th + lo.whh + (int64_t)(8 * hl) * H + j;
+    int kb, ke;
+    kw_range(((up ? 1 : 0) + (nx ? 1 : 0)) * (G4 / 16), wave, kb, ke);
+    while (ke - kb >= KW_BCH) {
+      bwd_kw_chunk<H, KW_BCH>(o, kb, acc);
+      kb += KW_BCH;
+    }
+    if (ke - kb >= 4) {
+      bwd_kw_chunk<H, 4>(o, kb, acc);
+      kb += 4;
+    }
+    for (; kb < ke; ++kb) bwd_kw_chunk<H, 1>(o, kb, acc);
+  }
+
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 2 * wave + q;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < KW_W; ++w) s += red[(w * 16 + r) * 64 + lane];
+    const int m = m0 + kw_row(r, hl);
+    if (m >= M) continue;
+    const float d = s + hd[q];
+    const float gi = g[q][0], gf = g[q][1], gg = g[q][2], go = g[q][3];
+    const float tc = tanhf_(lstm_cell_c(gi, gf, gg, cp[q]));
+    const float dct = dc[q] + d * go * (1.f - tc * tc);
+    const int64_t row = (int64_t)t * M + m;
+    float* gp = dGz + row * G4 + j;
+    gp[0] = dct * gg * gi * (1.f - gi);
+    gp[H] = dct * cp[q] * gf * (1.f - gf);
+    gp[2 * H] = dct * gi * (1.f - gg * gg);
+    gp[3 * H] = d * tc * go * (1.f - go);
+    dcz[(int64_t)m * H + j] = dct * gf;
+    if (dhz) dhz[row * H + j] = d;
+  }
+}
+
+bool small_kw_ok(const Dims& d, const Work& w) {
+  if (!w.kn.small_kw || w.drop.lstm() || d.H % 32 != 0 || d.H > 256 || d.Hc % 16 != 0) return false;
+  return true;
+}
+
+void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta, int64_t tstride,
+                        const ParamOff& po) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  FwdWave wv{};
+  fwd_wave(d, w, po, diag, ((w.M + 31) / 32) * (d.H / 32), false, wv);
+  if (wv.n == 0) return;
+  const dim3 grid(wv.off[wv.n], 1, w.Z);
+  count_variant(w, V_FWD_KW);
+  if (w.gimg.th && w.gimg_src == theta) {
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, true><<<grid, 64 * KW_W, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
+                                                                               tstride, wv, d.T, w.M, w.gimg)));
+  } else {
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, false><<<grid, 64 * KW_W, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
+                                                                                tstride, wv, d.T, w.M, w.gimg)));
+  }
+}
+
+void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
+                        const ParamOff& po) {
+  const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
+  BwdWave wv{};
+  bwd_wave(d, w, po, e, ((w.M + 31) / 32) * (d.H / 32), false, wv);
+  if (wv.n == 0) return;
+  const dim3 grid(wv.off[wv.n], 1, w.Z);
+  count_variant(w, V_BWD_KW);
+  SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT><<<grid, 64 * KW_W, 0, s>>>(w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta,
+                                                                       tstride, wv, d.L, d.T, w.M)));
+}
+
+}  // namespace smaml
