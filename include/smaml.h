@@ -302,8 +302,9 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "bwdd_remap":                  tangent BPTT tiles dealt in pair-segment order per XCD (1) or in
  *                                  hardware order (0; bitwise equal);
  *   "small_kw":                    small-grid (batch-1) LSTM forward / BPTT diagonals as one launch
- *                                  with the K reduction split over the waves of a workgroup (1), or
- *                                  as the split-K part + cell launch pair (0). */
+ *                                  with the K reduction split over the waves of a workgroup (1; 2 =
+ *                                  also with pre-split BPTT weight images), or as the split-K part +
+ *                                  cell launch pair (0). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -83,12 +83,13 @@ def test_adaptation_matches_reference_adapt_model(golden_dir, region):
         assert rel(got[k].cpu().numpy(), z[f"{tag}/adapted/{k}"]) < 1e-5, k
 
 
-@pytest.mark.parametrize("small_kw", [0, 1], ids=["split-k", "kw"])
+@pytest.mark.parametrize("small_kw", [0, 1, 2], ids=["split-k", "kw", "kw-bwd-img"])
 def test_adaptation_n441_matches_oracle(small_kw):
     """BASELINE config 4 shapes (N=441, Hc=256, LSTM 4x128, batch-1 steps): 2 epochs over 16
     shuffled training windows + the 4-window validation, against the oracle. Runs the
     small-grid forward / BPTT steps -- the split-K part + cell launch pairs (small_kw 0) or the
-    one-launch K-split-over-waves kernels (kernels_small.hip, small_kw 1) -- and the per-window GCN
+    one-launch K-split-over-waves kernels (kernels_small.hip, small_kw 1; 2 with the BPTT's pre-split
+    weight images) -- and the per-window GCN
     feature cache (the second epoch reads every window's features from it)."""
     from weatherforecast_stgcn_maml_amd import _capi
     from weatherforecast_stgcn_maml_amd.config import CONFIG2

@@ -247,6 +247,8 @@ struct smaml_ctx {
   char* gcn_wimg = nullptr;   // pre-split GCN weight images of the fused t >= 1 GCN (kernels_gcn.hip)
   char* gimg_buf = nullptr;   // pre-split gate-GEMM weight images (prep_gate_images)
   int64_t gimg_cap = 0;
+  char* bimg_buf = nullptr;   // pre-split BPTT weight images (prep_bwd_images; small-grid BPTT)
+  int64_t bimg_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
   // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
   unsigned* bar = nullptr;
@@ -689,6 +691,33 @@ int prep_gate_images(smaml_ctx* c, hipStream_t s, const float* theta, int64_t ts
   return SMAML_OK;
 }
 
+// Pre-split images of theta's BPTT weights for this backward (launch_split_bwd) when the small-grid
+// BPTT steps will read them (small_kw 2, batch-1 sizes); like the gate images, re-split every call.
+int prep_bwd_images(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  w.bimg = BwdImgs{};
+  w.bimg_src = nullptr;
+  if (c->kn.small_kw != 2 || !small_kw_ok(d, w) || (int64_t)w.Z * w.M > c->kn.wgrad_group_max_rows) return SMAML_OK;
+  BwdImgs bi{};
+  const int64_t need = bwd_img_bytes(d, &bi) * w.Z;
+  if (need > c->bimg_cap) {
+    if (c->bimg_buf) HIP_TRY(hipFree(c->bimg_buf));
+    c->bimg_buf = nullptr;
+    c->bimg_cap = 0;
+    if (hipMalloc((void**)&c->bimg_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      return SMAML_OK;  // no room: the BPTT steps load and split the f32 weights themselves
+    }
+    c->bimg_cap = need;
+  }
+  bi.th = c->bimg_buf;
+  TIMED(c, s, C_MISC, 0, launch_split_bwd(s, d, c->po, theta, tstride, w.Z, bi));
+  w.bimg = bi;
+  w.bimg_src = theta;
+  return SMAML_OK;
+}
+
 // LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront).
 int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   const Dims& d = c->d;
@@ -747,6 +776,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   // BPTT as reverse anti-diagonals; layer l's weight gradient as soon as its t = 0 step is done,
   // or, for small grids (batch-1 adaptation), all layers' in one launch after the sweep
   const bool grouped = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows;
+  TRY(prep_bwd_images(c, s, theta, tstride));
   WgradPlan plans[MAX_LAYERS];
   double gfl = 0.0;
   for (int e = 0; e < d.T + d.L - 1; ++e) {
@@ -997,6 +1027,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->so_F) (void)hipFree(c->so_F);
   if (c->gcn_wimg) (void)hipFree(c->gcn_wimg);
   if (c->gimg_buf) (void)hipFree(c->gimg_buf);
+  if (c->bimg_buf) (void)hipFree(c->bimg_buf);
   if (c->bar) (void)hipFree(c->bar);
   if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);
@@ -1497,7 +1528,7 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_ws = (int)value;
   } else if (k == "bwdd_remap" && (value == 0 || value == 1)) {
     c->kn.bwdd_remap = (int)value;
-  } else if (k == "small_kw" && (value == 0 || value == 1)) {
+  } else if (k == "small_kw" && value >= 0 && value <= 2) {
     c->kn.small_kw = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);

@@ -123,7 +123,8 @@ struct Knobs {
   int wgrad_pair;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
   int wgrad_ws;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
   int bwdd_remap;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
-  int small_kw;              // 1: small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip)
+  int small_kw;              // small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip):
+                             // 1 = on, 2 = on with pre-split BPTT weight images (launch_split_bwd), 0 = split-K pairs
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -157,8 +158,21 @@ struct GateImgs {
   int64_t tstride;             // bytes per task
   int64_t off[MAX_LAYERS][2];  // byte offset of (layer, W_ih | W_hh) in a task's images
 };
+// ---- pre-split BPTT weight images (kernels_small.hip launch_split_bwd; small-grid BPTT) ----
+// Per task, for W_hh of every layer and W_ih of layers >= 1 (the [4H][H] matrices the BPTT step reads
+// as B[k][j]): per K-tile kt (16 gate rows) and unit tile tn (32 units) three bf16 planes of
+// [32 units][16 k], so a lane's MFMA B fragment (unit jj, k = 8h .. 8h + 7) is one 16-B load per plane.
+constexpr int BWD_IMG_BYTES = 3 * 32 * 16 * 2;
+struct BwdImgs {
+  char* th;                   // null = not built
+  int64_t tstride;            // bytes per task
+  int64_t off_hh[MAX_LAYERS];  // byte offset of W_hh(l) in a task's images
+  int64_t off_ih[MAX_LAYERS];  // ... W_ih(l), l >= 1 (0 for l = 0: not built)
+};
 struct Work {
   int Z, B, M;
+  BwdImgs bimg;            // pre-split BPTT weight images (launch_split_bwd), small-grid BPTT only
+  const float* bimg_src;   // the parameter vector bimg.th was split from
   GateImgs gimg;           // pre-split images of the weights the gate GEMMs read (launch_split_gate)
   const float* gimg_src;   // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src; // ... and gimg.u (the sweep's tangent direction)
@@ -377,6 +391,9 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 // kernels_small.hip: the small-grid (batch-1) forward / BPTT diagonal as one launch with the K
 // reduction split over the waves of a workgroup (used where the split-K pair would run)
 bool small_kw_ok(const Dims& d, const Work& w);
+int64_t bwd_img_bytes(const Dims& d, BwdImgs* bi);  // per task; fills bi's offsets / tstride
+void launch_split_bwd(hipStream_t s, const Dims& d, const ParamOff& po, const float* theta, int64_t tstride, int Z,
+                      const BwdImgs& bi);
 void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta, int64_t tstride,
                         const ParamOff& po);
 void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,

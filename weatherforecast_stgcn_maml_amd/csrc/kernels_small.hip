@@ -220,13 +220,17 @@ struct BwdKw {
   const float* a1;  // segment 1 (dG next)
   const float* w0;  // W (k = 8 hl, unit j) of segment 0: W_ih(l+1) or W_hh(l), [4H][H]
   const float* w1;  // ... segment 1: W_hh(l)
+  const char* i0;   // (IMG) segment 0's image at K-tile 0, unit tile tn, this lane's 16-B chunk
+  const char* i1;   // ... segment 1
 };
 
-template <int H, int N>
+template <int H, bool IMG, int N>
 __device__ __forceinline__ void bwd_kw_chunk(const BwdKw& o, int kt0, f32x16& acc) {
   constexpr int G4 = 4 * H;
+  constexpr int KT_BYTES = (H / 32) * BWD_IMG_BYTES;  // one K-tile of an image, all unit tiles
   float4 a[N][2];
   float b[N][8];
+  uint4 bi[N][3];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int k = 16 * (kt0 + i);
@@ -235,26 +239,41 @@ __device__ __forceinline__ void bwd_kw_chunk(const BwdKw& o, int kt0, f32x16& ac
     const float* ap = (s1 ? o.a1 : o.a0) + kk;
     a[i][0] = ld4(ap);
     a[i][1] = ld4(ap + 4);
-    const float* wp = (s1 ? o.w1 : o.w0) + (int64_t)kk * H;
+    if constexpr (IMG) {
+      const char* q = (s1 ? o.i1 : o.i0) + (kk / 16) * KT_BYTES;
+      bi[i][0] = *reinterpret_cast<const uint4*>(q);
+      bi[i][1] = *reinterpret_cast<const uint4*>(q + 1024);
+      bi[i][2] = *reinterpret_cast<const uint4*>(q + 2048);
+    } else {
+      const float* wp = (s1 ? o.w1 : o.w0) + (int64_t)kk * H;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) b[i][e] = wp[e * H];
+      for (int e = 0; e < 8; ++e) b[i][e] = wp[e * H];
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const Split3 as = split3(a[i][0], a[i][1]);
-    const Split3 bs = split3(make_float4(b[i][0], b[i][1], b[i][2], b[i][3]), make_float4(b[i][4], b[i][5], b[i][6], b[i][7]));
+    Split3 bs;
+    if constexpr (IMG) {
+      bs.p0 = __builtin_bit_cast(bf16x8_t, bi[i][0]);
+      bs.p1 = __builtin_bit_cast(bf16x8_t, bi[i][1]);
+      bs.p2 = __builtin_bit_cast(bf16x8_t, bi[i][2]);
+    } else {
+      bs = split3(make_float4(b[i][0], b[i][1], b[i][2], b[i][3]), make_float4(b[i][4], b[i][5], b[i][6], b[i][7]));
+    }
     acc = mfma_x6(as, bs, acc);
   }
 }
 
 // ---- BPTT: tile = 32 rows x 32 units of dh = [dG(l+1,t) | dG(l,t+1)] . [W_ih(l+1) ; W_hh(l)] -----
-template <int H>
+template <int H, bool IMG>
 __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, float* dGAll, float* __restrict__ dhAll,
                                                           const float* __restrict__ CsAll,
                                                           const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                           int64_t lsz, const float* __restrict__ theta,
-                                                          int64_t tstride, BwdWave wv, int L, int T, int M) {
+                                                          int64_t tstride, BwdWave wv, int L, int T, int M,
+                                                          BwdImgs bim) {
   static_assert(H % 32 == 0, "32-unit tiles");
   constexpr int G4 = 4 * H;
   __shared__ float red[KW_W * 16 * 64];  // [wave][r][lane]
@@ -308,17 +327,29 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
     o.a1 = pn + (int64_t)ar * G4 + 8 * hl;
     o.w0 = (up ? th + wih_up : th + lo.whh) + (int64_t)(8 * hl) * H + j;
     o.w1 = th + lo.whh + (int64_t)(8 * hl) * H + j;
+    o.i0 = o.i1 = nullptr;
+    if constexpr (IMG) {
+      int64_t ohh = 0, oih = 0;  // (layer l's W_hh and layer l+1's W_ih, selected with scalar compares)
+#pragma unroll
+      for (int q = 0; q < MAX_LAYERS; ++q) {
+        if (q == l) ohh = bim.off_hh[q];
+        if (q == l + 1) oih = bim.off_ih[q];
+      }
+      const char* ib = bim.th + (int64_t)z * bim.tstride + tn * BWD_IMG_BYTES + jj * 32 + hl * 16;
+      o.i0 = ib + (up ? oih : ohh);
+      o.i1 = ib + ohh;
+    }
     int kb, ke;
     kw_range(((up ? 1 : 0) + (nx ? 1 : 0)) * (G4 / 16), wave, kb, ke);
     while (ke - kb >= KW_BCH) {
-      bwd_kw_chunk<H, KW_BCH>(o, kb, acc);
+      bwd_kw_chunk<H, IMG, KW_BCH>(o, kb, acc);
       kb += KW_BCH;
     }
     if (ke - kb >= 4) {
-      bwd_kw_chunk<H, 4>(o, kb, acc);
+      bwd_kw_chunk<H, IMG, 4>(o, kb, acc);
       kb += 4;
     }
-    for (; kb < ke; ++kb) bwd_kw_chunk<H, 1>(o, kb, acc);
+    for (; kb < ke; ++kb) bwd_kw_chunk<H, IMG, 1>(o, kb, acc);
   }
 
 #pragma unroll
@@ -377,8 +408,67 @@ void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, cons
   if (wv.n == 0) return;
   const dim3 grid(wv.off[wv.n], 1, w.Z);
   count_variant(w, V_BWD_KW);
-  SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT><<<grid, 64 * KW_W, 0, s>>>(w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta,
-                                                                       tstride, wv, d.L, d.T, w.M)));
+  if (w.bimg.th && w.bimg_src == theta) {
+    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, true><<<grid, 64 * KW_W, 0, s>>>(
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg)));
+  } else {
+    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, false><<<grid, 64 * KW_W, 0, s>>>(
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg)));
+  }
+}
+
+// ---- pre-split BPTT weight images (kernels.h BwdImgs) ----------------------------------------
+int64_t bwd_img_bytes(const Dims& d, BwdImgs* bi) {
+  const int64_t per = (int64_t)(4 * d.H / 16) * (d.H / 32) * BWD_IMG_BYTES;  // one [4H][H] matrix
+  int64_t off = 0;
+  for (int l = 0; l < d.L; ++l) {
+    if (bi) bi->off_hh[l] = off;
+    off += per;
+    if (bi) bi->off_ih[l] = l > 0 ? off : 0;
+    if (l > 0) off += per;
+  }
+  if (bi) bi->tstride = off;
+  return off;
+}
+
+// One thread per (task, matrix, K-tile kt, unit tile tn, unit jj, half h): W[16 kt + 8 h + e][32 tn + jj],
+// e = 0..7, split into three bf16 pieces, one 16-B chunk per plane.
+__global__ void k_split_bwd(const float* __restrict__ theta, int64_t tstride, ParamOff po, int L, int H,
+                            BwdImgs bi, int64_t nthreads) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int z = blockIdx.y;
+  if (i >= nthreads) return;
+  const int h = (int)(i & 1), jj = (int)((i >> 1) & 31);
+  const int ntn = H / 32, nkt = 4 * H / 16;
+  int64_t r = i >> 6;
+  const int tn = (int)(r % ntn);
+  r /= ntn;
+  const int kt = (int)(r % nkt);
+  const int mat = (int)(r / nkt);  // bwd_img_bytes order: W_hh(0), W_hh(1), W_ih(1), W_hh(2), W_ih(2), ...
+  const int l = (mat + 1) / 2;
+  const bool ih = mat > 0 && mat % 2 == 0;
+  if (l >= L) return;
+  const LayerOff& lo = po.lay[l];
+  const float* src = theta + (int64_t)z * tstride + (ih ? lo.wih : lo.whh) + (int64_t)(16 * kt + 8 * h) * H + 32 * tn + jj;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = src[(int64_t)e * H];
+  const Split3 p = split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  int64_t moff = 0;
+#pragma unroll
+  for (int q = 0; q < MAX_LAYERS; ++q)
+    if (q == l) moff = ih ? bi.off_ih[q] : bi.off_hh[q];
+  char* o = bi.th + (int64_t)z * bi.tstride + moff + ((int64_t)kt * ntn + tn) * BWD_IMG_BYTES + jj * 32 + h * 16;
+  *reinterpret_cast<uint4*>(o) = __builtin_bit_cast(uint4, p.p0);
+  *reinterpret_cast<uint4*>(o + 1024) = __builtin_bit_cast(uint4, p.p1);
+  *reinterpret_cast<uint4*>(o + 2048) = __builtin_bit_cast(uint4, p.p2);
+}
+
+void launch_split_bwd(hipStream_t s, const Dims& d, const ParamOff& po, const float* theta, int64_t tstride, int Z,
+                      const BwdImgs& bi) {
+  const int nmat = 2 * d.L - 1;
+  const int64_t threads = (int64_t)nmat * (4 * d.H / 16) * (d.H / 32) * 64;
+  k_split_bwd<<<dim3((unsigned)((threads + 255) / 256), Z), 256, 0, s>>>(theta, tstride, po, d.L, d.H, bi, threads);
 }
 
 }  // namespace smaml
