@@ -1405,6 +1405,8 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
   if (!theta || !m || !v || nsteps <= 0 || batch <= 0 || !windows_host || !lr_dev || !losses || step0 < 0)
     return fail(SMAML_EINVAL, "bad adapt_steps arguments");
   TRY(ensure_device(c));
+  TRY(ensure_bar(c));
+  TRY(check_device_error(c));
   hipStream_t s = (hipStream_t)stream;
   const Dims& d = c->d;
   const int B = batch;
@@ -1457,7 +1459,7 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     TRY(run_backward(c, s, theta, 0, c->grad));
     TIMED(c, s, C_MISC, 0,
           launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
-                         weight_decay, max_norm));
+                         weight_decay, max_norm, bar_plan(c)));
   }
   c->w.F = c->F_main;
   c->w.drop = Drop{};

@@ -471,7 +471,8 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
                   float max_norm, float* norm_out);
 
 void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
-                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm);
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm,
+                    const BarPlan& bp);  // bp.fused: one grid-barrier launch (k_adam_l2_fused), else two
 
 // ---- second-order launchers (kernels_dual.hip) ----
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
