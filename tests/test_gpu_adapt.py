@@ -124,25 +124,3 @@ def test_adaptation_n441_matches_oracle(small_kw):
         assert rel(got[k].cpu().numpy(), ref_p[k].numpy()) < 1e-5, k
     assert abs(res.val_loss - ref_val) < 1e-5 * ref_val
 
-
-def test_adaptation_fused_update_bitwise():
-    """The adaptation step's clip + Adam(L2) as one grid-barrier launch (k_adam_l2_fused) against the
-    two-launch form (k_sqsum + k_adam_l2, option grid_barrier 0): bitwise-equal parameters."""
-    from weatherforecast_stgcn_maml_amd import _capi
-
-    d = CONFIG1
-    P = synth.init_params(23, d, gcn_bias_scale=0.1)
-    tr, gcn = _split(P)
-    lats, lons = synth.region_grid(n_lat=5, n_lon=5)
-    ei = build_spatial_graph(lats, lons, 4)[0]
-    feats = synth.make_features(3300, d.num_nodes, synth.t_total_for(20))
-    out = []
-    for fused in (1, 0):
-        ctx = _capi.Context(d, 0)
-        ctx.set_option("grid_barrier", fused)
-        torch.manual_seed(9)
-        res = adapt(d, feats, ei, {k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, tr, "Delhi",
-                    epochs=2, device="cuda:0", ctx=ctx)
-        out.append((res.theta.detach().cpu().clone(), np.asarray(res.epoch_losses)))
-    assert torch.equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])

@@ -227,7 +227,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, 1, 0, SMAML_SMALL_KW};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, 0, SMAML_SMALL_KW};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -1405,8 +1405,6 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
   if (!theta || !m || !v || nsteps <= 0 || batch <= 0 || !windows_host || !lr_dev || !losses || step0 < 0)
     return fail(SMAML_EINVAL, "bad adapt_steps arguments");
   TRY(ensure_device(c));
-  TRY(ensure_bar(c));
-  TRY(check_device_error(c));
   hipStream_t s = (hipStream_t)stream;
   const Dims& d = c->d;
   const int B = batch;
@@ -1459,7 +1457,7 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     TRY(run_backward(c, s, theta, 0, c->grad));
     TIMED(c, s, C_MISC, 0,
           launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
-                         weight_decay, max_norm, bar_plan(c)));
+                         weight_decay, max_norm));
   }
   c->w.F = c->F_main;
   c->w.drop = Drop{};

@@ -132,8 +132,11 @@ struct Knobs {
 #ifndef SMAML_GCN_FUSED
 #define SMAML_GCN_FUSED 1
 #endif
+#ifndef SMAML_WGRAD_WS_DEFAULT
+#define SMAML_WGRAD_WS_DEFAULT 0  // k_wgrad_ws measured slower than the staged tiles in every arm
+#endif
 #ifndef SMAML_SMALL_KW
-#define SMAML_SMALL_KW 0
+#define SMAML_SMALL_KW 1
 #endif
 #ifndef SMAML_WGRAD_PAIR
 #define SMAML_WGRAD_PAIR 1
@@ -471,8 +474,7 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
                   float max_norm, float* norm_out);
 
 void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
-                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm,
-                    const BarPlan& bp);  // bp.fused: one grid-barrier launch (k_adam_l2_fused), else two
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm);
 
 // ---- second-order launchers (kernels_dual.hip) ----
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,

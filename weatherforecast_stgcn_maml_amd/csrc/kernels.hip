@@ -2497,53 +2497,13 @@ __global__ void k_adam_l2(float* __restrict__ p, const float* __restrict__ g, fl
   }
 }
 
-// The same update as ONE grid-barrier launch (batch-1 adaptation: two latency-bound launches per
-// sample-step become one): phase 1 = k_sqsum's partials (same partition, same order), grid barrier,
-// phase 2 = k_adam_l2's element update. Bitwise equal to the two-launch form.
-__global__ __launch_bounds__(NT) void k_adam_l2_fused(float* __restrict__ p, const float* __restrict__ g,
-                                                      float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                      double* __restrict__ part, const float* __restrict__ lr_dev,
-                                                      int step, float b1, float b2, float eps, float wd,
-                                                      float max_norm, GridBar gb) {
-  __shared__ double red[NT / 64];
-  const int64_t per = (n + SQB - 1) / SQB;
-  for (int it = blockIdx.x; it < SQB; it += gridDim.x) {
-    const int64_t beg = (int64_t)it * per, end = beg + per < n ? beg + per : n;
-    double acc = 0.0;
-    for (int64_t i = beg + threadIdx.x; i < end; i += NT) {
-      const double x = g[i];
-      acc += x * x;
-    }
-    const double sum = block_sum_d(acc, red);
-    if (threadIdx.x == 0) part[it] = sum;
-  }
-  if (!grid_barrier(gb, gridDim.x)) return;
-  float total;
-  const float coef = clip_coef_from(part, max_norm, &total);
-  const float lr = *lr_dev;
-  const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = fmaf(wd, p[i], g[i] * coef);
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-    p[i] = p[i] - step_size * (mi / (sqrtf(vi) / bc2_sqrt + eps));
-    m[i] = mi;
-    v[i] = vi;
-  }
-}
-
+// (measured: the same update as ONE grid-barrier launch -- k_sqsum's partials, a grid barrier over ~512
+// blocks, the element update -- took 81 us per sample-step against 23 for these two launches,
+// profiles/r04_rocprof_adapt_kw.md: 512 arrivals on one counter cost more than a launch boundary)
 void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
-                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm,
-                    const BarPlan& bp) {
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm) {
   int nb = (int)((n + NT - 1) / NT);
   if (nb > 2048) nb = 2048;
-  const int nf = bp.fused ? grid_barrier_grid(grid_barrier_capacity((const void*)k_adam_l2_fused), nb, bp.oversize) : 0;
-  if (nf > 0) {
-    k_adam_l2_fused<<<nf, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, step, b1, b2, eps, wd, max_norm, bp.gb);
-    return;
-  }
   k_sqsum<<<dim3(SQB, 1), NT, 0, s>>>(g, n, part);
   k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, step, b1, b2, eps, wd, max_norm);
 }
