@@ -21,6 +21,37 @@
 
 namespace smaml {
 
+#ifndef SMAML_KW_PROBE
+#define SMAML_KW_PROBE 0  // diagnostic builds only: per-workgroup phase timestamps (tools/kw_probe.py)
+#endif
+#if SMAML_KW_PROBE
+// wall_clock64 at 5 points (start, K-loop loads issued, K loop done, partials in LDS, epilogue issued) of
+// wave 0 of every workgroup of the launch whose id (forward diagonal, or 100 + BPTT diagonal) is the target
+__device__ int g_kwp_target = -1;
+__device__ unsigned long long g_kwp[1024][5];
+#define KWP(id, slot) \
+  if (id == g_kwp_target && threadIdx.x == 0 && blockIdx.x < 1024) g_kwp[blockIdx.x][slot] = wall_clock64()
+// out == null: arm `target` and zero the records; else copy n workgroups' records out. Returns the wall
+// clock rate in kHz (> 0) or -1.
+extern "C" int smaml_kw_probe(int target, unsigned long long* out, int n) {
+  int khz = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+    return -1;
+  if (!out) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_kwp)) != hipSuccess || hipMemset(p, 0, sizeof(g_kwp)) != hipSuccess)
+      return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_kwp_target), &target, sizeof(int)) == hipSuccess ? khz : -1;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kwp), sizeof(unsigned long long) * 5 * (n < 1024 ? n : 1024)) ==
+                 hipSuccess ? khz : -1;
+}
+#else
+#define KWP(id, slot) (void)0
+#endif
+
 constexpr int KW_W = 8;   // waves per workgroup (two per SIMD)
 constexpr int KW_CH = 2;  // K-tiles per wave whose loads are in flight together (forward)
 constexpr int KW_BCH = 8; // same, BPTT (a K-tile's fragments are 16 VGPRs against the forward's 56)
@@ -110,8 +141,10 @@ template <int H, bool IMG>
 __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restrict__ F, float* __restrict__ HsAll,
                                                           float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                           int64_t lsz, const float* __restrict__ theta,
-                                                          int64_t tstride, FwdWave wv, int T, int M, GateImgs gi) {
+                                                          int64_t tstride, FwdWave wv, int T, int M, GateImgs gi,
+                                                          int pid) {
   static_assert(H % 32 == 0, "32-unit groups");
+  KWP(pid, 0);
   __shared__ float red[KW_W * 64 * 64];  // [wave][gate*16 + r][lane]
   int l, t, b0;
   LayerOff lo;
@@ -172,6 +205,7 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
     o.jj = jj;
     int kb, ke;
     kw_range((cin + (t > 0 ? H : 0)) / 16, wave, kb, ke);
+    KWP(pid, 1);
     // (uniform branches between straight-line chunks)
     while (ke - kb >= KW_CH) {
       fwd_kw_chunk<H, IMG, KW_CH>(o, kb, acc);
@@ -181,11 +215,13 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
   }
 
   // partial tiles -> LDS (lane-contiguous: conflict-free), summed in wave order
+  KWP(pid, 2);
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 64 + g * 16 + r) * 64 + lane] = acc[g][r];
   __syncthreads();
+  KWP(pid, 3);
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -212,6 +248,7 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
     stb(Cz, 4u * oh, c);
     stb(Hz, 4u * oh, h);
   }
+  KWP(pid, 4);
 }
 
 // Operands of one BPTT tile's K loop: this lane's rows of the two dG segments and weight columns.
@@ -273,8 +310,9 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
                                                           const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                           int64_t lsz, const float* __restrict__ theta,
                                                           int64_t tstride, BwdWave wv, int L, int T, int M,
-                                                          BwdImgs bim) {
+                                                          BwdImgs bim, int pid) {
   static_assert(H % 32 == 0, "32-unit tiles");
+  KWP(pid, 0);
   constexpr int G4 = 4 * H;
   __shared__ float red[KW_W * 16 * 64];  // [wave][r][lane]
   const int p = wave_index(wv, (int)blockIdx.x);
@@ -341,6 +379,7 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
     }
     int kb, ke;
     kw_range(((up ? 1 : 0) + (nx ? 1 : 0)) * (G4 / 16), wave, kb, ke);
+    KWP(pid, 1);
     while (ke - kb >= KW_BCH) {
       bwd_kw_chunk<H, IMG, KW_BCH>(o, kb, acc);
       kb += KW_BCH;
@@ -352,9 +391,11 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
     for (; kb < ke; ++kb) bwd_kw_chunk<H, IMG, 1>(o, kb, acc);
   }
 
+  KWP(pid, 2);
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
   __syncthreads();
+  KWP(pid, 3);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int r = 2 * wave + q;
@@ -376,6 +417,7 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
     dcz[(int64_t)m * H + j] = dct * gf;
     if (dhz) dhz[row * H + j] = d;
   }
+  KWP(pid, 4);
 }
 
 bool small_kw_ok(const Dims& d, const Work& w) {
@@ -393,10 +435,10 @@ void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, c
   count_variant(w, V_FWD_KW);
   if (w.gimg.th && w.gimg_src == theta) {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, true><<<grid, 64 * KW_W, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
-                                                                               tstride, wv, d.T, w.M, w.gimg)));
+                                                                               tstride, wv, d.T, w.M, w.gimg, diag)));
   } else {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, false><<<grid, 64 * KW_W, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
-                                                                                tstride, wv, d.T, w.M, w.gimg)));
+                                                                                tstride, wv, d.T, w.M, w.gimg, diag)));
   }
 }
 
@@ -410,10 +452,10 @@ void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, cons
   count_variant(w, V_BWD_KW);
   if (w.bimg.th && w.bimg_src == theta) {
     SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, true><<<grid, 64 * KW_W, 0, s>>>(
-                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg)));
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg, 100 + e)));
   } else {
     SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, false><<<grid, 64 * KW_W, 0, s>>>(
-                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg)));
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg, 100 + e)));
   }
 }
 
