@@ -1193,6 +1193,7 @@ int smaml_gcn_conv_backward(smaml_ctx* c, void* stream, const float* x, int32_t 
     Work w = c->w;
     w.Z = 1;
     w.drop = Drop{};
+    w.kn = c->kn;
     launch_wgrad(s, c->d, w, dz, 0, cout, ax, 0, cin, nullptr, 0, 0, rows, 0, dwb, 0, 0, 0,
                  (int64_t)cout * cin, -1, true, false);
   }

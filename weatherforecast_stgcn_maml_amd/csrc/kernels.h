@@ -423,9 +423,9 @@ struct WgradPlan {
   float* part;
   int ldp, ntm, ntn, nsplit;
   int64_t kchunk;
-  Drop drop;       // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
-  int drop_layer;
-  bool wide;       // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
+  Drop drop{};          // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
+  int drop_layer = -1;  // (defaults: no dropout -- launch_wgrad's callers never set these)
+  bool wide = false;    // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
   bool ws = false; // warp-specialised 256 x 128 tiles (k_wgrad_ws; dropout-free launches only)
   // pair (pair_wgrad): slices [nsplit1, nsplit) sum A2^T [B1s | B2s] (same shape and strides) into
   // the same gradient; A2 == nullptr: one problem
