@@ -553,11 +553,12 @@ def test_second_order_bench_tiles_b32_dropout():
     _check_meta_step(res, ml, ref, d, names, 1, cfg.inner_steps)
 
 
-@pytest.mark.parametrize("tiles", ["big", "small", "split"])
+@pytest.mark.parametrize("tiles", ["big", "small", "split", "kw"])
 @pytest.mark.parametrize("keep", [-1, 0])
 def test_second_order_tile_variants_task_groups(tiles, keep):
     """Every BPTT tile variant forced at config-2 shapes (B=1, K=2, 3 tasks run in task groups
-    of 2): 128x128 tiles (the bench's), 64x64 tiles, and the split-K small-grid steps."""
+    of 2): 128x128 tiles (the bench's), 64x64 tiles, and the small-grid steps -- split-K part + cell
+    pairs (small_kw 0) or one launch with the K split over waves (kernels_small.hip, small_kw 1)."""
     d = CONFIG2
     cfg = MamlConfig(inner_steps=2, batch=1, order=2)
     P = synth.init_params(14, d, gcn_bias_scale=0.1)
@@ -570,7 +571,8 @@ def test_second_order_tile_variants_task_groups(tiles, keep):
     big = 0 if tiles == "big" else 1 << 30
     ml.ctx.set_option("bwd_big_min", big)
     ml.ctx.set_option("bwdd_big_min", big)
-    ml.ctx.set_option("split_max", 4 if tiles == "split" else 1)
+    ml.ctx.set_option("split_max", 4 if tiles in ("split", "kw") else 1)
+    ml.ctx.set_option("small_kw", 1 if tiles == "kw" else 0)
     ml.ctx.set_option("keep", keep)
     ml.ctx.variant_counts(reset=True)
     res = ml.meta_step()
@@ -581,7 +583,9 @@ def test_second_order_tile_variants_task_groups(tiles, keep):
         assert vc["bwd_big"] > 0 and vc["bwd_small"] == vc["bwd_split"] == 0, vc
     elif tiles == "small":
         assert vc["bwd_small"] > 0 and vc["bwd_big"] == vc["bwd_split"] == 0 and vc["fwd_split"] == 0, vc
-    else:
+    elif tiles == "split":
         assert vc["bwd_split"] > 0 and vc["fwd_split"] > 0 and vc["bwd_big"] == 0, vc
+    else:
+        assert vc["bwd_kw"] > 0 and vc["fwd_kw"] > 0 and vc["bwd_split"] == vc["bwd_big"] == 0, vc
     ref = _oracle_meta_step("groups", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
     _check_meta_step(res, ml, ref, d, names, 3, cfg.inner_steps)
