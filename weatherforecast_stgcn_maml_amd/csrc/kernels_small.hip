@@ -52,9 +52,6 @@ extern "C" int smaml_kw_probe(int target, unsigned long long* out, int n) {
 #define KWP(id, slot) (void)0
 #endif
 
-#ifndef SMAML_KW_LDS3
-#define SMAML_KW_LDS3 1  // forward: a wave's three K-tiles in one round trip (third B image via LDS)
-#endif
 constexpr int KW_W = 8;   // waves per workgroup (two per SIMD)
 constexpr int KW_CH = 2;  // K-tiles per wave whose loads are in flight together (forward)
 constexpr int KW_BCH = 8; // same, BPTT (a K-tile's fragments are 16 VGPRs against the forward's 56)
@@ -129,67 +126,6 @@ __device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, f32x16 (&a
       }
       acc[g] = mfma_x6(as, b, acc[g]);
     }
-  }
-}
-
-// Three K-tiles in ONE load round trip (the layer-0 problem's share per wave at Hc = 256): tiles 0 and 1
-// as register fragments, tile 2's B image copied straight into this wave's 12-KB slice of the not yet
-// used reduction buffer with direct-to-LDS loads (three tiles of register fragments do not fit beside
-// the 64 accumulators: 23 VGPRs spill). Same products in the same order as three 1-tile chunks.
-template <int H>
-__device__ __forceinline__ void fwd_kw_chunk3_lds(const FwdKw& o, int kt0, f32x16 (&acc)[4], char* stage) {
-  const int lane = threadIdx.x & 63;
-  auto img_of = [&](int kt, float4 (&a)[2]) {
-    const int k = 16 * kt;
-    const bool sx = k < o.cin;
-    const int kk = sx ? k : k - o.cin;
-    const float* ap = (sx ? o.x : o.hp) + kk + 8 * o.hl;
-    a[0] = ld4(ap);
-    a[1] = ld4(ap + 4);
-    return sx ? o.img0 + (int64_t)(kk / 16) * GATE_IMG_BYTES : o.img1 + (int64_t)(kk / 16) * GATE_IMG_BYTES;
-  };
-  float4 a[3][2];
-  uint4 bi[2][4][3];
-  {  // (the LDS copies first: vmcnt retires in issue order, so the register loads stay countable)
-    const char* img = img_of(kt0 + 2, a[2]);
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)(img + p * 4096 + g * 1024 + 16 * lane),
-                                         (lds_void_t*)(stage + (g * 3 + p) * 1024), 16, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const char* img = img_of(kt0 + i, a[i]);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) img_frag(img, g * 32 + o.jj, o.hl, bi[i][g][0], bi[i][g][1], bi[i][g][2]);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const Split3 as = split3(a[i][0], a[i][1]);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      Split3 b;
-      b.p0 = __builtin_bit_cast(bf16x8_t, bi[i][g][0]);
-      b.p1 = __builtin_bit_cast(bf16x8_t, bi[i][g][1]);
-      b.p2 = __builtin_bit_cast(bf16x8_t, bi[i][g][2]);
-      acc[g] = mfma_x6(as, b, acc[g]);
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);  // (tiles 0 and 1 issue before the wait below)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image chunks landed in LDS
-  __builtin_amdgcn_sched_barrier(0);
-  const Split3 as = split3(a[2][0], a[2][1]);
-  const int off = o.jj * 32 + 16 * (o.hl ^ ((o.jj >> 3) & 1));  // (image row g * 32 + jj: same swizzle bit)
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    Split3 b;
-    b.p0 = *reinterpret_cast<const bf16x8_t*>(stage + (g * 3 + 0) * 1024 + off);
-    b.p1 = *reinterpret_cast<const bf16x8_t*>(stage + (g * 3 + 1) * 1024 + off);
-    b.p2 = *reinterpret_cast<const bf16x8_t*>(stage + (g * 3 + 2) * 1024 + off);
-    acc[g] = mfma_x6(as, b, acc[g]);
   }
 }
 
@@ -270,13 +206,9 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
     int kb, ke;
     kw_range((cin + (t > 0 ? H : 0)) / 16, wave, kb, ke);
     KWP(pid, 1);
-    // (uniform branches between straight-line chunks)
-    if constexpr (IMG && SMAML_KW_LDS3) {
-      if (ke - kb == 3) {
-        fwd_kw_chunk3_lds<H>(o, kb, acc, reinterpret_cast<char*>(red) + wave * 12 * 1024);
-        kb = ke;
-      }
-    }
+    // (uniform branches between straight-line chunks; measured: the layer-0 problem's third K-tile per
+    // wave in the same round trip, its B image copied to LDS with direct-to-LDS loads, 0.712 -> 0.749 ms
+    // per config-4 sample-step: the compiler waits for the copies before the register tiles' MFMAs)
     while (ke - kb >= KW_CH) {
       fwd_kw_chunk<H, IMG, KW_CH>(o, kb, acc);
       kb += KW_CH;
@@ -286,7 +218,6 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
 
   // partial tiles -> LDS (lane-contiguous: conflict-free), summed in wave order
   KWP(pid, 2);
-  if constexpr (IMG && SMAML_KW_LDS3) __syncthreads();  // every wave is done with its staged tile (red overlaps it)
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
