@@ -55,6 +55,19 @@ extern "C" int smaml_kw_probe(int target, unsigned long long* out, int n) {
 constexpr int KW_W = 8;   // waves per workgroup (two per SIMD)
 constexpr int KW_CH = 2;  // K-tiles per wave whose loads are in flight together (forward)
 constexpr int KW_BCH = 8; // same, BPTT (a K-tile's fragments are 16 VGPRs against the forward's 56)
+#ifndef SMAML_KW_BWD_WAVES
+#define SMAML_KW_BWD_WAVES 16  // BPTT workgroup: 8 waves (two per SIMD) or 16 (four per SIMD, half the K range
+#endif                         // each; config 4: 0.717 -> 0.698 ms per sample-step)
+#ifndef SMAML_KW_FWD_WAVES
+#define SMAML_KW_FWD_WAVES 8  // forward workgroup: 8 waves (one K range each, all 4 gates) or 16 (8 K ranges x
+#endif                        // 2 gate pairs: half the accumulators and B fragments per wave)
+constexpr int KW_FW = SMAML_KW_FWD_WAVES;
+constexpr int KW_FNG = 4 * 8 / KW_FW;  // gates per forward wave
+constexpr int KW_FRPT = 16 / KW_FW;    // forward epilogue accumulator rows per thread
+static_assert(KW_FW == 8 || KW_FW == 16, "forward waves");
+constexpr int KW_BW = SMAML_KW_BWD_WAVES;
+constexpr int KW_BRPT = 16 / KW_BW;  // epilogue accumulator rows per thread
+static_assert(KW_BW == 8 || KW_BW == 16, "BPTT waves");
 
 // Accumulator register r of lane (.., hl) holds tile row (r & 3) + 8 (r >> 2) + 4 hl; the inverse:
 __device__ __forceinline__ int kw_row(int r, int hl) { return (r & 3) + 8 * (r >> 2) + 4 * hl; }
@@ -82,11 +95,11 @@ struct FwdKw {
 
 // N K-tiles from kt0 on: every load first (no branch between them, so all are in flight together),
 // then the splits and MFMAs in K order.
-template <int H, bool IMG, int N>
-__device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, f32x16 (&acc)[4]) {
+template <int H, bool IMG, int N, int NG>
+__device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, int g0, f32x16 (&acc)[NG]) {
   float4 a[N][2];
-  uint4 bi[N][4][3];
-  float4 bf[N][4][2];
+  uint4 bi[N][NG][3];
+  float4 bf[N][NG][2];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int k = 16 * (kt0 + i);
@@ -98,13 +111,13 @@ __device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, f32x16 (&a
     if constexpr (IMG) {
       const char* img = sx ? o.img0 + (int64_t)(kk / 16) * GATE_IMG_BYTES : o.img1 + (int64_t)(kk / 16) * GATE_IMG_BYTES;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) img_frag(img, g * 32 + o.jj, o.hl, bi[i][g][0], bi[i][g][1], bi[i][g][2]);
+      for (int g = 0; g < NG; ++g) img_frag(img, (g0 + g) * 32 + o.jj, o.hl, bi[i][g][0], bi[i][g][1], bi[i][g][2]);
     } else {
       const int ws = sx ? o.cin : H;
       const float* wb = (sx ? o.wih : o.whh) + kk + 8 * o.hl;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float* wr = wb + (int64_t)g * H * ws;
+      for (int g = 0; g < NG; ++g) {
+        const float* wr = wb + (int64_t)(g0 + g) * H * ws;
         bf[i][g][0] = ld4(wr);
         bf[i][g][1] = ld4(wr + 4);
       }
@@ -115,7 +128,7 @@ __device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, f32x16 (&a
   for (int i = 0; i < N; ++i) {
     const Split3 as = split3(a[i][0], a[i][1]);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NG; ++g) {
       Split3 b;
       if constexpr (IMG) {
         b.p0 = __builtin_bit_cast(bf16x8_t, bi[i][g][0]);
@@ -130,22 +143,23 @@ __device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, f32x16 (&a
 }
 
 // Contiguous K-tile range [kb, ke) of wave `wave` out of KW_W (deterministic partition).
+template <int NW = KW_W>
 __device__ __forceinline__ void kw_range(int nkt, int wave, int& kb, int& ke) {
-  const int per = (nkt + KW_W - 1) / KW_W;
+  const int per = (nkt + NW - 1) / NW;
   kb = min(nkt, wave * per);
   ke = min(nkt, kb + per);
 }
 
 // ---- forward: tile = 32 rows x 32 units (the 4 gates: 128 gate columns) ------------------------
 template <int H, bool IMG>
-__global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restrict__ F, float* __restrict__ HsAll,
+__global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restrict__ F, float* __restrict__ HsAll,
                                                           float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                           int64_t lsz, const float* __restrict__ theta,
                                                           int64_t tstride, FwdWave wv, int T, int M, GateImgs gi,
                                                           int pid) {
   static_assert(H % 32 == 0, "32-unit groups");
   KWP(pid, 0);
-  __shared__ float red[KW_W * 64 * 64];  // [wave][gate*16 + r][lane]
+  __shared__ float red[KW_W * 64 * 64];  // [K range][gate*16 + r][lane]
   int l, t, b0;
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
@@ -162,22 +176,23 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
   float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * (4 * H);
   const float* Hp = Hz + (int64_t)(t > 0 ? t - 1 : 0) * M * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane >> 5, jj = lane & 31;
+  const int kg = wave % KW_W, g0 = (wave / KW_W) * KW_FNG;  // this wave's K range and first gate
   const int m0 = tm * 32, j = ug * 32 + jj;
 
-  // epilogue operands: this thread's elements are rows kw_row(2 wave + q, hl), unit j
-  float bs[4], cp[2];
+  // epilogue operands: this thread's elements are rows kw_row(KW_FRPT wave + q, hl), unit j
+  float bs[4], cp[KW_FRPT];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bs[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int m = min(m0 + kw_row(2 * wave + q, hl), M - 1);
+  for (int q = 0; q < KW_FRPT; ++q) {
+    const int m = min(m0 + kw_row(KW_FRPT * wave + q, hl), M - 1);
     const float v = Cz[((int64_t)(t > 0 ? t - 1 : 0) * M + m) * H + j];  // (t = 0: a valid address, selected out)
     cp[q] = t > 0 ? v : 0.f;
   }
 
-  f32x16 acc[4];
+  f32x16 acc[KW_FNG];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+  for (int g = 0; g < KW_FNG; ++g)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[g][r] = 0.f;
   {
@@ -204,30 +219,31 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_fwd_kw(const float* __restri
     o.hl = hl;
     o.jj = jj;
     int kb, ke;
-    kw_range((cin + (t > 0 ? H : 0)) / 16, wave, kb, ke);
+    kw_range((cin + (t > 0 ? H : 0)) / 16, kg, kb, ke);
     KWP(pid, 1);
     // (uniform branches between straight-line chunks; measured: the layer-0 problem's third K-tile per
     // wave in the same round trip, its B image copied to LDS with direct-to-LDS loads, 0.712 -> 0.749 ms
     // per config-4 sample-step: the compiler waits for the copies before the register tiles' MFMAs)
-    while (ke - kb >= KW_CH) {
-      fwd_kw_chunk<H, IMG, KW_CH>(o, kb, acc);
-      kb += KW_CH;
+    constexpr int CH = KW_CH;
+    while (ke - kb >= CH) {
+      fwd_kw_chunk<H, IMG, CH, KW_FNG>(o, kb, g0, acc);
+      kb += CH;
     }
-    for (; kb < ke; ++kb) fwd_kw_chunk<H, IMG, 1>(o, kb, acc);
+    for (; kb < ke; ++kb) fwd_kw_chunk<H, IMG, 1, KW_FNG>(o, kb, g0, acc);
   }
 
   // partial tiles -> LDS (lane-contiguous: conflict-free), summed in wave order
   KWP(pid, 2);
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+  for (int g = 0; g < KW_FNG; ++g)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(wave * 64 + g * 16 + r) * 64 + lane] = acc[g][r];
+    for (int r = 0; r < 16; ++r) red[(kg * 64 + (g0 + g) * 16 + r) * 64 + lane] = acc[g][r];
   __syncthreads();
   KWP(pid, 3);
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 2 * wave + q;
+  for (int q = 0; q < KW_FRPT; ++q) {
+    const int r = KW_FRPT * wave + q;
     float pre[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -307,7 +323,7 @@ __device__ __forceinline__ void bwd_kw_chunk(const BwdKw& o, int kt0, f32x16& ac
 
 // ---- BPTT: tile = 32 rows x 32 units of dh = [dG(l+1,t) | dG(l,t+1)] . [W_ih(l+1) ; W_hh(l)] -----
 template <int H, bool IMG>
-__global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, float* dGAll, float* __restrict__ dhAll,
+__global__ __launch_bounds__(64 * KW_BW) void k_lstm_bwd_kw(const float* GsAll, float* dGAll, float* __restrict__ dhAll,
                                                           const float* __restrict__ CsAll,
                                                           const float* __restrict__ dHhead, float* __restrict__ dcAll,
                                                           int64_t lsz, const float* __restrict__ theta,
@@ -316,7 +332,7 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
   static_assert(H % 32 == 0, "32-unit tiles");
   KWP(pid, 0);
   constexpr int G4 = 4 * H;
-  __shared__ float red[KW_W * 16 * 64];  // [wave][r][lane]
+  __shared__ float red[KW_BW * 16 * 64];  // [wave][r][lane]
   const int p = wave_index(wv, (int)blockIdx.x);
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
   const LayerOff lo = wave_sel(wv.lo, p);
@@ -337,12 +353,12 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane >> 5, jj = lane & 31;
   const int m0 = tm * 32, j = tn * 32 + jj;
 
-  // epilogue operands of this thread's elements (rows kw_row(2 wave + q, hl), unit j), loaded first;
-  // uniform conditions select after loads from valid addresses (no branch around a load)
-  float g[2][4], cp[2], dc[2], hd[2];
+  // epilogue operands of this thread's elements (rows kw_row(KW_BRPT wave + q, hl), unit j), loaded
+  // first; uniform conditions select after loads from valid addresses (no branch around a load)
+  float g[KW_BRPT][4], cp[KW_BRPT], dc[KW_BRPT], hd[KW_BRPT];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int m = min(m0 + kw_row(2 * wave + q, hl), M - 1);
+  for (int q = 0; q < KW_BRPT; ++q) {
+    const int m = min(m0 + kw_row(KW_BRPT * wave + q, hl), M - 1);
     const int64_t row = (int64_t)t * M + m;
 #pragma unroll
     for (int k = 0; k < 4; ++k) g[q][k] = Gz[row * G4 + k * H + j];
@@ -380,7 +396,7 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
       o.i1 = ib + ohh;
     }
     int kb, ke;
-    kw_range(((up ? 1 : 0) + (nx ? 1 : 0)) * (G4 / 16), wave, kb, ke);
+    kw_range<KW_BW>(((up ? 1 : 0) + (nx ? 1 : 0)) * (G4 / 16), wave, kb, ke);
     KWP(pid, 1);
     while (ke - kb >= KW_BCH) {
       bwd_kw_chunk<H, IMG, KW_BCH>(o, kb, acc);
@@ -399,11 +415,11 @@ __global__ __launch_bounds__(64 * KW_W) void k_lstm_bwd_kw(const float* GsAll, f
   __syncthreads();
   KWP(pid, 3);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 2 * wave + q;
+  for (int q = 0; q < KW_BRPT; ++q) {
+    const int r = KW_BRPT * wave + q;
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < KW_W; ++w) s += red[(w * 16 + r) * 64 + lane];
+    for (int w = 0; w < KW_BW; ++w) s += red[(w * 16 + r) * 64 + lane];
     const int m = m0 + kw_row(r, hl);
     if (m >= M) continue;
     const float d = s + hd[q];
@@ -436,10 +452,10 @@ void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, c
   const dim3 grid(wv.off[wv.n], 1, w.Z);
   count_variant(w, V_FWD_KW);
   if (w.gimg.th && w.gimg_src == theta) {
-    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, true><<<grid, 64 * KW_W, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, true><<<grid, 64 * KW_FW, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
                                                                                tstride, wv, d.T, w.M, w.gimg, diag)));
   } else {
-    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, false><<<grid, 64 * KW_W, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, false><<<grid, 64 * KW_FW, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
                                                                                 tstride, wv, d.T, w.M, w.gimg, diag)));
   }
 }
@@ -453,10 +469,10 @@ void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, cons
   const dim3 grid(wv.off[wv.n], 1, w.Z);
   count_variant(w, V_BWD_KW);
   if (w.bimg.th && w.bimg_src == theta) {
-    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, true><<<grid, 64 * KW_W, 0, s>>>(
+    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, true><<<grid, 64 * KW_BW, 0, s>>>(
                               w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg, 100 + e)));
   } else {
-    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, false><<<grid, 64 * KW_W, 0, s>>>(
+    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, false><<<grid, 64 * KW_BW, 0, s>>>(
                               w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.bimg, 100 + e)));
   }
 }
