@@ -16,6 +16,7 @@
 // into three bf16 pieces, six piece products per 16-k step; gemm_core.h mfma_x6), or with
 // -DSMAML_X6=0 on v_mfma_f32_32x32x2_f32. All reductions are in a fixed order (no float
 // atomics), so results are bitwise reproducible run to run and across ranks.
+#include <cmath>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -2320,6 +2321,8 @@ __global__ void k_sqsum(const float* __restrict__ g, int64_t P, double* __restri
   const int64_t per = (P + SQB - 1) / SQB;
   const int64_t b = (int64_t)blockIdx.x * per, e = b + per < P ? b + per : P;
   double acc = 0.0;
+  // (unrolled: the loads of 8 iterations in flight together; the same additions in the same order)
+#pragma unroll 8
   for (int64_t i = b + threadIdx.x; i < e; i += NT) {
     const double v = gz[i];
     acc += v * v;
@@ -2478,15 +2481,15 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
 // ====================================================================================
 // Regional adaptation step (adapt_hybrid_v5.py:196-201): clip_grad_norm_(max_norm) then
 // torch.optim.Adam with coupled L2 weight decay (g += wd * p), per-step learning rate.
+// bc1 = 1 - b1^step and bc2_sqrt = sqrt(1 - b2^step) come from the host (the step is a host integer):
+// a per-thread fp64 pow was most of this kernel's time at batch 1.
 __global__ void k_adam_l2(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                           float* __restrict__ v, int64_t n, const double* __restrict__ part, const float* __restrict__ lr_dev,
-                          int step, float b1, float b2, float eps, float wd, float max_norm) {
+                          double bc1, float bc2_sqrt, float b1, float b2, float eps, float wd, float max_norm) {
   float total;
   const float coef = clip_coef_from(part, max_norm, &total);
   const float lr = *lr_dev;
-  const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
   const float step_size = (float)((double)lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float gi = fmaf(wd, p[i], g[i] * coef);
     const float mi = m[i] + (1.f - b1) * (gi - m[i]);
@@ -2505,7 +2508,8 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
   int nb = (int)((n + NT - 1) / NT);
   if (nb > 2048) nb = 2048;
   k_sqsum<<<dim3(SQB, 1), NT, 0, s>>>(g, n, part);
-  k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, step, b1, b2, eps, wd, max_norm);
+  const double bc1 = 1.0 - std::pow((double)b1, step), bc2 = 1.0 - std::pow((double)b2, step);
+  k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, bc1, (float)std::sqrt(bc2), b1, b2, eps, wd, max_norm);
 }
 
 }  // namespace smaml

@@ -53,18 +53,24 @@ extern "C" int smaml_kw_probe(int target, unsigned long long* out, int n) {
 #endif
 
 constexpr int KW_W = 8;   // waves per workgroup (two per SIMD)
-constexpr int KW_CH = 2;  // K-tiles per wave whose loads are in flight together (forward)
 constexpr int KW_BCH = 8; // same, BPTT (a K-tile's fragments are 16 VGPRs against the forward's 56)
 #ifndef SMAML_KW_BWD_WAVES
 #define SMAML_KW_BWD_WAVES 16  // BPTT workgroup: 8 waves (two per SIMD) or 16 (four per SIMD, half the K range
 #endif                         // each; config 4: 0.717 -> 0.698 ms per sample-step)
 #ifndef SMAML_KW_FWD_WAVES
-#define SMAML_KW_FWD_WAVES 8  // forward workgroup: 8 waves (one K range each, all 4 gates) or 16 (8 K ranges x
-#endif                        // 2 gate pairs: half the accumulators and B fragments per wave)
+#define SMAML_KW_FWD_WAVES 8  // forward workgroup waves (8: two per SIMD; 16: four per SIMD, measured slower)
+#endif
+#ifndef SMAML_KW_FWD_KGROUPS
+#define SMAML_KW_FWD_KGROUPS 8  // forward K ranges; the waves split the 4 gates into FWD_WAVES / FWD_KGROUPS groups
+#endif
 constexpr int KW_FW = SMAML_KW_FWD_WAVES;
-constexpr int KW_FNG = 4 * 8 / KW_FW;  // gates per forward wave
-constexpr int KW_FRPT = 16 / KW_FW;    // forward epilogue accumulator rows per thread
-static_assert(KW_FW == 8 || KW_FW == 16, "forward waves");
+constexpr int KW_FKG = SMAML_KW_FWD_KGROUPS;
+constexpr int KW_FNG = 4 * KW_FKG / KW_FW;  // gates per forward wave
+constexpr int KW_FRPT = 16 / KW_FW;         // forward epilogue accumulator rows per thread
+static_assert((KW_FW == 8 || KW_FW == 16) && KW_FW % KW_FKG == 0 && KW_FNG >= 1 && KW_FNG <= 4, "forward waves");
+#ifndef SMAML_KW_FWD_CH
+#define SMAML_KW_FWD_CH (KW_FNG == 4 ? 2 : 6)  // K-tiles per load round trip (registers: A 8 + B 12 per gate)
+#endif
 constexpr int KW_BW = SMAML_KW_BWD_WAVES;
 constexpr int KW_BRPT = 16 / KW_BW;  // epilogue accumulator rows per thread
 static_assert(KW_BW == 8 || KW_BW == 16, "BPTT waves");
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
                                                           int pid) {
   static_assert(H % 32 == 0, "32-unit groups");
   KWP(pid, 0);
-  __shared__ float red[KW_W * 64 * 64];  // [K range][gate*16 + r][lane]
+  __shared__ float red[KW_FKG * 64 * 64];  // [K range][gate*16 + r][lane]
   int l, t, b0;
   LayerOff lo;
   wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
   float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * (4 * H);
   const float* Hp = Hz + (int64_t)(t > 0 ? t - 1 : 0) * M * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane >> 5, jj = lane & 31;
-  const int kg = wave % KW_W, g0 = (wave / KW_W) * KW_FNG;  // this wave's K range and first gate
+  const int kg = wave % KW_FKG, g0 = (wave / KW_FKG) * KW_FNG;  // this wave's K range and first gate
   const int m0 = tm * 32, j = ug * 32 + jj;
 
   // epilogue operands: this thread's elements are rows kw_row(KW_FRPT wave + q, hl), unit j
@@ -219,12 +225,12 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
     o.hl = hl;
     o.jj = jj;
     int kb, ke;
-    kw_range((cin + (t > 0 ? H : 0)) / 16, kg, kb, ke);
+    kw_range<KW_FKG>((cin + (t > 0 ? H : 0)) / 16, kg, kb, ke);
     KWP(pid, 1);
     // (uniform branches between straight-line chunks; measured: the layer-0 problem's third K-tile per
     // wave in the same round trip, its B image copied to LDS with direct-to-LDS loads, 0.712 -> 0.749 ms
     // per config-4 sample-step: the compiler waits for the copies before the register tiles' MFMAs)
-    constexpr int CH = KW_CH;
+    constexpr int CH = SMAML_KW_FWD_CH;
     while (ke - kb >= CH) {
       fwd_kw_chunk<H, IMG, CH, KW_FNG>(o, kb, g0, acc);
       kb += CH;
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
     for (int g = 0; g < 4; ++g) {
       float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < KW_W; ++w) s += red[(w * 64 + g * 16 + r) * 64 + lane];
+      for (int w = 0; w < KW_FKG; ++w) s += red[(w * 64 + g * 16 + r) * 64 + lane];
       pre[g] = s + bs[g];
     }
     const int m = m0 + kw_row(r, hl);
