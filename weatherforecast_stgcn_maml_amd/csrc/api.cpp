@@ -227,7 +227,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, 0, SMAML_SMALL_KW};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;

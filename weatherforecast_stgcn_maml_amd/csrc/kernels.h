@@ -135,6 +135,9 @@ struct Knobs {
 #ifndef SMAML_WGRAD_WS_DEFAULT
 #define SMAML_WGRAD_WS_DEFAULT 0  // k_wgrad_ws measured slower than the staged tiles in every arm
 #endif
+#ifndef SMAML_BWDD_REMAP_DEFAULT
+#define SMAML_BWDD_REMAP_DEFAULT 1  // tangent BPTT pair-segment tile order: -0.55 GB of HBM reads per launch,
+#endif                              // time-neutral (3-round A/B 1785.6 -> 1784.5 ms per meta-step)
 #ifndef SMAML_SMALL_KW
 #define SMAML_SMALL_KW 1
 #endif
