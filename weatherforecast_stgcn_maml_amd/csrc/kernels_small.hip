@@ -6,13 +6,14 @@
 // At M = 441 sequences a diagonal holds <= 4 problems x 14 row tiles x 4 unit groups of work, and
 // its time is one tile's latency chain, not throughput. The split-K pair it replaces
 // (k_lstm_*_part + k_lstm_*_cell_q, kernels.hip) spreads a tile's K over S workgroups on S CUs and
-// pays a second launch plus a partial-slab round trip through L2 per diagonal. Here one workgroup of
-// KW_W waves owns a 32-row tile; wave w accumulates the w-th contiguous K-tile range with its operands
-// loaded from global memory straight into MFMA fragments (no wave shares an operand with another,
-// so there is no LDS staging and no barrier in the K loop), the KW_W partial tiles meet in LDS and
-// are summed in wave order (deterministic), and the workgroup runs the cell epilogue. The
+// pays a second launch plus a partial-slab round trip through L2 per diagonal. Here one workgroup owns
+// a 32-row tile (forward: 8 waves, BPTT: 16); each wave accumulates one contiguous K-tile range with
+// its operands loaded from global memory straight into MFMA fragments (no wave shares an operand with
+// another, so there is no LDS staging and no barrier in the K loop), the partial tiles meet in LDS and
+// are summed in K-range order (deterministic), and the workgroup runs the cell epilogue. The
 // epilogue's own operands (bias sums, c_{t-1}; gates, carry, head dh in the BPTT) are loaded before
-// the K loop, so their latency hides under it.
+// the K loop, so their latency hides under it. The problem of a diagonal is the grid row (blockIdx.y).
+// Config 4: 1.03 -> 0.68 ms per sample-step with these kernels.
 //
 // Products: bf16x6 (gemm_core.h mfma_x6, f32-accurate). Forward B operand: the pre-split gate
 // images (launch_split_gate) read straight into fragments, or the f32 weights split in registers.
@@ -29,8 +30,9 @@ namespace smaml {
 // wave 0 of every workgroup of the launch whose id (forward diagonal, or 100 + BPTT diagonal) is the target
 __device__ int g_kwp_target = -1;
 __device__ unsigned long long g_kwp[1024][5];
-#define KWP(id, slot) \
-  if (id == g_kwp_target && threadIdx.x == 0 && blockIdx.x < 1024) g_kwp[blockIdx.x][slot] = wall_clock64()
+#define KWP(id, slot)                                                                    \
+  if (id == g_kwp_target && threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < 1024) \
+  g_kwp[blockIdx.y * gridDim.x + blockIdx.x][slot] = wall_clock64()
 // out == null: arm `target` and zero the records; else copy n workgroups' records out. Returns the wall
 // clock rate in kHz (> 0) or -1.
 extern "C" int smaml_kw_probe(int target, unsigned long long* out, int n) {
@@ -52,8 +54,9 @@ extern "C" int smaml_kw_probe(int target, unsigned long long* out, int n) {
 #define KWP(id, slot) (void)0
 #endif
 
-constexpr int KW_W = 8;   // waves per workgroup (two per SIMD)
-constexpr int KW_BCH = 8; // same, BPTT (a K-tile's fragments are 16 VGPRs against the forward's 56)
+constexpr int KW_W = 8;   // forward workgroup waves / K ranges (two waves per SIMD)
+constexpr int KW_CH = 2;  // forward: K-tiles per wave whose loads are in flight together (56 VGPRs each)
+constexpr int KW_BCH = 8; // BPTT: the same (a K-tile's fragments are 16 VGPRs)
 #ifndef SMAML_KW_BWD_WAVES
 #define SMAML_KW_BWD_WAVES 16  // BPTT workgroup: 8 waves (two per SIMD) or 16 (four per SIMD, half the K range
 #endif                         // each; config 4: 0.717 -> 0.698 ms per sample-step)
@@ -69,7 +72,7 @@ constexpr int KW_FNG = 4 * KW_FKG / KW_FW;  // gates per forward wave
 constexpr int KW_FRPT = 16 / KW_FW;         // forward epilogue accumulator rows per thread
 static_assert((KW_FW == 8 || KW_FW == 16) && KW_FW % KW_FKG == 0 && KW_FNG >= 1 && KW_FNG <= 4, "forward waves");
 #ifndef SMAML_KW_FWD_CH
-#define SMAML_KW_FWD_CH (KW_FNG == 4 ? 2 : 6)  // K-tiles per load round trip (registers: A 8 + B 12 per gate)
+#define SMAML_KW_FWD_CH (KW_FNG == 4 ? KW_CH : 6)  // K-tiles per load round trip (registers: A 8 + B 12 per gate)
 #endif
 constexpr int KW_BW = SMAML_KW_BWD_WAVES;
 constexpr int KW_BRPT = 16 / KW_BW;  // epilogue accumulator rows per thread
@@ -166,11 +169,13 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
   static_assert(H % 32 == 0, "32-unit groups");
   KWP(pid, 0);
   __shared__ float red[KW_FKG * 64 * 64];  // [K range][gate*16 + r][lane]
-  int l, t, b0;
-  LayerOff lo;
-  wave_problem(wv, (int)blockIdx.x, l, t, lo, b0);
+  // problem = blockIdx.y (not found from blockIdx.x by compares: its fields' kernel-argument loads then
+  // depend on nothing loaded and issue with the first batch)
+  const int pb = blockIdx.y;
+  const int l = wave_sel(wv.l, pb), t = wave_sel(wv.t, pb);
+  const LayerOff lo = wave_sel(wv.lo, pb);
   const int ntm = (M + 31) / 32;
-  const int bl = (int)blockIdx.x - b0;
+  const int bl = (int)blockIdx.x;
   const int tm = bl % ntm, ug = bl / ntm;  // row tiles fastest (all XCDs see every unit group)
   const int z = blockIdx.z;
   const float* th = theta + (int64_t)z * tstride;
@@ -339,12 +344,12 @@ __global__ __launch_bounds__(64 * KW_BW) void k_lstm_bwd_kw(const float* GsAll, 
   KWP(pid, 0);
   constexpr int G4 = 4 * H;
   __shared__ float red[KW_BW * 16 * 64];  // [wave][r][lane]
-  const int p = wave_index(wv, (int)blockIdx.x);
-  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p), b0 = wave_sel(wv.off, p);
+  const int p = blockIdx.y;  // (problem per grid row, as in k_lstm_fwd_kw)
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
   const int ntm = (M + 31) / 32;
-  const int bl = (int)blockIdx.x - b0;
+  const int bl = (int)blockIdx.x;
   const int tm = bl % ntm, tn = bl / ntm;
   const int z = blockIdx.z;
   const int64_t slab = (int64_t)z * T * M;
@@ -455,7 +460,7 @@ void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, c
   FwdWave wv{};
   fwd_wave(d, w, po, diag, ((w.M + 31) / 32) * (d.H / 32), false, wv);
   if (wv.n == 0) return;
-  const dim3 grid(wv.off[wv.n], 1, w.Z);
+  const dim3 grid(((w.M + 31) / 32) * (d.H / 32), wv.n, w.Z);
   count_variant(w, V_FWD_KW);
   if (w.gimg.th && w.gimg_src == theta) {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, true><<<grid, 64 * KW_FW, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
@@ -472,7 +477,7 @@ void launch_lstm_bwd_kw(hipStream_t s, const Dims& d, const Work& w, int e, cons
   BwdWave wv{};
   bwd_wave(d, w, po, e, ((w.M + 31) / 32) * (d.H / 32), false, wv);
   if (wv.n == 0) return;
-  const dim3 grid(wv.off[wv.n], 1, w.Z);
+  const dim3 grid(((w.M + 31) / 32) * (d.H / 32), wv.n, w.Z);
   count_variant(w, V_BWD_KW);
   if (w.bimg.th && w.bimg_src == theta) {
     SMAML_DISPATCH_H(d.H, (k_lstm_bwd_kw<HT, true><<<grid, 64 * KW_BW, 0, s>>>(
