@@ -249,6 +249,8 @@ struct smaml_ctx {
   int64_t gimg_cap = 0;
   char* bimg_buf = nullptr;   // pre-split BPTT weight images (prep_bwd_images; small-grid BPTT)
   int64_t bimg_cap = 0;
+  float* xg_buf = nullptr;    // small-grid forward: layer 0's hoisted input projection (run_lstm)
+  int64_t xg_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
   // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
   unsigned* bar = nullptr;
@@ -723,11 +725,40 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   const Dims& d = c->d;
   Work& w = c->w;
   TRY(prep_gate_images(c, s, theta, tstride));
+  // Batch-1 sizes (the small-grid steps): layer 0's input projection F . W_ih0^T does not depend on the
+  // recurrence, so it runs for all T steps as one throughput-bound GEMM before the wavefront and the
+  // layer-0 steps' latency-bound K loops cover only the recurrent segment (kernels_small.hip).
+  w.xg = nullptr;
+  w.xg_src = nullptr;
+  if (small_kw_ok(d, w) && (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows) {
+    const int64_t per = (int64_t)d.T * w.M * 4 * d.H, need = per * w.Z;
+    if (need > c->xg_cap) {
+      if (c->xg_buf) HIP_TRY(hipFree(c->xg_buf));
+      c->xg_buf = nullptr;
+      c->xg_cap = 0;
+      if (hipMalloc((void**)&c->xg_buf, need * 4) == hipSuccess)
+        c->xg_cap = need;
+      else
+        (void)hipGetLastError();  // no room: the layer-0 steps form the projection themselves
+    }
+    if (c->xg_buf) {
+      TIMED(c, s, C_FWD, 2.0 * w.Z * d.T * w.M * 4 * d.H * d.Hc,
+            launch_gemm_nt(s, w.F, (int64_t)d.T * w.M * d.Hc, d.T * w.M, d.Hc, theta + c->po.lay[0].wih, tstride,
+                           4 * d.H, c->xg_buf, per, w.Z));
+      w.xg = c->xg_buf;
+      w.xg_src = theta;
+    }
+  }
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
-    const double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
+    double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
+    if (w.xg)  // (the hoisted projection's flops are counted above)
+      for (int q = 0; q < wv.n; ++q)
+        if (wv.l[q] == 0) fl -= 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
     TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
   }
+  w.xg = nullptr;
+  w.xg_src = nullptr;
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1028,6 +1059,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->gcn_wimg) (void)hipFree(c->gcn_wimg);
   if (c->gimg_buf) (void)hipFree(c->gimg_buf);
   if (c->bimg_buf) (void)hipFree(c->bimg_buf);
+  if (c->xg_buf) (void)hipFree(c->xg_buf);
   if (c->bar) (void)hipFree(c->bar);
   if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);

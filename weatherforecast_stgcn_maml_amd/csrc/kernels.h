@@ -179,6 +179,9 @@ struct Work {
   int Z, B, M;
   BwdImgs bimg;            // pre-split BPTT weight images (launch_split_bwd), small-grid BPTT only
   const float* bimg_src;   // the parameter vector bimg.th was split from
+  const float* xg;         // small-grid forward: layer 0's input projection F . W_ih0^T for all steps
+                           // [Z][T][M][4H] (run_lstm), or null: the layer-0 steps form it themselves
+  const float* xg_src;     // the parameter vector xg was formed with
   GateImgs gimg;           // pre-split images of the weights the gate GEMMs read (launch_split_gate)
   const float* gimg_src;   // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src; // ... and gimg.u (the sweep's tangent direction)
@@ -470,6 +473,9 @@ void launch_gather_rows(hipStream_t s, const float* src, float* out, int rows, i
                         const float* ell_v, const int* csr_p, const int* csr_c, const float* csr_v);
 void launch_relu_mask(hipStream_t s, float* g, const float* h, int64_t n);  // g *= (h > 0)
 void launch_gemm_nn_plain(hipStream_t s, const float* A, int rows, int K, const float* W, int ncols, float* out);
+// out[z] = A[z] . W[z]^T (both K-contiguous), Z problems with the given element strides
+void launch_gemm_nt(hipStream_t s, const float* A, int64_t a_zstride, int rows, int K, const float* W,
+                    int64_t w_zstride, int ncols, float* out, int64_t o_zstride, int Z);
 void launch_sum_tasks(hipStream_t s, const float* g, int64_t P, int Z, float* out);
 void launch_broadcast(hipStream_t s, const float* theta, int64_t P, int Z, float* out);
 void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,

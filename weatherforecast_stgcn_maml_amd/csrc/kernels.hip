@@ -2312,6 +2312,40 @@ void launch_gemm_nn_plain(hipStream_t s, const float* A, int rows, int K, const 
   k_gemm_nn<<<grid, CfgNN::NTH, 0, s>>>(A, 0, rows, K, W, 0, 0, ncols, out, 0);
 }
 
+// out[z] = A[z] . W[z]^T, both operands K-contiguous ([rows][K], [ncols][K]); the batch-1 forward's
+// hoisted layer-0 input projection (XG[t*M + m][n] = F[t][m] . W_ih0[n] for all T steps in one
+// throughput-bound launch instead of inside every latency-bound wavefront diagonal). CfgGateP tiles.
+__global__ __launch_bounds__(CfgGateP::NTH) void k_gemm_nt(const float* __restrict__ A, int64_t a_zstride, int rows,
+                                                         int K, const float* __restrict__ W, int64_t w_zstride,
+                                                         int ncols, float* __restrict__ out, int64_t o_zstride) {
+  __shared__ float smem[CfgGateP::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  const int m0 = blockIdx.x * CfgGateP::BM, n0 = blockIdx.y * CfgGateP::BN;
+  Acc<CfgGateP> acc;
+  acc.zero();
+  gemm_mainloop<CfgGateP>(RowMajorKC{A + (int64_t)z * a_zstride, rows, K}, RowMajorKC{W + (int64_t)z * w_zstride, ncols, K},
+                          m0, n0, 0, K, acc, smem);
+  float* o = out + (int64_t)z * o_zstride;
+#pragma unroll
+  for (int i = 0; i < CfgGateP::WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < CfgGateP::WTN; ++j) {
+      const int c = n0 + acc_col<CfgGateP>(j);
+      if (c >= ncols) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + acc_row<CfgGateP>(i, r);
+        if (row < rows) o[(int64_t)row * ncols + c] = acc.v[i][j][r];
+      }
+    }
+}
+
+void launch_gemm_nt(hipStream_t s, const float* A, int64_t a_zstride, int rows, int K, const float* W,
+                    int64_t w_zstride, int ncols, float* out, int64_t o_zstride, int Z) {
+  dim3 grid((rows + CfgGateP::BM - 1) / CfgGateP::BM, (ncols + CfgGateP::BN - 1) / CfgGateP::BN, Z);
+  k_gemm_nt<<<grid, CfgGateP::NTH, 0, s>>>(A, a_zstride, rows, K, W, w_zstride, ncols, out, o_zstride);
+}
+
 // ====================================================================================
 // clip_grad_norm_ + SGD, per task z. Squared norm accumulated in fp64, fixed order.
 __global__ void k_sqsum(const float* __restrict__ g, int64_t P, double* __restrict__ part) {

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
                                                           float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                           int64_t lsz, const float* __restrict__ theta,
                                                           int64_t tstride, FwdWave wv, int T, int M, GateImgs gi,
-                                                          int pid) {
+                                                          const float* __restrict__ XG, int pid) {
   static_assert(H % 32 == 0, "32-unit groups");
   KWP(pid, 0);
   __shared__ float red[KW_FKG * 64 * 64];  // [K range][gate*16 + r][lane]
@@ -190,13 +190,22 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
   const int kg = wave % KW_FKG, g0 = (wave / KW_FKG) * KW_FNG;  // this wave's K range and first gate
   const int m0 = tm * 32, j = ug * 32 + jj;
 
+  // layer 0 with the input projection hoisted (XG = F . W_ih0^T for all steps, run_lstm): its K loop
+  // covers only the recurrent segment and the epilogue adds XG
+  const bool hx = XG != nullptr && l == 0;
   // epilogue operands: this thread's elements are rows kw_row(KW_FRPT wave + q, hl), unit j
-  float bs[4], cp[KW_FRPT];
+  float bs[4], cp[KW_FRPT], xg[KW_FRPT][4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bs[g] = th[lo.bih + g * H + j] + th[lo.bhh + g * H + j];
 #pragma unroll
   for (int q = 0; q < KW_FRPT; ++q) {
     const int m = min(m0 + kw_row(KW_FRPT * wave + q, hl), M - 1);
+    const float* xr = (hx ? XG + (slab + (int64_t)t * M + m) * (4 * H) : th) + j;  // (not hx: a valid address)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float v = xr[g * H];
+      xg[q][g] = hx ? v : 0.f;
+    }
     const float v = Cz[((int64_t)(t > 0 ? t - 1 : 0) * M + m) * H + j];  // (t = 0: a valid address, selected out)
     cp[q] = t > 0 ? v : 0.f;
   }
@@ -230,7 +239,11 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
     o.hl = hl;
     o.jj = jj;
     int kb, ke;
-    kw_range<KW_FKG>((cin + (t > 0 ? H : 0)) / 16, kg, kb, ke);
+    kw_range<KW_FKG>(((hx ? 0 : cin) + (t > 0 ? H : 0)) / 16, kg, kb, ke);
+    if (hx) {  // (K-tile indices past the input segment: the recurrent one)
+      kb += cin / 16;
+      ke += cin / 16;
+    }
     KWP(pid, 1);
     // (uniform branches between straight-line chunks; measured: the layer-0 problem's third K-tile per
     // wave in the same round trip, its B image copied to LDS with direct-to-LDS loads, 0.712 -> 0.749 ms
@@ -261,7 +274,7 @@ __global__ __launch_bounds__(64 * KW_FW) void k_lstm_fwd_kw(const float* __restr
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < KW_FKG; ++w) s += red[(w * 64 + g * 16 + r) * 64 + lane];
-      pre[g] = s + bs[g];
+      pre[g] = s + bs[g] + xg[q][g];
     }
     const int m = m0 + kw_row(r, hl);
     if (m >= M) continue;
@@ -462,12 +475,13 @@ void launch_lstm_fwd_kw(hipStream_t s, const Dims& d, const Work& w, int diag, c
   if (wv.n == 0) return;
   const dim3 grid(((w.M + 31) / 32) * (d.H / 32), wv.n, w.Z);
   count_variant(w, V_FWD_KW);
+  const float* xg = w.xg && w.xg_src == theta ? w.xg : nullptr;
   if (w.gimg.th && w.gimg_src == theta) {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, true><<<grid, 64 * KW_FW, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
-                                                                               tstride, wv, d.T, w.M, w.gimg, diag)));
+                                                                               tstride, wv, d.T, w.M, w.gimg, xg, diag)));
   } else {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_kw<HT, false><<<grid, 64 * KW_FW, 0, s>>>(w.F, w.Hs, w.Cs, w.Gs, lsz, theta,
-                                                                                tstride, wv, d.T, w.M, w.gimg, diag)));
+                                                                                tstride, wv, d.T, w.M, w.gimg, xg, diag)));
   }
 }
 
