@@ -2314,27 +2314,31 @@ void launch_gemm_nn_plain(hipStream_t s, const float* A, int rows, int K, const 
 
 // out[z] = A[z] . W[z]^T, both operands K-contiguous ([rows][K], [ncols][K]); the batch-1 forward's
 // hoisted layer-0 input projection (XG[t*M + m][n] = F[t][m] . W_ih0[n] for all T steps in one
-// throughput-bound launch instead of inside every latency-bound wavefront diagonal). CfgGateP tiles.
-__global__ __launch_bounds__(CfgGateP::NTH) void k_gemm_nt(const float* __restrict__ A, int64_t a_zstride, int rows,
-                                                         int K, const float* __restrict__ W, int64_t w_zstride,
-                                                         int ncols, float* __restrict__ out, int64_t o_zstride) {
-  __shared__ float smem[CfgGateP::SMEM_FLOATS];
+// throughput-bound launch instead of inside every latency-bound wavefront diagonal).
+#ifndef SMAML_GEMM_NT_BIG
+#define SMAML_GEMM_NT_BIG 0  // k_gemm_nt tiles: 0 = CfgGateP (128 x 128, 4 waves), 1 = CfgGate (256 x 128, 8 waves)
+#endif
+using CfgNT2 = std::conditional_t<SMAML_GEMM_NT_BIG != 0, CfgGate, CfgGateP>;
+__global__ __launch_bounds__(CfgNT2::NTH) void k_gemm_nt(const float* __restrict__ A, int64_t a_zstride, int rows,
+                                                       int K, const float* __restrict__ W, int64_t w_zstride,
+                                                       int ncols, float* __restrict__ out, int64_t o_zstride) {
+  __shared__ float smem[CfgNT2::SMEM_FLOATS];
   const int z = blockIdx.z;
-  const int m0 = blockIdx.x * CfgGateP::BM, n0 = blockIdx.y * CfgGateP::BN;
-  Acc<CfgGateP> acc;
+  const int m0 = blockIdx.x * CfgNT2::BM, n0 = blockIdx.y * CfgNT2::BN;
+  Acc<CfgNT2> acc;
   acc.zero();
-  gemm_mainloop<CfgGateP>(RowMajorKC{A + (int64_t)z * a_zstride, rows, K}, RowMajorKC{W + (int64_t)z * w_zstride, ncols, K},
-                          m0, n0, 0, K, acc, smem);
+  gemm_mainloop<CfgNT2>(RowMajorKC{A + (int64_t)z * a_zstride, rows, K}, RowMajorKC{W + (int64_t)z * w_zstride, ncols, K},
+                        m0, n0, 0, K, acc, smem);
   float* o = out + (int64_t)z * o_zstride;
 #pragma unroll
-  for (int i = 0; i < CfgGateP::WTM; ++i)
+  for (int i = 0; i < CfgNT2::WTM; ++i)
 #pragma unroll
-    for (int j = 0; j < CfgGateP::WTN; ++j) {
-      const int c = n0 + acc_col<CfgGateP>(j);
+    for (int j = 0; j < CfgNT2::WTN; ++j) {
+      const int c = n0 + acc_col<CfgNT2>(j);
       if (c >= ncols) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + acc_row<CfgGateP>(i, r);
+        const int row = m0 + acc_row<CfgNT2>(i, r);
         if (row < rows) o[(int64_t)row * ncols + c] = acc.v[i][j][r];
       }
     }
@@ -2342,8 +2346,8 @@ __global__ __launch_bounds__(CfgGateP::NTH) void k_gemm_nt(const float* __restri
 
 void launch_gemm_nt(hipStream_t s, const float* A, int64_t a_zstride, int rows, int K, const float* W,
                     int64_t w_zstride, int ncols, float* out, int64_t o_zstride, int Z) {
-  dim3 grid((rows + CfgGateP::BM - 1) / CfgGateP::BM, (ncols + CfgGateP::BN - 1) / CfgGateP::BN, Z);
-  k_gemm_nt<<<grid, CfgGateP::NTH, 0, s>>>(A, a_zstride, rows, K, W, w_zstride, ncols, out, o_zstride);
+  dim3 grid((rows + CfgNT2::BM - 1) / CfgNT2::BM, (ncols + CfgNT2::BN - 1) / CfgNT2::BN, Z);
+  k_gemm_nt<<<grid, CfgNT2::NTH, 0, s>>>(A, a_zstride, rows, K, W, w_zstride, ncols, out, o_zstride);
 }
 
 // ====================================================================================
