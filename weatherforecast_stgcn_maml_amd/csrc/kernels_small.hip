@@ -151,7 +151,7 @@ __device__ __forceinline__ void fwd_kw_chunk(const FwdKw& o, int kt0, int g0, f3
   }
 }
 
-// Contiguous K-tile range [kb, ke) of wave `wave` out of KW_W (deterministic partition).
+// Contiguous K-tile range [kb, ke) of K range `wave` out of NW (deterministic partition).
 template <int NW = KW_W>
 __device__ __forceinline__ void kw_range(int nkt, int wave, int& kb, int& ke) {
   const int per = (nkt + NW - 1) / NW;
