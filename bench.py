@@ -439,6 +439,14 @@ def main():
         q = torch.tensor([qsum], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(q)
         qmse = float(q.item()) / args.tasks
+        if backend == "nccl" and os.environ.get("SMAML_BENCH_CAPI_COMM", "1") != "0":
+            # after the timed region: the C ABI's own RCCL communicator (smaml_comm_*) across
+            # the same ranks, on a buffer the size of the meta-step's one all-reduce
+            from weatherforecast_stgcn_maml_amd.distributed import capi_comm_check
+            try:
+                comm["capi_comm_check"] = capi_comm_check(ml.ctx, ml.theta.numel() + 64)
+            except Exception as e:  # noqa: BLE001 - reported in the line; the headline is already measured
+                comm["capi_comm_check"] = {"status": f"error: {e}", "world": world}
 
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed

@@ -304,7 +304,11 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "small_kw":                    small-grid (batch-1) LSTM forward / BPTT diagonals as one launch
  *                                  with the K reduction split over the waves of a workgroup (1; 2 =
  *                                  also with pre-split BPTT weight images), or as the split-K part +
- *                                  cell launch pair (0). */
+ *                                  cell launch pair (0);
+ *   "adapt_gcn_batch":             smaml_adapt_steps fills its per-window GCN feature cache up front,
+ *                                  runs of up to this many consecutive missing windows per GCN pass
+ *                                  (default 32; 0 or 1 = one window per step as it is first read;
+ *                                  bitwise equal). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -124,3 +124,31 @@ def test_adaptation_n441_matches_oracle(small_kw):
         assert rel(got[k].cpu().numpy(), ref_p[k].numpy()) < 1e-5, k
     assert abs(res.val_loss - ref_val) < 1e-5 * ref_val
 
+
+
+def test_adaptation_cache_fill_batched_bitwise():
+    """The adaptation feature cache filled up front in runs of consecutive windows, each run as one
+    GCN pass over single-window tasks (api.cpp ad_cache_fill, option adapt_gcn_batch), against the
+    per-step fill (adapt_gcn_batch 0): bitwise the same features, so bitwise the same adaptation
+    (config-4 shapes, 2 epochs over 16 shuffled windows; runs of 16 and of <= 3 windows)."""
+    from weatherforecast_stgcn_maml_amd import _capi
+    from weatherforecast_stgcn_maml_amd.config import CONFIG2
+
+    d = CONFIG2
+    P = synth.init_params(23, d, gcn_bias_scale=0.1)
+    tr, gcn = _split(P)
+    lats, lons = synth.region_grid()
+    ei = build_spatial_graph(lats, lons, 4)[0]
+    feats = synth.make_features(3300, d.num_nodes, synth.t_total_for(20))
+    out = {}
+    for nb in (0, 32, 3):
+        ctx = _capi.Context(d, 0)
+        ctx.set_option("adapt_gcn_batch", nb)
+        torch.manual_seed(9)
+        res = adapt(d, feats, ei, {k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, tr, "Moscow",
+                    epochs=2, device="cuda:0", ctx=ctx)
+        out[nb] = (res.theta.cpu().numpy(), res.epoch_losses, res.val_loss)
+        ctx.close()
+    for nb in (32, 3):
+        assert np.array_equal(out[nb][0], out[0][0]), nb
+        assert out[nb][1] == out[0][1] and out[nb][2] == out[0][2], nb

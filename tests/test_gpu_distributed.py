@@ -70,6 +70,50 @@ def _run(world, tasks):
     return res
 
 
+def _comm_main(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    from weatherforecast_stgcn_maml_amd import _capi
+    from weatherforecast_stgcn_maml_amd.config import CONFIG1
+    from weatherforecast_stgcn_maml_amd.distributed import capi_comm_check
+
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    ctx = _capi.Context(CONFIG1, rank)
+    out_q.put((rank, capi_comm_check(ctx, 1 << 20, iters=3)))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_capi_rccl_communicator(world):
+    """The C ABI's own RCCL communicator (smaml_comm_unique_id / init / allreduce / destroy,
+    include/smaml.h) through distributed.capi_comm_check, the collective a non-torch host binds
+    for the outer step (train_hybrid_maml_v5.py:174-179); bench.py runs the same check at every
+    N>1. RCCL rejects two ranks on one device ("Duplicate GPU detected"), so world 2 needs a box
+    with two GPUs; world 1 runs the same id exchange, init, all-reduce and destroy."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < world:
+        pytest.skip(f"{n} GPU(s) visible: RCCL needs one GPU per rank")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, r in res:
+        assert r["status"] == "ok", r
+        assert r["world"] == world and r["elements"] == 1 << 20 and r["allreduce_ms"] > 0
+
+
 @pytest.mark.parametrize("tasks", [4, 1])
 def test_two_rank_meta_learner_matches_one_rank(tasks):
     """tasks = 1: rank 1 holds no task; it still joins the one all-reduce with zeros and takes

@@ -263,6 +263,7 @@ struct smaml_ctx {
   float* ad_F = nullptr;
   int64_t ad_cap = 0;              // windows the cache holds
   std::vector<uint8_t> ad_valid;   // per window start
+  int ad_gcn_batch = 32;           // windows per GCN pass when filling the cache (<= 1: one per step)
   float *Hs_main = nullptr, *Cs_main = nullptr, *Gs_main = nullptr;  // the workspace's own activations
   // primal of the last inner steps kept for the second-order sweep (ensure_keep): slot 0 adds
   // dG + dh to the workspace's Hs/Cs/Gs, slot i >= 1 holds Hs/Cs/Gs/dG/dh of its own
@@ -784,12 +785,15 @@ int run_backward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstrid
   const ParamOff& po = c->po;
   const int64_t TM = (int64_t)d.T * w.M;
   const int64_t lsz = (int64_t)w.Z * TM * d.H;
-  TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
+  // batch-1 sizes without LSTM dropout: dh_T comes from the head's weight-gradient launch
+  const bool dh_fused = head_small(d, w.M) && !w.drop.lstm();
+  if (!dh_fused) TIMED(c, s, C_HEAD_DH, 2.0 * w.Z * w.M * d.HfC * d.H, launch_head_dh(s, d, w, theta, tstride, po));
   int64_t hz = 0;
   const float* hT = head_input(d, w, false, &hz);  // h_T, or drop(h_T) under dropout
   if (head_small(d, w.M)) {
-    TIMED(c, s, C_WGRAD, 2.0 * w.Z * w.M * d.HfC * d.H,
-          launch_head_wgrad_small(s, d, w, w.dpred, hT, hz, grad, po.P, po.wo, po.bo));
+    TIMED(c, s, C_WGRAD, (dh_fused ? 4.0 : 2.0) * w.Z * w.M * d.HfC * d.H,
+          launch_head_wgrad_small(s, d, w, w.dpred, hT, hz, grad, po.P, po.wo, po.bo, dh_fused ? theta : nullptr,
+                                  tstride));
     return run_bptt(c, s, theta, tstride, grad);
   }
   timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, hT, hz, d.H, nullptr, 0, 0,
@@ -1430,6 +1434,35 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   return SMAML_OK;
 }
 
+// Fill the adaptation feature cache for every window this call reads that it does not hold yet
+// (frozen GCN, F2): the missing windows in runs of consecutive starts, each run as ONE GCN pass over
+// Z = run-length single-window "tasks" (B = 1), whose [Z][T][N][Hc] output is exactly the run's
+// cache slots. Per-row GCN arithmetic does not depend on how many samples a launch holds, so the
+// features are bitwise those of the per-step fill (the first epoch no longer runs 960 batch-1 GCNs).
+static int ad_cache_fill(smaml_ctx* c, hipStream_t s, const int32_t* windows, int64_t n) {
+  const Dims& d = c->d;
+  const int64_t fsz = (int64_t)d.T * d.N * d.Hc;
+  std::vector<int32_t> need;
+  for (int64_t i = 0; i < n; ++i)
+    if (!c->ad_valid[windows[i]]) need.push_back(windows[i]);
+  if (need.empty()) return SMAML_OK;
+  std::sort(need.begin(), need.end());
+  need.erase(std::unique(need.begin(), need.end()), need.end());
+  std::vector<const float*> ptrs(need.size());
+  for (size_t i = 0; i < need.size(); ++i) ptrs[i] = c->feats[0] + (int64_t)need[i] * d.N * d.Cin0;
+  TRY(upload_xtab(c, s, ptrs.data(), (int64_t)ptrs.size()));
+  for (size_t i = 0; i < need.size();) {
+    size_t j = i + 1;
+    while (j < need.size() && need[j] == need[j - 1] + 1 && (int)(j - i) < c->ad_gcn_batch) ++j;
+    set_work(c, (int)(j - i), 1);
+    c->w.F = c->ad_F + (int64_t)need[i] * fsz;
+    TRY(run_gcn(c, s, c->xtab + i));
+    for (size_t k = i; k < j; ++k) c->ad_valid[need[k]] = 1;
+    i = j;
+  }
+  return SMAML_OK;
+}
+
 int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float* v, int32_t step0, int32_t nsteps,
                       int32_t batch, const int32_t* windows_host, const float* lr_dev, float beta1, float beta2,
                       float eps, float weight_decay, float max_norm, float* losses) {
@@ -1441,8 +1474,6 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
   hipStream_t s = (hipStream_t)stream;
   const Dims& d = c->d;
   const int B = batch;
-  TRY(reserve(c, 1, B));
-  set_work(c, 1, B);
   const int64_t nptr = (int64_t)nsteps * B;
   std::vector<const float*> ptrs(nptr);
   for (int64_t i = 0; i < nptr; ++i) {
@@ -1450,7 +1481,10 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     if (wv < 0 || wv + d.T + d.Hf >= c->t_total[0]) return fail(SMAML_EINVAL, "window start out of range");
     ptrs[i] = c->feats[0] + (int64_t)wv * d.N * d.Cin0;
   }
-  TRY(upload_xtab(c, s, ptrs.data(), nptr));
+  // (the cache fill's GCN passes run ad_gcn_batch windows as tasks: size the workspace for them
+  // first, since a growing workspace drops the cache)
+  const bool fill_batched = B == 1 && !(c->p_gcn > 0.f) && c->ad_gcn_batch > 1;
+  TRY(reserve(c, fill_batched ? c->ad_gcn_batch : 1, B));
   const int64_t P = c->po.P;
   const float inv = 1.f / ((float)d.N * d.HfC * B);
   const bool dropout = c->p_gcn > 0.f || c->p_lstm > 0.f;
@@ -1471,6 +1505,9 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     }
   }
   cache = cache && c->ad_F;
+  if (cache && fill_batched) TRY(ad_cache_fill(c, s, windows_host, nsteps));
+  set_work(c, 1, B);
+  TRY(upload_xtab(c, s, ptrs.data(), nptr));
   for (int k = 0; k < nsteps; ++k) {
     const float* const* xt = c->xtab + (int64_t)k * B;
     if (dropout) set_step_drop(c, step0 + k);
@@ -1486,11 +1523,11 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
       TRY(run_forward(c, s, theta, 0, xt));
     }
     TIMED(c, s, C_HEAD, 2.0 * c->w.M * d.HfC * d.H, launch_head_loss(s, d, c->w, theta, 0, c->po, xt, 2.f * inv, true));
-    TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + k));
     TRY(run_backward(c, s, theta, 0, c->grad));
+    // (the step's loss is summed by the Adam launch's block 0: the backward leaves the head's partials alone)
     TIMED(c, s, C_MISC, 0,
           launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
-                         weight_decay, max_norm));
+                         weight_decay, max_norm, c->w.lpart, c->w.lblocks, inv, losses + k));
   }
   c->w.F = c->F_main;
   c->w.drop = Drop{};
@@ -1563,6 +1600,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bwdd_remap = (int)value;
   } else if (k == "small_kw" && value >= 0 && value <= 2) {
     c->kn.small_kw = (int)value;
+  } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
+    c->ad_gcn_batch = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {
     c->kn.wgrad_group_wgs = (int)std::min<int64_t>(value, 1 << 20);
   } else if (k == "grid_barrier" && (value == 0 || value == 1)) {

@@ -384,8 +384,10 @@ void launch_loss_final(hipStream_t s, const Work& w, float inv_count, float* out
 bool head_small(const Dims& d, int M);
 int head_lblocks(const Dims& d, int M);  // loss partials per task written by the head launch
 // head weight gradient (dWo, dbo) for head_small() sizes; overwrites
+// theta != null: the same launch also writes the top layer's dh_T = dpred . Wo into w.dH (no LSTM dropout)
 void launch_head_wgrad_small(hipStream_t s, const Dims& d, const Work& w, const float* dpred, const float* hT,
-                             int64_t hz, float* grad, int64_t P, int64_t wo, int64_t bo);
+                             int64_t hz, float* grad, int64_t P, int64_t wo, int64_t bo, const float* theta,
+                             int64_t tstride);
 // dst[z] = drop(src[z]) with the head-input mask ([M][H] rows per task; src == dst allowed)
 void launch_drop_rows(hipStream_t s, const Work& w, int H, const float* src, int64_t src_zstride, float* dst);
 // x[i] = drop(x[i]) in place with the GCN-output masks (kind 1, `layer`, step 0, task 0, sample 0):
@@ -482,8 +484,10 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
                   float lr, float b1, float b2, float eps, float wd, float step_size, float bc2_sqrt,
                   float max_norm, float* norm_out);
 
+// loss != null: block 0 also writes the step's loss from the head's partials (launch_loss_final's sum)
 void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
-                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm);
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm,
+                    const float* lpart, int lblocks, float inv_count, float* loss);
 
 // ---- second-order launchers (kernels_dual.hip) ----
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,

@@ -924,13 +924,28 @@ static int head_small_threads(const Dims& d) { return d.HfC > 64 ? 128 : 64; }
 // dWo[c][j] = sum_m dpred[m][c] h_T[m][j], dbo[c] = sum_m dpred[m][c] for small M: one workgroup
 // per output row c, HW row groups x H units; each row group sums its contiguous share of the rows
 // in order, then the groups are added in a fixed order through LDS (deterministic).
+// With theta (no LSTM dropout): blocks HfC .. also form the top layer's dh_T = dpred . Wo into dH
+// [Z][M][H], HWG rows per block, one thread per (row, unit) -- the head's two backward products in
+// one launch instead of this kernel plus a k_gemm_nn (launch_head_dh) at batch-1 sizes.
 constexpr int HWG = 8;  // row groups
 __global__ __launch_bounds__(1024) void k_head_wgrad_small(const float* __restrict__ dpred, int64_t dp_zstride,
                                                          const float* __restrict__ hT, int64_t hz, int M, int H,
                                                          int HfC, float* __restrict__ grad, int64_t P, int64_t wo,
-                                                         int64_t bo) {
+                                                         int64_t bo, const float* __restrict__ theta, int64_t tstride,
+                                                         float* __restrict__ dH) {
   __shared__ float red[HWG][SMAML_HEAD_MAX_H + 1];
   const int c = blockIdx.x, z = blockIdx.y, j = threadIdx.x % H, rg = threadIdx.x / H;
+  if (c >= HfC) {  // dh_T rows (uniform per block: no barrier below is skipped by part of a block)
+    const int m = (c - HfC) * HWG + rg;
+    if (m >= M) return;
+    const float* dp = dpred + (int64_t)z * dp_zstride + (int64_t)m * HfC;
+    const float* W = theta + (int64_t)z * tstride + wo + j;
+    float a = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < HfC; ++k) a = fmaf(dp[k], W[(int64_t)k * H], a);
+    dH[((int64_t)z * M + m) * H + j] = a;
+    return;
+  }
   const float* dp = dpred + (int64_t)z * dp_zstride + c;
   const float* h = hT + (int64_t)z * hz + j;
   const int per = (M + HWG - 1) / HWG, mb = rg * per, me = min(M, mb + per);
@@ -959,9 +974,11 @@ __global__ __launch_bounds__(1024) void k_head_wgrad_small(const float* __restri
 }
 
 void launch_head_wgrad_small(hipStream_t s, const Dims& d, const Work& w, const float* dpred, const float* hT,
-                             int64_t hz, float* grad, int64_t P, int64_t wo, int64_t bo) {
-  k_head_wgrad_small<<<dim3(d.HfC, w.Z), HWG * d.H, 0, s>>>(dpred, (int64_t)w.M * d.HfC, hT, hz, w.M, d.H, d.HfC,
-                                                           grad, P, wo, bo);
+                             int64_t hz, float* grad, int64_t P, int64_t wo, int64_t bo, const float* theta,
+                             int64_t tstride) {
+  const int dh_blocks = theta ? (w.M + HWG - 1) / HWG : 0;
+  k_head_wgrad_small<<<dim3(d.HfC + dh_blocks, w.Z), HWG * d.H, 0, s>>>(
+      dpred, (int64_t)w.M * d.HfC, hT, hz, w.M, d.H, d.HfC, grad, P, wo, bo, theta, tstride, w.dH);
 }
 
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
@@ -2523,7 +2540,15 @@ void launch_adamw(hipStream_t s, float* p, const float* g, float* m, float* v, i
 // a per-thread fp64 pow was most of this kernel's time at batch 1.
 __global__ void k_adam_l2(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                           float* __restrict__ v, int64_t n, const double* __restrict__ part, const float* __restrict__ lr_dev,
-                          double bc1, float bc2_sqrt, float b1, float b2, float eps, float wd, float max_norm) {
+                          double bc1, float bc2_sqrt, float b1, float b2, float eps, float wd, float max_norm,
+                          const float* __restrict__ lpart, int lblocks, float inv_count, float* __restrict__ loss) {
+  if (loss && blockIdx.x == 0) {  // the step's loss from the head's partials: k_loss_final's sum, same order
+    __shared__ float red[NT / 64];
+    float a = 0.f;
+    for (int i = threadIdx.x; i < lblocks; i += NT) a += lpart[i];
+    const float s = block_sum(a, red);
+    if (threadIdx.x == 0) *loss = s * inv_count;
+  }
   float total;
   const float coef = clip_coef_from(part, max_norm, &total);
   const float lr = *lr_dev;
@@ -2542,12 +2567,14 @@ __global__ void k_adam_l2(float* __restrict__ p, const float* __restrict__ g, fl
 // blocks, the element update -- took 81 us per sample-step against 23 for these two launches,
 // profiles/r04_rocprof_adapt_kw.md: 512 arrivals on one counter cost more than a launch boundary)
 void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v, int64_t n, double* part,
-                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm) {
+                    const float* lr_dev, int step, float b1, float b2, float eps, float wd, float max_norm,
+                    const float* lpart, int lblocks, float inv_count, float* loss) {
   int nb = (int)((n + NT - 1) / NT);
   if (nb > 2048) nb = 2048;
   k_sqsum<<<dim3(SQB, 1), NT, 0, s>>>(g, n, part);
   const double bc1 = 1.0 - std::pow((double)b1, step), bc2 = 1.0 - std::pow((double)b2, step);
-  k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, bc1, (float)std::sqrt(bc2), b1, b2, eps, wd, max_norm);
+  k_adam_l2<<<nb, NT, 0, s>>>(p, g, m, v, n, part, lr_dev, bc1, (float)std::sqrt(bc2), b1, b2, eps, wd, max_norm,
+                              lpart, lblocks, inv_count, loss);
 }
 
 }  // namespace smaml

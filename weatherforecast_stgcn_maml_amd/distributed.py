@@ -43,6 +43,53 @@ def reduce_meta(buf: torch.Tensor, group=None):
     dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
 
 
+def capi_comm_check(ctx, n: int, iters: int = 10) -> dict:
+    """Drive the C ABI's own RCCL communicator (``smaml_comm_*``, include/smaml.h: the
+    collective a non-torch host binds for train_hybrid_maml_v5.py:174-179's outer step) across
+    the ranks of the initialised torch.distributed group, one GPU per rank: rank 0's unique id
+    travels over the torch group, every rank all-reduces a length-``n`` f32 buffer holding
+    rank + 1 through the C ABI, and the result must be world * (world + 1) / 2 everywhere.
+    Returns {"status", "world", "elements", "allreduce_ms"} (status "ok" or the error text).
+    RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so this needs world GPUs."""
+    from . import _capi
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", ctx.device)
+    # every rank must reach ncclCommInitRank, or the others block in it: agree first that
+    # librccl resolved everywhere (smaml_comm_unique_id dlopens it)
+    try:
+        uid = _capi.comm_unique_id()
+        ok = 1
+    except Exception as e:  # noqa: BLE001 - reported, not raised
+        uid, ok, err = b"", 0, str(e)
+    flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not int(flag.item()):
+        return {"status": f"error: librccl unavailable on some rank ({err if not ok else 'other rank'})",
+                "world": world}
+    box = [uid]
+    dist.broadcast_object_list(box, src=0, device=dev)
+    ctx.comm_init(rank, world, box[0])
+    try:
+        s = torch.cuda.current_stream(dev)
+        buf = torch.full((n,), float(rank + 1), dtype=torch.float32, device=dev)
+        ctx.comm_allreduce(s.cuda_stream, buf)
+        torch.cuda.synchronize(dev)
+        want = world * (world + 1) / 2
+        good = bool(torch.all(buf == want).item())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(iters):
+            ctx.comm_allreduce(s.cuda_stream, buf)
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        ms = max_over_ranks(e0.elapsed_time(e1) / iters, dev)
+        good = int(min_over_ranks(float(good), dev)) == 1
+    finally:
+        ctx.comm_destroy()
+    return {"status": "ok" if good else "error: wrong sum", "world": world, "elements": n, "allreduce_ms": ms}
+
+
 def max_over_ranks(x: float, device) -> float:
     if not active():
         return x
