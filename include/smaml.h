@@ -268,7 +268,7 @@ int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* cou
 /* Launch counts per kernel variant (tile configuration) since the last reset, in the order of
  * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
  * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
- * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw.
+ * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw, gcn_dedup.
  * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
  * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
@@ -308,7 +308,11 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "adapt_gcn_batch":             smaml_adapt_steps fills its per-window GCN feature cache up front,
  *                                  runs of up to this many consecutive missing windows per GCN pass
  *                                  (default 32; 0 or 1 = one window per step as it is first read;
- *                                  bitwise equal). */
+ *                                  bitwise equal);
+ *   "gcn_dedup":                   smaml_meta_step steps whose every task reads B consecutive windows
+ *                                  run the fused GCN rows t >= 1 once per distinct stream row and
+ *                                  store each to every (sample, step) holding it (1, the default;
+ *                                  bitwise equal to 0, which computes every sample's rows). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

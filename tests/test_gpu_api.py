@@ -494,11 +494,13 @@ def test_stgcn_autograd_matches_oracle(d, p):
     assert rel(xg.grad.cpu(), xt.grad) < 1e-4
 
 
-@pytest.mark.parametrize("knob", ["bwdd_remap"])
+@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup"])
 def test_order_only_knobs_bitwise(knob):
-    """Knobs that only reorder work between workgroups (bwdd_remap: the tangent BPTT's pair-segment
-    tile order per XCD) leave every tile's arithmetic unchanged: a second-order meta-step (big tangent
-    BPTT tiles forced, every primal kept) is bitwise equal with the knob on and off."""
+    """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
+    order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
+    stored to every sample holding them) leave every row's arithmetic unchanged: a second-order
+    meta-step (big tangent BPTT tiles forced, every primal kept) is bitwise equal with the knob on and
+    off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
@@ -517,6 +519,8 @@ def test_order_only_knobs_bitwise(knob):
         res = ml.meta_step()
         vc = ml.ctx.variant_counts()
         assert vc["bwd_dual_big_kept"] > 0, vc
+        if knob == "gcn_dedup":
+            assert (vc["gcn_dedup"] > 0) == bool(on), vc
         out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
         del ml
     for a, b in zip(out[0], out[1]):

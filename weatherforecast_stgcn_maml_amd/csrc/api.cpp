@@ -227,7 +227,7 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -616,7 +616,9 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
 // rows t >= 1 (no neighbours, F3) run all four convs in one launch (k_gcn_mlp, activations kept in
 // registers), the t = 0 rows (ELL gather) four per-layer launches over N-row blocks.
-int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
+// consec: every task's B windows start at consecutive stream rows (the caller checked the window
+// table): the fused kernel then computes each distinct stream row once (k_gcn_mlp dedup).
+int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, bool consec = false) {
   const Dims& d = c->d;
   Work& w = c->w;
   const int rps = d.T * d.N;
@@ -632,9 +634,11 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev) {
     }
     // the GCN parameters may change between calls (smaml_set_gcn_params keeps the pointer): re-split
     TIMED(c, s, C_MISC, 0, launch_gcn_wsplit(s, d, c->gcn, wo, c->gcn_wimg));
-    const double rows1 = (double)zb * (d.T - 1) * d.N;
+    const bool dedup = consec && c->kn.gcn_dedup && w.B > 1 && !w.drop.gcn();
+    if (dedup) count_variant(w, V_GCN_DEDUP);
+    const double rows1 = dedup ? (double)w.Z * (w.B + d.T - 2) * d.N : (double)zb * (d.T - 1) * d.N;
     TIMED(c, s, C_GCN, 2.0 * rows1 * d.Hc * (d.Cin0 + 3.0 * d.Hc),
-          launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop));
+          launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop, dedup));
     for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks, masks indexed as rows of T*N-row samples
       const bool last = k == 3;
       float* dst = last ? w.F : bufs[k & 1];
@@ -771,8 +775,9 @@ static void ad_cache_drop(smaml_ctx* c) {
   c->ad_valid.clear();
 }
 
-int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev) {
-  TRY(run_gcn(c, s, xtab_dev));
+int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev,
+                bool consec = false) {
+  TRY(run_gcn(c, s, xtab_dev, consec));
   return run_lstm(c, s, theta, tstride);
 }
 
@@ -843,10 +848,10 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
 
 // Primal recompute + tangent along U (second-order sweep), GCN features recomputed.
 int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride,
-                     const float* const* xtab_dev, bool gcn_cached) {
+                     const float* const* xtab_dev, bool gcn_cached, bool consec) {
   const Dims& d = c->d;
   Work& w = c->w;
-  if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev));
+  if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, consec));
   TRY(prep_gate_images(c, s, theta, tstride, U));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
@@ -1334,6 +1339,16 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
         ptrs[i] = c->feats[z] + (int64_t)wv * d.N * d.Cin0;
       }
   TRY(upload_xtab(c, s, ptrs.data(), nptr));
+  // steps whose every task reads B consecutive windows (the reference's support and query batches)
+  std::vector<uint8_t> consec(steps + 1, 0);
+  for (int k = 0; k <= steps; ++k) {
+    bool ok = B > 1;
+    for (int z = 0; z < Z && ok; ++z) {
+      const int32_t* wz = windows_host + ((int64_t)k * Z + z) * B;
+      for (int b = 1; b < B && ok; ++b) ok = wz[b] == wz[0] + b;
+    }
+    consec[k] = ok ? 1 : 0;
+  }
   if (!losses) {
     const int64_t need = (int64_t)(steps + 1) * Z;
     if (need > c->scratch_loss_cap) {
@@ -1359,7 +1374,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     }
     const int slot = steps - 1 - k;
     use_primal(c, slot < nkeep ? slot : SET_MAIN);
-    TRY(run_forward(c, s, c->fast, P, xt));
+    TRY(run_forward(c, s, c->fast, P, xt, consec[k]));
     TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
     TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
     TRY(run_backward(c, s, c->fast, P, c->grad));
@@ -1381,7 +1396,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   c->w.F = c->F_main;
   use_primal(c, nkeep > 0 ? SET_QUERY : SET_MAIN);  // slot 0 holds the workspace's own Hs/Cs/Gs
   if (dropout) set_step_drop(c, steps);
-  TRY(run_forward(c, s, c->fast, P, xq));
+  TRY(run_forward(c, s, c->fast, P, xq, consec[steps]));
   TIMED(c, s, C_HEAD, head_fl,
         launch_head_loss(s, d, c->w, c->fast, P, c->po, xq, 2.f * inv * query_scale, true));
   TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)steps * Z));
@@ -1411,7 +1426,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       use_primal(c, slot < nkeep ? slot : SET_MAIN);
       c->w.primal_kept = slot < nkeep ? 1 : 0;
       if (dropout) set_step_drop(c, k);  // the masks of inner step k's forward
-      TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr));
+      TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr, consec[k]));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
       if (k > 0)  // v_k = v_{k+1} - lr H_k w_k and w_{k-1} (dot g_{k-1} . v_k, direction): one kernel
@@ -1600,6 +1615,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bwdd_remap = (int)value;
   } else if (k == "small_kw" && value >= 0 && value <= 2) {
     c->kn.small_kw = (int)value;
+  } else if (k == "gcn_dedup" && (value == 0 || value == 1)) {
+    c->kn.gcn_dedup = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
     c->ad_gcn_batch = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {

@@ -95,6 +95,7 @@ enum Variant {
   V_WGRAD_WS,        // k_wgrad_ws, warp-specialised (also counted as V_WGRAD)
   V_FWD_KW,          // k_lstm_fwd_kw (small grids: K split over the waves of one workgroup)
   V_BWD_KW,          // k_lstm_bwd_kw (same, BPTT)
+  V_GCN_DEDUP,       // k_gcn_mlp once per distinct stream row of consecutive windows
   NVAR
 };
 
@@ -125,6 +126,7 @@ struct Knobs {
   int bwdd_remap;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
   int small_kw;              // small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip):
                              // 1 = on, 2 = on with pre-split BPTT weight images (launch_split_bwd), 0 = split-K pairs
+  int gcn_dedup;             // 1: batches of consecutive windows run the fused GCN rows once per distinct stream row
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -363,13 +365,17 @@ struct GcnMlpArgs {
   int64_t R1, M;             // rows t >= 1 over all samples; B*N
   FastDiv rows_div, b_div, n_div;
   int rows1, N, T, B, cin0;
+  int dedup;                 // 1: every task's B windows are consecutive; rows1 = (B + T - 2) * N distinct
+                             // time steps per task, each row written to every (sample, t >= 1) holding it
   Drop dr;
 };
 bool gcn_mlp_supported(const Dims& d);
 int64_t gcn_wimg_bytes(const Dims& d);
 void launch_gcn_wsplit(hipStream_t s, const Dims& d, const float* gcn, const GcnWOff& wo, char* img);
+// dedup: the B windows of every task start at consecutive stream rows (xtab[z*B + b] = xtab[z*B] + b
+// time steps) and there is no GCN dropout -- see k_gcn_mlp
 void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
-                    const GcnWOff& wo, const char* img, float* F, const Drop* drop);
+                    const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup = false);
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,

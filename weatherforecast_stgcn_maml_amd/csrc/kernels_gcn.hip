@@ -19,6 +19,14 @@
 // the next layer without any cross-lane exchange or LDS round trip. Activations between the four
 // layers never touch HBM: per row the kernel reads Cin0 floats and writes HC floats (the LSTM
 // input F, in the time-major layout [Z][T][B*N][HC] of k_gcn_layer's remap).
+//
+// Consecutive windows (dedup): a row t >= 1 sees only its own input row (F3), so its features are a
+// function of the stream row alone, and window b's step t is window b + 1's step t - 1. When a task's B
+// windows start at consecutive stream rows (the support batches and the query batch of the reference's
+// window table), the kernel computes each distinct stream row tau' = b + t in [1, B + T - 2] once --
+// (B + T - 2) N rows per task instead of B (T - 1) N, 55 instead of 736 time steps at B = 32 -- and
+// stores the result to every (b, t >= 1) with b + t = tau'. Same per-row arithmetic, so F is bitwise
+// the per-sample result.
 #include "kernels.h"
 #include "loaders.h"
 
@@ -92,16 +100,20 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
   __shared__ __attribute__((aligned(16))) float bias_s[4][HC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
 
-  // this lane's data row (t >= 1 rows of sample g: q in [N, T*N))
+  // this lane's data row (t >= 1 rows of sample g: q in [N, T*N)); dedup: g is the task and
+  // t = q / N the stream row tau' relative to its first window, in [1, B + T - 2]
   const int64_t r1 = (int64_t)blockIdx.x * GM_ROWS + wave * 32 + (lane & 31);
   const bool valid = r1 < a.R1;
   const uint32_t rr = valid ? (uint32_t)r1 : 0u;
   const int g = (int)a.rows_div.div(rr);
   const int q = a.N + (int)(rr - (uint32_t)g * (uint32_t)a.rows1);
-  const int z = (int)a.b_div.div((uint32_t)g), s = g - z * a.B;
+  const int z = a.dedup ? g : (int)a.b_div.div((uint32_t)g), s = a.dedup ? 0 : g - z * a.B;
   const int t = (int)a.n_div.div((uint32_t)q), n = q - t * a.N;
-  const float* xrow = a.xtab[g] + (int64_t)q * a.cin0;
-  float* frow = a.F + (((int64_t)z * a.T + t) * a.M + (int64_t)s * a.N + n) * HC;
+  const float* xrow = a.xtab[a.dedup ? g * a.B : g] + (int64_t)q * a.cin0;
+  // destinations: (sample boff - tt, step tt) for tt in [t_lo, t_hi]
+  const int t_lo = a.dedup ? max(1, t - (a.B - 1)) : t, t_hi = a.dedup ? min(a.T - 1, t) : t;
+  const int boff = s + t;
+  float* frow = a.F + (((int64_t)z * a.T) * a.M + n) * HC;
   uint64_t didx = 0;
   if (a.dr.gcn()) didx = (((uint64_t)a.dr.task_id[z] * a.B + s) * (uint64_t)(a.T * a.N) + (uint64_t)q) * HC;
 
@@ -200,12 +212,15 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
     epilogue(layer);
   }
   if (valid) {
+    for (int tt = t_lo; tt <= t_hi; ++tt) {
+      float* fr = frow + ((int64_t)tt * a.M + (int64_t)(boff - tt) * a.N) * HC;
 #pragma unroll
-    for (int ci = 0; ci < NT; ++ci)
+      for (int ci = 0; ci < NT; ++ci)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq)
-        st4(frow + 32 * ci + 8 * gq + 4 * h,
-            make_float4(act[ci][4 * gq], act[ci][4 * gq + 1], act[ci][4 * gq + 2], act[ci][4 * gq + 3]));
+        for (int gq = 0; gq < 4; ++gq)
+          st4(fr + 32 * ci + 8 * gq + 4 * h,
+              make_float4(act[ci][4 * gq], act[ci][4 * gq + 1], act[ci][4 * gq + 2], act[ci][4 * gq + 3]));
+    }
   }
 }
 
@@ -221,15 +236,16 @@ int64_t gcn_wimg_bytes(const Dims& d) {
 bool gcn_mlp_supported(const Dims& d) { return d.Hc == 256 && d.Cin0 <= 32 && d.Cin0 % 4 == 0 && d.T > 1; }
 
 void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
-                    const GcnWOff& wo, const char* img, float* F, const Drop* drop) {
+                    const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup) {
   GcnMlpArgs a{};
   a.xtab = xtab;
   a.gcn = gcn;
   a.wo = wo;
   a.wimg = img;
   a.F = F;
-  a.rows1 = (d.T - 1) * d.N;
-  a.R1 = (int64_t)Zb * a.rows1;
+  a.dedup = dedup && B > 1 && !(drop && drop->gcn()) ? 1 : 0;
+  a.rows1 = (a.dedup ? B + d.T - 2 : d.T - 1) * d.N;
+  a.R1 = (int64_t)(a.dedup ? Zb / B : Zb) * a.rows1;
   a.rows_div = FastDiv((uint32_t)a.rows1);
   a.b_div = FastDiv((uint32_t)B);
   a.n_div = FastDiv((uint32_t)d.N);
