@@ -473,7 +473,9 @@ def main():
             "maml_order": cfg.order,
             "parallelism": (f"task-sharded x{world} + one {'RCCL' if backend == 'nccl' else backend} all-reduce "
                             f"per meta-step" if world > 1 else "single GPU, no collective"),
-            "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2)",
+            "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2); the fused rows t >= 1 "
+                         "of a batch of consecutive windows once per distinct stream row (F3, option gcn_dedup, "
+                         "bitwise equal); meta_step_tflop still counts the GCN once per sample-step (SURVEY 8d)",
             "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
             "task_group": len(ml._groups[0][1]) if ml._groups else 0,
             "dropout": list(args.dropout),
