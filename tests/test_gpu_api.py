@@ -494,13 +494,14 @@ def test_stgcn_autograd_matches_oracle(d, p):
     assert rel(xg.grad.cpu(), xt.grad) < 1e-4
 
 
-@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup"])
+@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
-    stored to every sample holding them) leave every row's arithmetic unchanged: a second-order
-    meta-step (big tangent BPTT tiles forced, every primal kept) is bitwise equal with the knob on and
-    off."""
+    stored to every sample holding them; gcn_dedup_layers: the same on the per-layer GCN path,
+    gcn_fused 0, as one pseudo-sample of distinct stream rows per task expanded into F) leave every
+    row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
+    kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
@@ -514,12 +515,14 @@ def test_order_only_knobs_bitwise(knob):
         ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
         ml.set_tasks(feats)
         ml.ctx.set_option("bwdd_big_min", 0)
-        ml.ctx.set_option(knob, on)
+        if knob == "gcn_dedup_layers":
+            ml.ctx.set_option("gcn_fused", 0)
+        ml.ctx.set_option("gcn_dedup" if knob.startswith("gcn_dedup") else knob, on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()
         vc = ml.ctx.variant_counts()
         assert vc["bwd_dual_big_kept"] > 0, vc
-        if knob == "gcn_dedup":
+        if knob.startswith("gcn_dedup"):
             assert (vc["gcn_dedup"] > 0) == bool(on), vc
         out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
         del ml

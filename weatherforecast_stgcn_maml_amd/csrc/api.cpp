@@ -616,9 +616,12 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
 // rows t >= 1 (no neighbours, F3) run all four convs in one launch (k_gcn_mlp, activations kept in
 // registers), the t = 0 rows (ELL gather) four per-layer launches over N-row blocks.
-// consec: every task's B windows start at consecutive stream rows (the caller checked the window
-// table): the fused kernel then computes each distinct stream row once (k_gcn_mlp dedup).
-int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, bool consec = false) {
+// first_tab (device, [Z]: each task's first window pointer), given when every task's B windows start at
+// consecutive stream rows (the caller checked the window table): the rows t >= 1 are then computed
+// once per distinct stream row -- by the fused kernel (k_gcn_mlp dedup), or, on the per-layer path,
+// as one (B + T - 1) N-row pseudo-sample per task without neighbours, expanded into F afterwards.
+int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, const float* const* first_tab = nullptr) {
+  const bool consec = first_tab != nullptr;
   const Dims& d = c->d;
   Work& w = c->w;
   const int rps = d.T * d.N;
@@ -640,6 +643,31 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, bool cons
     TIMED(c, s, C_GCN, 2.0 * rows1 * d.Hc * (d.Cin0 + 3.0 * d.Hc),
           launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop, dedup));
     for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks, masks indexed as rows of T*N-row samples
+      const bool last = k == 3;
+      float* dst = last ? w.F : bufs[k & 1];
+      TIMED(c, s, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
+            launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
+                             c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
+                             d.N, d.N, &w.drop, rps));
+      src = dst;
+    }
+    HIP_TRY(hipGetLastError());
+    return SMAML_OK;
+  }
+  if (consec && c->kn.gcn_dedup && w.B > 1 && !w.drop.gcn()) {
+    count_variant(w, V_GCN_DEDUP);
+    const int rpsC = (w.B + d.T - 1) * d.N;  // stream rows w0 .. w0 + B + T - 2 of each task
+    for (int k = 0; k < 4; ++k) {
+      float* dst = bufs[k & 1];
+      TIMED(c, s, C_GCN, 2.0 * w.Z * rpsC * c->go.cin[k] * d.Hc,
+            launch_gcn_layer(s, d, k, w.Z, 1, k == 0 ? first_tab : nullptr, src, dst, false, true,
+                             c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
+                             rpsC, 0, nullptr));
+      src = dst;
+    }
+    TIMED(c, s, C_GCN, 0, launch_gcn_expand(s, d, w.Z, w.B, src, w.F));
+    src = nullptr;
+    for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks with the ELL gather, as on the fused path
       const bool last = k == 3;
       float* dst = last ? w.F : bufs[k & 1];
       TIMED(c, s, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
@@ -776,8 +804,8 @@ static void ad_cache_drop(smaml_ctx* c) {
 }
 
 int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev,
-                bool consec = false) {
-  TRY(run_gcn(c, s, xtab_dev, consec));
+                const float* const* first_tab = nullptr) {
+  TRY(run_gcn(c, s, xtab_dev, first_tab));
   return run_lstm(c, s, theta, tstride);
 }
 
@@ -848,10 +876,10 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
 
 // Primal recompute + tangent along U (second-order sweep), GCN features recomputed.
 int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride,
-                     const float* const* xtab_dev, bool gcn_cached, bool consec) {
+                     const float* const* xtab_dev, bool gcn_cached, const float* const* first_tab) {
   const Dims& d = c->d;
   Work& w = c->w;
-  if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, consec));
+  if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, first_tab));
   TRY(prep_gate_images(c, s, theta, tstride, U));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
@@ -1327,7 +1355,8 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   c->keep_last = nkeep;
   // sample window table for every step (support steps then the query batch)
   const int64_t nptr = (int64_t)(steps + 1) * Z * B;
-  std::vector<const float*> ptrs(nptr);
+  // (+ each step's per-task first-window pointers, the GCN's consecutive-window tables)
+  std::vector<const float*> ptrs(nptr + (int64_t)(steps + 1) * Z);
   const int max_w_off = d.T + d.Hf;  // last stream index read by a sample = w + T + Hf
   for (int k = 0; k <= steps; ++k)
     for (int z = 0; z < Z; ++z)
@@ -1338,17 +1367,20 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
           return fail(SMAML_EINVAL, "window start out of range for task " + std::to_string(z));
         ptrs[i] = c->feats[z] + (int64_t)wv * d.N * d.Cin0;
       }
-  TRY(upload_xtab(c, s, ptrs.data(), nptr));
   // steps whose every task reads B consecutive windows (the reference's support and query batches)
-  std::vector<uint8_t> consec(steps + 1, 0);
+  std::vector<const float* const*> consec(steps + 1, nullptr);
   for (int k = 0; k <= steps; ++k) {
     bool ok = B > 1;
     for (int z = 0; z < Z && ok; ++z) {
       const int32_t* wz = windows_host + ((int64_t)k * Z + z) * B;
       for (int b = 1; b < B && ok; ++b) ok = wz[b] == wz[0] + b;
     }
-    consec[k] = ok ? 1 : 0;
+    for (int z = 0; z < Z; ++z) ptrs[nptr + (int64_t)k * Z + z] = ptrs[((int64_t)k * Z + z) * B];
+    consec[k] = ok ? ptrs.data() : nullptr;  // (flag only: the device table may move in upload_xtab)
   }
+  TRY(upload_xtab(c, s, ptrs.data(), (int64_t)ptrs.size()));
+  for (int k = 0; k <= steps; ++k)
+    if (consec[k]) consec[k] = c->xtab + nptr + (int64_t)k * Z;
   if (!losses) {
     const int64_t need = (int64_t)(steps + 1) * Z;
     if (need > c->scratch_loss_cap) {

@@ -370,6 +370,7 @@ struct GcnMlpArgs {
   Drop dr;
 };
 bool gcn_mlp_supported(const Dims& d);
+void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F);
 int64_t gcn_wimg_bytes(const Dims& d);
 void launch_gcn_wsplit(hipStream_t s, const Dims& d, const float* gcn, const GcnWOff& wo, char* img);
 // dedup: the B windows of every task start at consecutive stream rows (xtab[z*B + b] = xtab[z*B] + b

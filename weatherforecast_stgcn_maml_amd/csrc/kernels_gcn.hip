@@ -233,6 +233,23 @@ int64_t gcn_wimg_bytes(const Dims& d) {
   return (int64_t)(GM_KS1 + 3 * (d.Hc / 16)) * gm_step_bytes(d.Hc);
 }
 
+// Consecutive windows on the per-layer path: C [Z][B + T - 1][N][Hc] holds each task's stream rows
+// w0 .. w0 + B + T - 2 (rows without neighbours); F[z][t][b N + n] = C[z][b + t][n] for t >= 1 -- one
+// workgroup per (task, t, window) N x Hc block, float4 copies.
+__global__ void k_gcn_expand(const float* __restrict__ C, float* __restrict__ F, int B, int T, int64_t blk) {
+  const int b = blockIdx.y % B, t = 1 + (int)(blockIdx.y / B) % (T - 1), z = blockIdx.y / (B * (T - 1));
+  const float4* src = reinterpret_cast<const float4*>(C + ((int64_t)z * (B + T - 1) + b + t) * blk);
+  float4* dst = reinterpret_cast<float4*>(F + (((int64_t)z * T + t) * B + b) * blk);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < blk / 4; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F) {
+  const int64_t blk = (int64_t)d.N * d.Hc;  // floats per (task, t, window) block; Hc % 4 == 0
+  const unsigned gx = (unsigned)std::min<int64_t>((blk / 4 + 255) / 256, 64);
+  k_gcn_expand<<<dim3(gx, (unsigned)(Z * B * (d.T - 1))), 256, 0, s>>>(C, F, B, d.T, blk);
+}
+
 bool gcn_mlp_supported(const Dims& d) { return d.Hc == 256 && d.Cin0 <= 32 && d.Cin0 % 4 == 0 && d.T > 1; }
 
 void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
