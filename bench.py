@@ -246,7 +246,7 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
     return out, feats
 
 
-def config5_share_bench(tasks, steps=1, warmup=1):
+def config5_share_bench(tasks, steps=1, warmup=1, timing=True):
     """BASELINE config 5 (stress: 64 tasks, N=1024 (32x32 grid), Hc=512, LSTM 4x128, K=10, second
     order), the share one rank holds when the driver's 8-GPU run shards the 64 tasks round-robin:
     ``tasks`` tasks on this GPU, ``warmup`` untimed + ``steps`` timed meta-steps on a fresh
@@ -273,6 +273,9 @@ def config5_share_bench(tasks, steps=1, warmup=1):
     ml.set_tasks(feats, task_ids=ids)
     for _ in range(warmup):
         ml.meta_step(sync=False)
+    if timing:
+        ml.ctx.timing_collect()  # drop warmup records
+        ml.ctx.timing(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = None
@@ -280,23 +283,33 @@ def config5_share_bench(tasks, steps=1, warmup=1):
         res = ml.meta_step(sync=False)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    kern = None
+    if timing:
+        ml.ctx.timing(False)
+        kern = ml.ctx.timing_collect()
     qmse = float(res.losses[-1].sum().item()) / tasks
     kept = ml.ctx.so_kept_steps()
+    groups = len(ml._groups)
     ml.ctx.close()
     del ml
     torch.cuda.empty_cache()
     assert np.isfinite(qmse), qmse
     flops = algorithmic_flops(d, tasks, cfg.inner_steps, cfg.batch, cfg.order)
     ms = elapsed / steps * 1e3
-    return {
+    out = {
         "metric": "config-5 rank share: ms per second-order meta-step of one rank's tasks",
         "value": ms, "unit": "ms/meta-step", "higher_is_better": False, "steps": steps, "warmup": warmup,
+        "meta_step_tflop": flops / 1e12,
         "achieved_tflops_whole_step": flops / (elapsed / steps) / 1e12, "query_mse": qmse,
         "config": {"workload": f"BASELINE config 5 share: {tasks} of 64 tasks x B={cfg.batch} x T={d.window_size} x "
                                f"N={d.num_nodes} x C={d.input_channels}, Hc={d.hidden_channels}, LSTM "
                                f"{d.lstm_num_layers}x{d.lstm_hidden_size}, K={cfg.inner_steps} inner steps",
-                   "tasks": tasks, "so_kept_steps": kept},
+                   "tasks": tasks, "so_kept_steps": kept, "task_groups": groups},
+        "rank_workload": rank_workload(d, cfg, tasks, 5),
     }
+    if kern is not None:
+        out.update(kernel_report(kern, steps, elapsed, out["rank_workload"]))
+    return out
 
 
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
@@ -336,6 +349,50 @@ def measured_traffic(category, rank_key):
     return c
 
 
+def kernel_report(kern, steps, elapsed, rank_key):
+    """Per-category kernel times of the timed region (HIP events on the launch stream), the executed
+    flops (each launch's count is what its kernel actually computes -- GCN rows of consecutive windows
+    once per distinct stream row, no recurrent products at t = 0, tangent-only passes of kept steps --
+    beside SURVEY §8(d)'s convention, which counts the GCN once per sample-step), and the roofline of
+    the dominant kernel: its average launch's flops over its average launch duration, with the HBM
+    bytes per launch from the committed PMC passes of the same per-rank workload."""
+    from weatherforecast_stgcn_maml_amd import _capi
+
+    forms = _capi.product_forms()
+    executed = sum(v["flops"] for v in kern.values()) / steps
+    out = {"executed_tflop": executed / 1e12,
+           "achieved_tflops_executed": executed / (elapsed / steps) / 1e12,
+           "executed_flops_basis": "sum of the flops of every timed launch (what each kernel computes; the "
+                                   "deduplicated GCN rows once, no h_{-1} = 0 products, tangent-only kept steps)"}
+    # each timing category is one kernel symbol (api.cpp enum Cat); the roofline is quoted for the one
+    # with the most time: its average launch duration here must match rocprofv3's for that symbol
+    dom = max((k for k in kern if k not in ("misc", "wgrad_reduce")), key=lambda k: kern[k]["ms"])
+    kd = kern[dom]
+    ach = kd["flops"] / (kd["ms"] * 1e-3) / 1e12 if kd["ms"] > 0 else 0.0
+    traffic = measured_traffic(dom, rank_key)
+    x6 = forms.get(CAT_FAMILY.get(dom, ""), 0) > 0
+    peak = PEAK_X6_TFLOPS if x6 else PEAK_FP32_MFMA_TFLOPS
+    roof = {
+        "kernel": KERNEL_SYMBOL.get(dom, dom), "category": dom, "bound": "mfma", "achieved": ach, "peak": peak,
+        "unit": "TFLOP/s", "frac": ach / peak,
+        "peak_basis": ("f32 work as six bf16 piece products: dense BF16 MFMA 2516.8 TF / 6 (the native f32 MFMA "
+                       "peak is 157.3 TF)" if x6 else "v_mfma_f32_32x32x2_f32 dense peak"),
+        "traffic": traffic["bytes_per_launch"] if traffic else None,
+        "avg_launch_us": kd["ms"] * 1e3 / max(kd["launches"], 1),
+        "flops_per_launch": kd["flops"] / max(kd["launches"], 1),
+    }
+    if traffic:
+        roof["traffic_unit"] = "bytes/launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        roof["traffic_source"] = traffic["source"]
+        roof["hbm_tbs"] = traffic["bytes_per_launch"] / (roof["avg_launch_us"] * 1e-6) / 1e12
+    out["roofline"] = roof
+    out["kernels"] = {k: {"ms_per_step": v["ms"] / steps,
+                          "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
+                          "launches_per_step": v["launches"] / steps}
+                      for k, v in kern.items()}
+    return out
+
+
 def relaunch(args) -> int:
     """``--gpus N`` without a torch.distributed launcher: start N ranks (one per GPU) through
     torch.distributed.run as a child process, before this process touches the GPU, and return
@@ -370,7 +427,6 @@ def main():
 
     from weatherforecast_stgcn_maml_amd import _capi
 
-    forms = _capi.product_forms()
     rank, world, local = env_rank()
     # one process per GPU; SMAML_DIST_BACKEND=gloo + LOCAL_RANK mod device count lets a
     # single-GPU box rehearse the N>1 path (the driver's 8-GPU runs use RCCL, one GPU each)
@@ -415,10 +471,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    progress(f"rank {rank}: timed region done")
-    from weatherforecast_stgcn_maml_amd import _capi as _c
-    ml.ctx.sync(_c.stream_ptr(torch))  # a timed-out grid-barrier kernel would have invalidated the run: raise
     elapsed = time.perf_counter() - t0
+    progress(f"rank {rank}: timed region done")
+    ml.ctx.sync(_capi.stream_ptr(torch))  # a timed-out grid-barrier kernel would have invalidated the run: raise
     kern = None
     if not args.no_timing:
         ml.ctx.timing(False)
@@ -473,9 +528,10 @@ def main():
             "maml_order": cfg.order,
             "parallelism": (f"task-sharded x{world} + one {'RCCL' if backend == 'nccl' else backend} all-reduce "
                             f"per meta-step" if world > 1 else "single GPU, no collective"),
-            "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2); the fused rows t >= 1 "
+            "gcn_hoist": "GCN features computed once per distinct sample per meta-step (F2); the rows t >= 1 "
                          "of a batch of consecutive windows once per distinct stream row (F3, option gcn_dedup, "
-                         "bitwise equal); meta_step_tflop still counts the GCN once per sample-step (SURVEY 8d)",
+                         "bitwise equal); meta_step_tflop counts the GCN once per sample-step (SURVEY 8d), "
+                         "executed_tflop counts what ran",
             "so_kept_steps": ml.ctx.so_kept_steps() if cfg.order == 2 else 0,
             "task_group": len(ml._groups[0][1]) if ml._groups else 0,
             "dropout": list(args.dropout),
@@ -487,31 +543,7 @@ def main():
         "query_mse": qmse,
     }
     if kern is not None:
-        # each timing category is one kernel symbol (api.cpp enum Cat); the roofline is
-        # quoted for the one with the most time: its average launch duration here must match
-        # rocprofv3's average for that symbol (profiles/)
-        dom = max((k for k in kern if k not in ("misc", "wgrad_reduce")), key=lambda k: kern[k]["ms"])
-        kd = kern[dom]
-        ach = kd["flops"] / (kd["ms"] * 1e-3) / 1e12 if kd["ms"] > 0 else 0.0
-        traffic = measured_traffic(dom, out["rank_workload"])
-        x6 = forms.get(CAT_FAMILY.get(dom, ""), 0) > 0
-        peak = PEAK_X6_TFLOPS if x6 else PEAK_FP32_MFMA_TFLOPS
-        out["roofline"] = {
-            "kernel": KERNEL_SYMBOL.get(dom, dom), "category": dom, "bound": "mfma", "achieved": ach, "peak": peak,
-            "unit": "TFLOP/s", "frac": ach / peak,
-            "peak_basis": ("f32 work as six bf16 piece products: dense BF16 MFMA 2516.8 TF / 6 (the native f32 MFMA "
-                           "peak is 157.3 TF)" if x6 else "v_mfma_f32_32x32x2_f32 dense peak"),
-            "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "avg_launch_us": kd["ms"] * 1e3 / max(kd["launches"], 1),
-            "flops_per_launch": kd["flops"] / max(kd["launches"], 1),
-        }
-        if traffic:
-            out["roofline"]["traffic_unit"] = "bytes/launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)"
-            out["roofline"]["traffic_source"] = traffic["source"]
-        out["kernels"] = {k: {"ms_per_step": v["ms"] / args.steps,
-                              "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
-                              "launches_per_step": v["launches"] / args.steps}
-                          for k, v in kern.items()}
+        out.update(kernel_report(kern, args.steps, elapsed, out["rank_workload"]))
     if comm is not None:
         # the all-reduce's exposed time per meta-step (HIP events on the compute stream: end of this
         # rank's meta-step work -> reduced buffer ready, incl. waiting for the slowest rank), max /

@@ -247,7 +247,11 @@ int smaml_free(smaml_ctx* ctx, void* p);
  * librccl is loaded on first use. Rank 0 calls smaml_comm_unique_id and ships the 128 bytes
  * to the other ranks (env/file/store); every rank then calls smaml_comm_init. The meta-
  * gradient all-reduce of one meta-step is smaml_comm_allreduce(meta_grad, P) (in-place sum,
- * fp32, on the given stream). The Python path uses torch.distributed's RCCL instead. */
+ * fp32, on the given stream). The Python path uses torch.distributed's RCCL instead.
+ * smaml_comm_init is bounded: where librccl has ncclCommInitRankConfig it creates the
+ * communicator non-blocking and polls it for at most smaml_set_option("comm_timeout_ms")
+ * (default 120 s); a rank whose peers never arrive gets SMAML_EHIP (communicator aborted)
+ * instead of blocking forever, so the ranks can agree on the outcome afterwards. */
 int smaml_comm_unique_id(uint8_t* id_out /* 128 bytes */);
 int smaml_comm_init(smaml_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id /* 128 bytes */);
 int smaml_comm_allreduce(smaml_ctx* ctx, void* stream, float* buf, int64_t n);
@@ -294,6 +298,8 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  equal);
  *   "barrier_timeout_us":          bound on a grid-barrier wait (default 4 s); on expiry the kernel
  *                                  exits and the next call / smaml_sync returns SMAML_EHIP;
+ *   "comm_timeout_ms":             bound on smaml_comm_init's wait for the other ranks (default
+ *                                  120000);
  *   "barrier_oversize":            debug: > 0 launches the grid-barrier kernels with that many
  *                                  times the resident capacity (+1 block), which can never be
  *                                  co-resident, to exercise the bounded wait;

@@ -75,3 +75,139 @@ def test_two_rank_meta_reduction_and_replicated_update(world):
     for r in res:
         for other in r[5]:
             assert np.array_equal(other, res[0][4])
+
+
+# ---- MetaLearner's own multi-rank path at world 8 -------------------------------
+# The device context is replaced by a CPU stand-in (test infrastructure, never shipped): its meta_step
+# writes a fixed per-task meta-gradient (task_grad of the task's global id, summed over the group) and
+# query losses, its adamw_step is the oracle's clip + AdamW on the flat vector. Everything else is the
+# product's MetaLearner: round-robin sharding, task groups, the ONE all-reduce of [meta-grad | qsum],
+# and the replicated outer step. 15 tasks over 8 ranks: {2,2,2,2,2,2,2,1}.
+
+from weatherforecast_stgcn_maml_amd.config import CONFIG1, MamlConfig  # noqa: E402
+
+
+def _qloss(j):
+    return 0.5 * (1.0 + 0.01 * j)
+
+
+class FakeContext:
+    def __init__(self, dims, device=0):
+        self.P = None
+        self.ids = []
+
+    def set_graph(self, ei):
+        pass
+
+    def set_gcn_params(self, g):
+        pass
+
+    def set_tasks(self, feats):
+        self.n = len(feats)
+
+    def reserve(self, z, b):
+        pass
+
+    def set_dropout(self, *a):
+        pass
+
+    def set_task_ids(self, ids):
+        self.ids = [int(i) for i in ids]
+
+    def meta_step(self, stream, theta, order, K, B, windows, lr, mx, qs, meta_grad=None, losses=None, norms=None,
+                  fast_out=None):
+        assert len(self.ids) == self.n == windows.shape[1]
+        P = theta.numel()
+        g = torch.zeros(P)
+        for j in self.ids:
+            g += _grad_of(j, P)
+        meta_grad.copy_(g)
+        losses.zero_()
+        losses[K] = torch.tensor([_qloss(j) for j in self.ids])
+        norms.zero_()
+
+    def adamw_step(self, stream, theta, g, m, v, step, lr, betas, eps, wd, max_norm, norm_out):
+        from oracle import refcpu
+
+        st = {"step": step - 1, "m_p": m, "v_p": v}
+        refcpu.adamw_step({"p": theta}, {"p": g.clone()}, st, lr, betas, eps, wd, max_norm)
+        norm_out.fill_(float(g.norm()))
+
+    def sync(self, stream):
+        pass
+
+
+def _grad_of(j, P):
+    # small multiples of 2^-10: every partial sum is exact, so the order in which ranks and groups add
+    # them cannot move AdamW's g / sqrt(v) on entries whose sum is near zero (world 1 comparison)
+    return torch.from_numpy(np.random.default_rng(100 + j).integers(-64, 65, P).astype(np.float32) / 1024.0)
+
+
+def _learner(task_ids):
+    from weatherforecast_stgcn_maml_amd import _capi, maml, synth
+
+    _capi.Context = FakeContext
+    _capi.stream_ptr = lambda torch_mod: 0
+    d = CONFIG1
+    cfg = MamlConfig(inner_steps=2, batch=2, order=2)
+    P = synth.init_params(7, d)
+    names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
+    ml = maml.MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names},
+                          np.zeros((2, 0), np.int64), device="cpu", task_group=1)
+    T = maml.stream_len_for(cfg, d)
+    ml.set_tasks([np.zeros((T, d.num_nodes, d.input_channels), np.float32) for _ in task_ids], task_ids=task_ids)
+    return ml
+
+
+def ml_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    r, w = D.init_from_env("gloo")
+    mine = D.shard_tasks(TASKS, r, w)
+    ml = _learner(mine)
+    calls = []
+    real = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append(t.numel())
+        return real(t, *a, **k)
+
+    dist.all_reduce = counting
+    metas = []
+    for _ in range(2):
+        n0 = len(calls)
+        res = ml.meta_step()
+        metas.append((len(calls) - n0, res.meta_loss))
+    dist.all_reduce = real
+    gathered = [torch.zeros_like(ml.theta) for _ in range(w)]
+    dist.all_gather(gathered, ml.theta)
+    out_q.put((rank, mine, len(ml._groups), metas, ml.theta.numpy(), [x.numpy() for x in gathered]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [8])
+def test_metalearner_eight_rank_rehearsal(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=ml_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [len(r[1]) for r in res] == [2, 2, 2, 2, 2, 2, 2, 1]
+    assert sorted(sum([r[1] for r in res], [])) == list(range(TASKS))
+    assert [r[2] for r in res] == [2, 2, 2, 2, 2, 2, 2, 1]  # task_group=1: one pass per task
+    qsum = sum(_qloss(j) for j in range(TASKS)) * MamlConfig().query_loss_scale
+    for r in res:
+        for n_calls, meta_loss in r[3]:
+            assert n_calls == 1  # ONE collective per meta-step
+            assert abs(meta_loss - qsum) < 1e-5
+        for other in r[5]:
+            assert np.array_equal(other, res[0][4])  # bitwise-identical theta on all 8 ranks
+    one = _learner(list(range(TASKS)))  # world 1 (no process group): all 15 tasks on one rank
+    for _ in range(2):
+        one.meta_step()
+    np.testing.assert_allclose(res[0][4], one.theta.numpy(), rtol=0, atol=1e-6)

@@ -126,6 +126,33 @@ def test_second_order_k10_cfg5():
     check(res, ml, ref, d, names, 1, cfg.inner_steps)
 
 
+def test_second_order_cfg5_gcn_dedup_against_oracle():
+    """The per-layer GCN path with consecutive windows (the config-5 share's path: Hc = 512 has no fused
+    t >= 1 kernel, so run_gcn computes the (B + T - 1) N distinct stream rows of a task as one
+    pseudo-sample through the four layers, k_gcn_expand copies them to every (window, t >= 1) slot and
+    the t = 0 rows run their ELL chain; F3, hybrid_model.py:65-75, dataset.py:30-37) against the
+    oracle, which computes every window's rows on its own: config-5 shapes, 1 task x B = 2 consecutive
+    windows x K = 2, second order, gcn_fused off. The dedup variant must have run on every step."""
+    d = CONFIG5
+    cfg = MamlConfig(inner_steps=2, batch=2, order=2)
+    P = synth.init_params(25, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(2500, d.num_nodes, stream_len_for(cfg, d))]
+    ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV)
+    ml.set_tasks(feats)
+    ml.ctx.set_option("gcn_fused", 0)
+    ml.ctx.set_option("gcn_dedup", 1)
+    w = ml.default_windows()
+    assert all((np.diff(w[k, 0]) == 1).all() for k in range(w.shape[0]))  # consecutive windows every step
+    ml.ctx.variant_counts(reset=True)
+    res = ml.meta_step()
+    vc = ml.ctx.variant_counts()
+    assert vc["gcn_dedup"] >= cfg.inner_steps + 1, vc  # every inner step and the query (the sweep reuses F)
+    ref = oracle("cfg5-dedup", d, P, names, feats, ei, cfg, list(w[-1, 0]))
+    check(res, ml, ref, d, names, 1, cfg.inner_steps)
+
+
 # ----------------------------------------------------------------------------- (c) the benched step
 def test_bench_configuration_properties_and_determinism():
     """The bench's own meta-step: BASELINE config 2 (15 tasks x B=32 x T=24 x N=441, K=5, second

@@ -4,6 +4,7 @@ drop-in must not copy edge_index to the host (a sync) or re-pack the flat parame
 and must notice every change (replaced tensors, in-place writes, optimizer steps)."""
 import torch
 
+from weatherforecast_stgcn_maml_amd import params
 from weatherforecast_stgcn_maml_amd.config import CONFIG2
 from weatherforecast_stgcn_maml_amd.hybrid_model import HybridSTGCN_LSTM
 from weatherforecast_stgcn_maml_amd.model import STGCN, _GraphMemo
@@ -30,6 +31,7 @@ def _model():
                             d.forecast_horizon), d
 
 
+@torch.no_grad()
 def test_packed_parameters_cached_until_changed():
     m, d = _model()
     dev = torch.device("cpu")
@@ -39,7 +41,8 @@ def test_packed_parameters_cached_until_changed():
     w = m.lstm.weight_ih_l0
     opt = torch.optim.SGD(m.get_trainable_parameters(), lr=0.1)
     w.grad = torch.ones_like(w)
-    opt.step()                              # optimizer update in place: re-packed into the same buffer
+    with torch.enable_grad():
+        opt.step()                             # optimizer update in place: re-packed into the same buffer
     th3, fresh3 = m._packed(0, m._trainable_params(), d, dev)
     assert fresh3 and th3 is th1
     assert torch.equal(th3[:w.numel()].view_as(w), w.detach())
@@ -51,3 +54,35 @@ def test_packed_parameters_cached_until_changed():
     g1, f1 = m._packed(1, m._gcn_params(), d, dev)
     g2, f2 = m._packed(1, m._gcn_params(), d, dev)
     assert f1 and not f2 and g1 is g2
+
+
+def test_untracked_data_writes_are_picked_up():
+    """writes through ``.data`` do not move the version counter. Grad-enabled calls (the
+    training forward, whose vector the backward also uses) always re-pack; under no_grad a storage
+    swap is seen through the data pointer and an in-place ``.data`` write needs invalidate_packed()."""
+    m, d = _model()
+    dev = torch.device("cpu")
+    w = m.lstm.weight_hh_l1
+    lay = {n: off for n, _, off in params.trainable_layout(d)[0]}
+    off = lay["lstm.weight_hh_l1"]
+    th, _ = m._packed(0, m._trainable_params(), d, dev)
+    w.data.copy_(torch.full_like(w, 0.25))         # untracked in-place write
+    th2, fresh = m._packed(0, m._trainable_params(), d, dev)  # grad enabled: re-packed
+    assert fresh and th2 is th and float(th2[off]) == 0.25
+    with torch.no_grad():
+        m._packed(0, m._trainable_params(), d, dev)
+        w.data -= 0.25                             # untracked, under no_grad: the cache keeps the old copy ...
+        assert float(m._packed(0, m._trainable_params(), d, dev)[0][off]) == 0.25
+        m.invalidate_packed()                      # ... until invalidated
+        assert float(m._packed(0, m._trainable_params(), d, dev)[0][off]) == 0.0
+        w.data = torch.full_like(w, 2.0)           # storage swap: seen through data_ptr
+        th3, fresh3 = m._packed(0, m._trainable_params(), d, dev)
+        assert fresh3 and float(th3[off]) == 2.0
+
+
+def test_graph_memo_notices_storage_swap():
+    m = _GraphMemo()
+    ei = torch.tensor([[0, 1], [1, 0]])
+    m.put(ei, 1)
+    ei.data = torch.tensor([[1, 0], [0, 1]])
+    assert m.get(ei) is None

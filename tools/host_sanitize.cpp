@@ -4,12 +4,18 @@
 // Covers the code that validates and transforms caller input before any launch: dimension checks,
 // the parameter layout (state_dict order, 64-float padded offsets), the normalised ELL build of the
 // graph (gcn_norm with self loops, in-degree limit), and the error paths of the entry points
-// (NULL handles / buffers, no device). Exit status 0 = every check passed.
+// (NULL handles / buffers, no device). Round 5: also the launch-plan builders every kernel launch
+// depends on (kernels.h: the LSTM wavefront diagonals, the split-K weight-gradient plans and their
+// pairing, the grid-barrier sizing), built with -Werror=missing-field-initializers, each plan checked
+// field by field against what was asked for. Exit status 0 = every check passed.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <set>
+#include <utility>
 #include <vector>
 
+#include "kernels.h"
 #include "smaml.h"
 
 static int failures = 0;
@@ -52,8 +58,126 @@ static std::vector<int64_t> grid_edges(int side) {
   return ei;
 }
 
+static smaml::Dims kdims_cfg2() {
+  smaml::Dims d;
+  d.N = 441;
+  d.T = 24;
+  d.Cin0 = 24;
+  d.Hc = 256;
+  d.H = 128;
+  d.L = 4;
+  d.Hf = 8;
+  d.C = 12;
+  d.HfC = 96;
+  return d;
+}
+
+// The wavefront diagonals cover every (layer, step) exactly once, each problem's dependencies lie on
+// earlier diagonals, and the block ranges are disjoint, increasing multiples of the per-problem count.
+static void check_waves() {
+  using namespace smaml;
+  const Dims d = kdims_cfg2();
+  Work w;
+  w.Z = 5;
+  w.B = 32;
+  w.M = w.B * d.N;
+  ParamOff po;
+  for (int l = 0; l < d.L; ++l) po.lay[l].cin = l == 0 ? d.Hc : d.H;
+  std::set<std::pair<int, int>> fwd, bwd;
+  double ffl = 0.0, bfl = 0.0;
+  for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
+    FwdWave wv;
+    ffl += fwd_wave(d, w, po, diag, 16, false, wv);
+    CHECK(wv.n >= 1 && wv.n <= d.L && wv.off[0] == 0);
+    for (int q = 0; q < wv.n; ++q) {
+      CHECK(wv.l[q] + wv.t[q] == diag && wv.l[q] >= 0 && wv.l[q] < d.L && wv.t[q] >= 0 && wv.t[q] < d.T);
+      CHECK(wv.off[q + 1] - wv.off[q] == 16);
+      CHECK(fwd.insert({wv.l[q], wv.t[q]}).second);
+      CHECK(wv.lo[q].cin == po.lay[wv.l[q]].cin);
+    }
+    BwdWave bv;
+    bfl += bwd_wave(d, w, po, diag, 16, false, bv);
+    CHECK(bv.n >= 1 && bv.n <= d.L && bv.off[0] == 0);
+    for (int q = 0; q < bv.n; ++q) {
+      CHECK((d.L - 1 - bv.l[q]) + (d.T - 1 - bv.t[q]) == diag);
+      CHECK(bv.off[q + 1] - bv.off[q] == 16);
+      CHECK(bwd.insert({bv.l[q], bv.t[q]}).second);
+    }
+  }
+  CHECK((int)fwd.size() == d.L * d.T && (int)bwd.size() == d.L * d.T);
+  // LSTM fwd = 2 T N 4H (Hc + H) + 2 T N 4H 2H (L - 1) per sample, less the recurrent
+  // products of the t = 0 steps (h_{-1} = 0: not executed, not counted)
+  const double lstm = 2.0 * d.T * d.N * 4 * d.H * (d.Hc + d.H) + 2.0 * d.T * d.N * 4 * d.H * 2 * d.H * (d.L - 1) -
+                      2.0 * d.N * 4 * d.H * d.H * d.L;
+  CHECK(std::fabs(ffl - lstm * w.Z * w.B) <= 1e-9 * ffl);
+  CHECK(bfl > 0.0);
+}
+
+// plan_wgrad fills every field from its arguments, its K slices cover [0, K) exactly, and its partial
+// slabs fit the buffer; pair_wgrad keeps both halves inside the buffer or leaves the plan unchanged.
+static void check_wgrad_plans() {
+  using namespace smaml;
+  Work w;
+  w.Z = 5;
+  w.B = 32;
+  w.M = w.B * 441;
+  w.wpart_floats = (int64_t)w.Z * 512 * (256 + 128 + 1) * SMAML_WGRAD_MAXSPLIT;
+  w.wpart = reinterpret_cast<float*>(0x1000);
+  w.kn.wgrad_wide = 1;
+  const float* A = reinterpret_cast<const float*>(0x2000);
+  const float* B1 = reinterpret_cast<const float*>(0x3000);
+  const float* B2 = reinterpret_cast<const float*>(0x4000);
+  float* grad = reinterpret_cast<float*>(0x5000);
+  struct Case {
+    int Mrows, c1, c2;
+    int64_t K;
+  } cases[] = {{512, 256, 128, 24LL * 14112}, {512, 128, 128, 24LL * 14112}, {96, 128, 0, 14112},
+               {512, 128, 128, 24LL * 441}, {512, 256, 128, 16}, {96, 128, 0, 1}};
+  for (const Case& k : cases) {
+    WgradPlan p;
+    plan_wgrad(w, A, 11, k.Mrows, B1, 12, k.c1, k.c2 ? B2 : nullptr, 13, k.c2, k.K, 7, grad, 606336, 100, 200, 300,
+               400, true, false, p);
+    CHECK(p.A == A && p.a_zstride == 11 && p.Mrows == k.Mrows && p.B1 == B1 && p.c1 == k.c1 && p.c2 == k.c2);
+    CHECK(p.B2 == (k.c2 ? B2 : nullptr) && p.b1_zstride == 12 && p.b2_zstride == 13 && p.K == k.K && p.Mshift == 7);
+    CHECK(p.grad == grad && p.P == 606336 && p.off_w1 == 100 && p.off_w2 == 200 && p.off_b1 == 300 && p.off_b2 == 400);
+    CHECK(p.with_bias && !p.accumulate && p.Z == w.Z && p.part == w.wpart && p.ldp == k.c1 + k.c2 + 1);
+    CHECK(p.ntm >= 1 && p.ntn >= 1 && p.nsplit >= 1 && p.kchunk >= 1);
+    CHECK((int64_t)p.nsplit * p.kchunk >= k.K && (int64_t)(p.nsplit - 1) * p.kchunk < k.K);
+    CHECK((int64_t)p.nsplit * p.Z * p.Mrows * p.ldp <= w.wpart_floats);
+    CHECK(p.A2 == nullptr && p.nsplit1 == 0 && p.drop_layer == -1 && p.drop.thr_lstm == 0);
+    WgradPlan q = p;
+    if (pair_wgrad(q, w, A, B1, B2)) {
+      CHECK(q.nsplit == 2 * q.nsplit1 && q.A2 == A && q.B1s == B1 && q.B2s == B2);
+      CHECK((int64_t)q.nsplit1 * q.kchunk >= k.K && (int64_t)(q.nsplit1 - 1) * q.kchunk < k.K);
+      CHECK((int64_t)q.nsplit * q.Z * q.Mrows * q.ldp <= w.wpart_floats);
+    } else {
+      CHECK(q.nsplit == p.nsplit && q.kchunk == p.kchunk && q.A2 == nullptr);
+    }
+  }
+  // a slab buffer too small for two slices: the pair is refused, the plan stays as planned
+  Work tiny = w;
+  tiny.wpart_floats = (int64_t)w.Z * 512 * 385;
+  WgradPlan p;
+  plan_wgrad(tiny, A, 0, 512, B1, 0, 256, B2, 0, 128, 24LL * 14112, 0, grad, 0, 0, 0, 0, 0, true, false, p);
+  CHECK(p.nsplit == 1);
+  CHECK(!pair_wgrad(p, tiny, A, B1, B2) && p.nsplit == 1 && p.A2 == nullptr);
+}
+
+static void check_barrier_grid() {
+  using smaml::grid_barrier_grid;
+  CHECK(grid_barrier_grid(0, 100, 0) == 0);      // capacity unknown: the two-launch form
+  CHECK(grid_barrier_grid(1024, 0, 0) == 0);
+  CHECK(grid_barrier_grid(1024, 100, 0) == 100);  // fewer items than a quarter of the capacity
+  CHECK(grid_barrier_grid(1024, 5000, 0) == 256);
+  CHECK(grid_barrier_grid(3, 5000, 0) == 1);
+  CHECK(grid_barrier_grid(1024, 5000, 2) == 2049);  // debug oversize: never co-resident
+}
+
 int main() {
   CHECK(smaml_abi_version() == 6);
+  check_waves();
+  check_wgrad_plans();
+  check_barrier_grid();
   CHECK(smaml_build_info() != nullptr && std::strlen(smaml_build_info()) > 0);
 
   // ---- parameter layout (hybrid_model.py state_dict order) ----

@@ -8,11 +8,13 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <dlfcn.h>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -221,8 +223,9 @@ struct smaml_ctx {
   float* scratch_loss = nullptr;  // [(steps+1)*Z] fallback when the caller passes no buffer
   int64_t scratch_loss_cap = 0;
   // device pointer table for sample windows (uploaded through the pinned staging ring)
-  const float** xtab = nullptr;
+  const float** xtab = nullptr;  // never index directly: xtab_at (the table moves when it grows)
   int64_t xtab_cap = 0;
+  int64_t xtab_n = 0;  // entries of the last upload_xtab
   Staging stage;
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
@@ -282,8 +285,10 @@ struct smaml_ctx {
   // activations of the last smaml_forward / smaml_lstm_forward (single task, act_B samples);
   // -1 once anything else has used the workspace (the backward consumes them: dG in place)
   int act_B = -1;
-  // RCCL communicator (smaml_comm_init), opaque
+  // RCCL communicator (smaml_comm_init), opaque; created non-blocking when the library allows it
   void* comm = nullptr;
+  int comm_nb = 0;
+  int64_t comm_timeout_ms = 120000;  // smaml_set_option("comm_timeout_ms")
 };
 
 namespace {
@@ -538,6 +543,7 @@ int ensure_xtab(smaml_ctx* c, int64_t n) {
     HIP_TRY(hipFree((void*)c->xtab));
   }
   const int64_t cap = std::max<int64_t>(n, 1024);
+  c->xtab_n = 0;
   HIP_TRY(hipMalloc((void**)&c->xtab, cap * sizeof(float*)));
   c->xtab_cap = cap;
   return SMAML_OK;
@@ -545,7 +551,21 @@ int ensure_xtab(smaml_ctx* c, int64_t n) {
 
 int upload_xtab(smaml_ctx* c, hipStream_t s, const float* const* ptrs, int64_t n) {
   TRY(ensure_xtab(c, n));
-  return c->stage.upload(s, (void*)c->xtab, ptrs, n * (int64_t)sizeof(float*));
+  c->xtab_n = 0;
+  TRY(c->stage.upload(s, (void*)c->xtab, ptrs, n * (int64_t)sizeof(float*)));
+  c->xtab_n = n;
+  return SMAML_OK;
+}
+
+// Device address of entry i of the window table. The only way table pointers are formed: after the
+// upload_xtab that wrote entry i (ensure_xtab may move the table, so a pointer taken before an upload
+// could dangle -- the fault class of round 4's first gcn_dedup run).
+int xtab_at(const smaml_ctx* c, int64_t i, const float* const** out) {
+  if (!c->xtab || i < 0 || i >= c->xtab_n)
+    return fail(SMAML_EINVAL, "internal: window-table entry " + std::to_string(i) + " read before its upload (" +
+                                  std::to_string(c->xtab_n) + " uploaded)");
+  *out = c->xtab + i;
+  return SMAML_OK;
 }
 
 void set_work(smaml_ctx* c, int Z, int B) {
@@ -763,7 +783,10 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   // layer-0 steps' latency-bound K loops cover only the recurrent segment (kernels_small.hip).
   w.xg = nullptr;
   w.xg_src = nullptr;
-  if (small_kw_ok(d, w) && (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows) {
+  // only the kw kernel reads the hoisted projection: hoist when every diagonal with a layer-0 step takes it
+  bool hoist = small_kw_ok(d, w) && (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows;
+  for (int diag = 0; hoist && diag < d.T; ++diag) hoist = fwd_wave_kw(d, w, c->po, diag);
+  if (hoist) {
     const int64_t per = (int64_t)d.T * w.M * 4 * d.H, need = per * w.Z;
     if (need > c->xg_cap) {
       if (c->xg_buf) HIP_TRY(hipFree(c->xg_buf));
@@ -785,7 +808,7 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
-    if (w.xg)  // (the hoisted projection's flops are counted above)
+    if (w.xg && fwd_wave_kw(d, w, c->po, diag))  // (the hoisted projection's flops are counted above)
       for (int q = 0; q < wv.n; ++q)
         if (wv.l[q] == 0) fl -= 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
     TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
@@ -1298,11 +1321,13 @@ int smaml_forward(smaml_ctx* c, void* stream, const float* theta, const float* c
   TRY(reserve(c, 1, nsamples));
   set_work(c, 1, nsamples);
   TRY(upload_xtab(c, s, x_host, nsamples));
+  const float* const* xt = nullptr;
+  TRY(xtab_at(c, 0, &xt));
   if (c->p_gcn > 0.f || c->p_lstm > 0.f) {  // train-mode module forward: masks of (seed, task id, step 0)
     TRY(upload_task_ids(c, s, 1));
     set_step_drop(c, 0);  // kept in c->w.drop for the smaml_backward of these activations
   }
-  TRY(run_forward(c, s, theta, 0, c->xtab));
+  TRY(run_forward(c, s, theta, 0, xt));
   Work w = c->w;
   w.pred = pred;
   launch_head_loss(s, c->d, w, theta, 0, c->po, nullptr, 0.f, false);
@@ -1368,7 +1393,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
         ptrs[i] = c->feats[z] + (int64_t)wv * d.N * d.Cin0;
       }
   // steps whose every task reads B consecutive windows (the reference's support and query batches)
-  std::vector<const float* const*> consec(steps + 1, nullptr);
+  std::vector<char> is_consec(steps + 1, 0);
   for (int k = 0; k <= steps; ++k) {
     bool ok = B > 1;
     for (int z = 0; z < Z && ok; ++z) {
@@ -1376,11 +1401,15 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       for (int b = 1; b < B && ok; ++b) ok = wz[b] == wz[0] + b;
     }
     for (int z = 0; z < Z; ++z) ptrs[nptr + (int64_t)k * Z + z] = ptrs[((int64_t)k * Z + z) * B];
-    consec[k] = ok ? ptrs.data() : nullptr;  // (flag only: the device table may move in upload_xtab)
+    is_consec[k] = ok;
   }
   TRY(upload_xtab(c, s, ptrs.data(), (int64_t)ptrs.size()));
-  for (int k = 0; k <= steps; ++k)
-    if (consec[k]) consec[k] = c->xtab + nptr + (int64_t)k * Z;
+  // device table pointers per step: windows [k][Z][B] and (consecutive steps) first windows [k][Z]
+  std::vector<const float* const*> xstep(steps + 1, nullptr), consec(steps + 1, nullptr);
+  for (int k = 0; k <= steps; ++k) {
+    TRY(xtab_at(c, (int64_t)k * Z * B, &xstep[k]));
+    if (is_consec[k]) TRY(xtab_at(c, nptr + (int64_t)k * Z, &consec[k]));
+  }
   if (!losses) {
     const int64_t need = (int64_t)(steps + 1) * Z;
     if (need > c->scratch_loss_cap) {
@@ -1398,7 +1427,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   const double head_fl = 2.0 * Z * c->w.M * d.HfC * d.H;
   const bool so = order == 2;
   for (int k = 0; k < steps; ++k) {
-    const float* const* xt = c->xtab + (int64_t)k * Z * B;
+    const float* const* xt = xstep[k];
     if (dropout) set_step_drop(c, k);
     if (so) {
       HIP_TRY(hipMemcpyAsync(c->so_theta + (int64_t)k * Z * P, c->fast, (size_t)Z * P * 4, hipMemcpyDeviceToDevice, s));
@@ -1424,7 +1453,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
                                      norms ? norms + (int64_t)k * Z : nullptr, nullptr, bar_plan(c))));
     }
   }
-  const float* const* xq = c->xtab + (int64_t)steps * Z * B;
+  const float* const* xq = xstep[steps];
   c->w.F = c->F_main;
   use_primal(c, nkeep > 0 ? SET_QUERY : SET_MAIN);  // slot 0 holds the workspace's own Hs/Cs/Gs
   if (dropout) set_step_drop(c, steps);
@@ -1452,7 +1481,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
                                         bar_plan(c))));
     for (int k = steps - 1; k >= 0; --k) {
       const float* th = c->so_theta + (int64_t)k * Z * P;
-      const float* const* xt = c->xtab + (int64_t)k * Z * B;
+      const float* const* xt = xstep[k];
       c->w.F = c->so_F ? c->so_F + (int64_t)k * Z * B * d.T * d.N * d.Hc : c->F_main;
       const int slot = steps - 1 - k;
       use_primal(c, slot < nkeep ? slot : SET_MAIN);
@@ -1503,7 +1532,9 @@ static int ad_cache_fill(smaml_ctx* c, hipStream_t s, const int32_t* windows, in
     while (j < need.size() && need[j] == need[j - 1] + 1 && (int)(j - i) < c->ad_gcn_batch) ++j;
     set_work(c, (int)(j - i), 1);
     c->w.F = c->ad_F + (int64_t)need[i] * fsz;
-    TRY(run_gcn(c, s, c->xtab + i));
+    const float* const* xt = nullptr;
+    TRY(xtab_at(c, (int64_t)i, &xt));
+    TRY(run_gcn(c, s, xt));
     for (size_t k = i; k < j; ++k) c->ad_valid[need[k]] = 1;
     i = j;
   }
@@ -1556,7 +1587,8 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
   set_work(c, 1, B);
   TRY(upload_xtab(c, s, ptrs.data(), nptr));
   for (int k = 0; k < nsteps; ++k) {
-    const float* const* xt = c->xtab + (int64_t)k * B;
+    const float* const* xt = nullptr;
+    TRY(xtab_at(c, (int64_t)k * B, &xt));
     if (dropout) set_step_drop(c, step0 + k);
     if (cache) {
       const int wv = windows_host[k];
@@ -1657,6 +1689,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->bar_fused = (int)value;
   } else if (k == "barrier_timeout_us" && value >= 1) {
     c->bar_timeout_us = std::min<int64_t>(value, 600000000);
+  } else if (k == "comm_timeout_ms" && value >= 1) {
+    c->comm_timeout_ms = std::min<int64_t>(value, 3600000);
   } else if (k == "barrier_oversize" && value >= 0 && value <= 64) {
     c->bar_oversize = (int)value;
   } else if (k == "keep" && value >= -1) {
@@ -1721,7 +1755,9 @@ int smaml_gcn_forward(smaml_ctx* c, void* stream, const float* const* x_host, in
   TRY(reserve(c, 1, nsamples));
   set_work(c, 1, nsamples);
   TRY(upload_xtab(c, s, x_host, nsamples));
-  TRY(run_gcn(c, s, c->xtab));
+  const float* const* xt = nullptr;
+  TRY(xtab_at(c, 0, &xt));
+  TRY(run_gcn(c, s, xt));
   const Dims& d = c->d;
   const int64_t blk = (int64_t)d.N * d.Hc;
   for (int si = 0; si < nsamples; ++si)  // F [T][M][Hc] -> feats [s][T*N][Hc]
@@ -1786,9 +1822,11 @@ int smaml_head_loss(smaml_ctx* c, void* stream, const float* theta, const float*
       if (!y_host[i]) return fail(SMAML_EINVAL, "null target pointer");
     TRY(upload_xtab(c, s, y_host, nsamples));
   }
+  const float* const* yt = nullptr;
+  if (y_host) TRY(xtab_at(c, 0, &yt));
   const Dims& d = c->d;
   const float inv = 1.f / ((float)nsamples * d.N * d.HfC);  // mean over samples and elements (F9)
-  launch_head_loss_y(s, d, c->w, hT, theta, c->po, y_host ? c->xtab : nullptr, pred, dpred, 2.f * inv);
+  launch_head_loss_y(s, d, c->w, hT, theta, c->po, yt, pred, dpred, 2.f * inv);
   if (y_host) launch_loss_final(s, c->w, inv, loss);
   c->w = saved;
   c->act_B = act;
@@ -1849,15 +1887,29 @@ int smaml_free(smaml_ctx* c, void* p) {
 // so the library has no link-time RCCL dependency (and shares the process's RCCL if torch
 // has already loaded one). Only the handful of symbols below are used.
 namespace {
+// ncclConfig_t as of NCCL 2.14 (size / magic / version + the first user fields): the library reads only
+// the fields the declared version has, so this prefix works with the RCCL torch bundles and /opt/rocm's
+struct NcclConfig214 {
+  size_t size = sizeof(NcclConfig214);
+  unsigned magic = 0xcafebeef;
+  unsigned version = 21400;  // NCCL_VERSION(2, 14, 0)
+  int blocking = 0;          // non-blocking: ncclCommInitRankConfig returns at once, progress is polled
+  int cgaClusterSize = (int)0x80000000, minCTAs = (int)0x80000000, maxCTAs = (int)0x80000000;  // UNDEF_INT
+  const char* netName = nullptr;
+};
 struct Rccl {
   void* h = nullptr;
   int (*get_unique_id)(void*) = nullptr;                                   // ncclGetUniqueId
   int (*comm_init_rank)(void**, int, std::array<char, 128>, int) = nullptr;  // ncclCommInitRank
+  int (*comm_init_rank_config)(void**, int, std::array<char, 128>, int, NcclConfig214*) = nullptr;
+  int (*get_async_error)(void*, int*) = nullptr;                           // ncclCommGetAsyncError
+  int (*comm_abort)(void*) = nullptr;                                      // ncclCommAbort
   int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
   int (*comm_destroy)(void*) = nullptr;
   const char* (*error_string)(int) = nullptr;
+  bool nonblocking() const { return comm_init_rank_config && get_async_error && comm_abort; }
 };
-constexpr int NCCL_FLOAT32 = 7, NCCL_SUM = 0;  // ncclFloat32, ncclSum (nccl.h enums)
+constexpr int NCCL_FLOAT32 = 7, NCCL_SUM = 0, NCCL_IN_PROGRESS = 7;  // ncclFloat32, ncclSum, ncclInProgress
 
 int rccl(Rccl** out) {
   static Rccl r;
@@ -1872,6 +1924,10 @@ int rccl(Rccl** out) {
     if (r.h) {
       r.get_unique_id = (int (*)(void*))dlsym(r.h, "ncclGetUniqueId");
       r.comm_init_rank = (int (*)(void**, int, std::array<char, 128>, int))dlsym(r.h, "ncclCommInitRank");
+      r.comm_init_rank_config =
+          (int (*)(void**, int, std::array<char, 128>, int, NcclConfig214*))dlsym(r.h, "ncclCommInitRankConfig");
+      r.get_async_error = (int (*)(void*, int*))dlsym(r.h, "ncclCommGetAsyncError");
+      r.comm_abort = (int (*)(void*))dlsym(r.h, "ncclCommAbort");
       r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(r.h, "ncclAllReduce");
       r.comm_destroy = (int (*)(void*))dlsym(r.h, "ncclCommDestroy");
       r.error_string = (const char* (*)(int))dlsym(r.h, "ncclGetErrorString");
@@ -1886,6 +1942,23 @@ int rccl(Rccl** out) {
 int nccl_fail(Rccl* r, int rc, const char* what) {
   return fail(SMAML_EHIP, std::string(what) + ": " + (r->error_string ? r->error_string(rc) : std::to_string(rc)));
 }
+
+// A non-blocking communicator's call returned rc: wait (bounded) until its state leaves ncclInProgress.
+// Returns the final state (0 = success), or -1 on timeout.
+int nccl_wait(Rccl* r, void* comm, int rc, int64_t timeout_ms) {
+  if (rc != NCCL_IN_PROGRESS || !comm || !r->get_async_error) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    int st = 0;
+    const int q = r->get_async_error(comm, &st);
+    if (q != 0) return q;
+    if (st != NCCL_IN_PROGRESS) return st;
+    if (std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+        timeout_ms)
+      return -1;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -1898,6 +1971,10 @@ int smaml_comm_unique_id(uint8_t* id_out) {
   return rc ? nccl_fail(r, rc, "ncclGetUniqueId") : SMAML_OK;
 }
 
+// Bounded: with ncclCommInitRankConfig available the communicator is created non-blocking and its
+// progress polled for at most comm_timeout_ms (smaml_set_option "comm_timeout_ms", default 120 s), so a
+// rank whose peers never arrive (one of them failed before or inside its init) returns SMAML_EHIP
+// instead of blocking forever; the half-built communicator is aborted.
 int smaml_comm_init(smaml_ctx* c, int32_t rank, int32_t world, const uint8_t* id) {
   if (!c || !id || world < 1 || rank < 0 || rank >= world) return fail(SMAML_EINVAL, "bad comm_init arguments");
   if (c->comm) return fail(SMAML_ESTATE, "communicator already initialised");
@@ -1907,8 +1984,27 @@ int smaml_comm_init(smaml_ctx* c, int32_t rank, int32_t world, const uint8_t* id
   std::array<char, 128> uid;
   std::memcpy(uid.data(), id, 128);
   void* comm = nullptr;
-  const int rc = r->comm_init_rank(&comm, world, uid, rank);
-  if (rc) return nccl_fail(r, rc, "ncclCommInitRank");
+  if (r->nonblocking()) {
+    NcclConfig214 cfg;
+    int rc = r->comm_init_rank_config(&comm, world, uid, rank, &cfg);
+    if (rc != 0 && rc != NCCL_IN_PROGRESS) {
+      if (comm) (void)r->comm_abort(comm);
+      return nccl_fail(r, rc, "ncclCommInitRankConfig");
+    }
+    rc = nccl_wait(r, comm, NCCL_IN_PROGRESS, c->comm_timeout_ms);
+    if (rc != 0) {
+      if (comm) (void)r->comm_abort(comm);
+      if (rc < 0)
+        return fail(SMAML_EHIP, "ncclCommInitRankConfig: timed out after " + std::to_string(c->comm_timeout_ms) +
+                                    " ms waiting for the other ranks (communicator aborted)");
+      return nccl_fail(r, rc, "ncclCommInitRankConfig");
+    }
+    c->comm_nb = 1;
+  } else {
+    const int rc = r->comm_init_rank(&comm, world, uid, rank);
+    if (rc) return nccl_fail(r, rc, "ncclCommInitRank");
+    c->comm_nb = 0;
+  }
   c->comm = comm;
   return SMAML_OK;
 }
@@ -1919,7 +2015,9 @@ int smaml_comm_allreduce(smaml_ctx* c, void* stream, float* buf, int64_t n) {
   Rccl* r = nullptr;
   TRY(rccl(&r));
   TRY(ensure_device(c));
-  const int rc = r->all_reduce(buf, buf, (size_t)n, NCCL_FLOAT32, NCCL_SUM, c->comm, (hipStream_t)stream);
+  int rc = r->all_reduce(buf, buf, (size_t)n, NCCL_FLOAT32, NCCL_SUM, c->comm, (hipStream_t)stream);
+  if (c->comm_nb) rc = nccl_wait(r, c->comm, rc, c->comm_timeout_ms);  // enqueue completes (not the collective)
+  if (rc < 0) return fail(SMAML_EHIP, "ncclAllReduce: enqueue timed out");
   return rc ? nccl_fail(r, rc, "ncclAllReduce") : SMAML_OK;
 }
 
@@ -1928,7 +2026,8 @@ int smaml_comm_destroy(smaml_ctx* c) {
   if (!c->comm) return SMAML_OK;
   Rccl* r = nullptr;
   TRY(rccl(&r));
-  const int rc = r->comm_destroy(c->comm);
+  int rc = r->comm_destroy(c->comm);
+  if (c->comm_nb && rc == NCCL_IN_PROGRESS) rc = 0;  // a non-blocking destroy finishes on its own
   c->comm = nullptr;
   return rc ? nccl_fail(r, rc, "ncclCommDestroy") : SMAML_OK;
 }

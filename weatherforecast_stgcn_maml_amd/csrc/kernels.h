@@ -9,34 +9,37 @@ namespace smaml {
 constexpr int ELLW = 8;        // ELL width of the normalised t=0 adjacency (max in-degree 6 + self)
 constexpr int MAX_LAYERS = 8;
 
+// Every host-built plan / launch-argument struct below gives each member a default initialiser, so a
+// plan a caller fills only partly can never hand a kernel an indeterminate field (round 4 found two
+// faults of that class; tools/host_sanitize.cpp builds this header with -Werror=missing-field-initializers).
 struct Dims {
-  int N;      // nodes per region (graph size)
-  int T;      // window (time steps)
-  int Cin0;   // input channels (24)
-  int Hc;     // GCN hidden channels (256)
-  int H;      // LSTM hidden (128)
-  int L;      // LSTM layers (4)
-  int Hf;     // forecast horizon (8)
-  int C;      // output channels (12)
-  int HfC;    // head width (96)
+  int N = 0;      // nodes per region (graph size)
+  int T = 0;      // window (time steps)
+  int Cin0 = 0;   // input channels (24)
+  int Hc = 0;     // GCN hidden channels (256)
+  int H = 0;      // LSTM hidden (128)
+  int L = 0;      // LSTM layers (4)
+  int Hf = 0;     // forecast horizon (8)
+  int C = 0;      // output channels (12)
+  int HfC = 0;    // head width (96)
 };
 
 struct LayerOff {
-  int64_t wih, whh, bih, bhh;  // offsets into the flat trainable vector
-  int cin;
+  int64_t wih = 0, whh = 0, bih = 0, bhh = 0;  // offsets into the flat trainable vector
+  int cin = 0;
 };
 
 struct ParamOff {
-  LayerOff lay[MAX_LAYERS];
-  int64_t wo, bo;
-  int64_t P;  // padded flat size (stride between tasks' fast weights)
-  int64_t n_valid;
+  LayerOff lay[MAX_LAYERS] = {};
+  int64_t wo = 0, bo = 0;
+  int64_t P = 0;  // padded flat size (stride between tasks' fast weights)
+  int64_t n_valid = 0;
 };
 
 struct GcnOff {
-  int64_t w[4], b[4];
-  int cin[4];
-  int64_t total;
+  int64_t w[4] = {}, b[4] = {};
+  int cin[4] = {};
+  int64_t total = 0;
 };
 
 // Train-mode dropout (hybrid_model.py:67,70,73 GCN outputs; nn.LSTM's inter-layer dropout :47;
@@ -63,11 +66,11 @@ __host__ __device__ inline bool drop_keep(uint32_t site, uint64_t idx, uint32_t 
   return (mix32(site ^ (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x9E3779B9U)) >> 8) >= thr;
 }
 struct Drop {
-  uint32_t seed;
-  int step;                  // inner step (K = the query batch) whose forward the masks belong to
-  uint32_t thr_gcn, thr_lstm;  // round(p * 2^24); 0 = off
-  float sc_gcn, sc_lstm;     // 1 / (1 - p)
-  const int* task_id;        // [Z] global task id of each workspace task (device)
+  uint32_t seed = 0;
+  int step = 0;                      // inner step (K = the query batch) whose forward the masks belong to
+  uint32_t thr_gcn = 0, thr_lstm = 0;  // round(p * 2^24); 0 = off
+  float sc_gcn = 1.f, sc_lstm = 1.f;  // 1 / (1 - p)
+  const int* task_id = nullptr;      // [Z] global task id of each workspace task (device)
   __host__ __device__ bool gcn() const { return thr_gcn != 0; }
   __host__ __device__ bool lstm() const { return thr_lstm != 0; }
 };
@@ -112,21 +115,21 @@ enum Variant {
 
 // Run-time tile-selection knobs (smaml_set_option; defaults = the build-time thresholds).
 struct Knobs {
-  int bwd_big_min;   // BPTT launches with >= this many 64-row x 128-unit tile units (a 128 x 128 big tile counts
+  int bwd_big_min = 0;   // BPTT launches with >= this many 64-row x 128-unit tile units (a 128 x 128 big tile counts
                      // 2) use the big tiles (else 64x64 / split-K)
-  int bwdd_big_min;  // same, tangent BPTT
-  int split_max;     // split-K ways for small-grid LSTM steps (1 = off)
-  int wgrad_group_max_rows;  // backward with Z*M <= this: all LSTM weight gradients in one launch
-  int wgrad_group_wgs;       // workgroups that grouped launch aims for
-  int gcn_fused;             // 1: GCN rows t >= 1 through the fused four-layer kernel (k_gcn_mlp)
-  int gate_img;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
-  int wgrad_wide;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
-  int wgrad_pair;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
-  int wgrad_ws;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
-  int bwdd_remap;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
-  int small_kw;              // small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip):
+  int bwdd_big_min = 0;  // same, tangent BPTT
+  int split_max = 1;     // split-K ways for small-grid LSTM steps (1 = off)
+  int wgrad_group_max_rows = 0;  // backward with Z*M <= this: all LSTM weight gradients in one launch
+  int wgrad_group_wgs = 1;       // workgroups that grouped launch aims for
+  int gcn_fused = 0;             // 1: GCN rows t >= 1 through the fused four-layer kernel (k_gcn_mlp)
+  int gate_img = 0;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
+  int wgrad_wide = 0;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
+  int wgrad_pair = 0;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
+  int wgrad_ws = 0;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
+  int bwdd_remap = 0;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
+  int small_kw = 0;              // small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip):
                              // 1 = on, 2 = on with pre-split BPTT weight images (launch_split_bwd), 0 = split-K pairs
-  int gcn_dedup;             // 1: batches of consecutive windows run the fused GCN rows once per distinct stream row
+  int gcn_dedup = 0;             // 1: batches of consecutive windows run the fused GCN rows once per distinct stream row
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -161,10 +164,10 @@ struct Knobs {
 // splitting them in every workgroup (the weights are the same for all row tiles of a launch).
 constexpr int GATE_IMG_BYTES = 3 * 128 * 16 * 2;
 struct GateImgs {
-  char* th;                    // images of theta (launch_split_gate), null = not built
-  char* u;                     // images of the tangent direction U (second-order sweep), or null
-  int64_t tstride;             // bytes per task
-  int64_t off[MAX_LAYERS][2];  // byte offset of (layer, W_ih | W_hh) in a task's images
+  char* th = nullptr;               // images of theta (launch_split_gate), null = not built
+  char* u = nullptr;                // images of the tangent direction U (second-order sweep), or null
+  int64_t tstride = 0;              // bytes per task
+  int64_t off[MAX_LAYERS][2] = {};  // byte offset of (layer, W_ih | W_hh) in a task's images
 };
 // ---- pre-split BPTT weight images (kernels_small.hip launch_split_bwd; small-grid BPTT) ----
 // Per task, for W_hh of every layer and W_ih of layers >= 1 (the [4H][H] matrices the BPTT step reads
@@ -172,45 +175,45 @@ struct GateImgs {
 // [32 units][16 k], so a lane's MFMA B fragment (unit jj, k = 8h .. 8h + 7) is one 16-B load per plane.
 constexpr int BWD_IMG_BYTES = 3 * 32 * 16 * 2;
 struct BwdImgs {
-  char* th;                   // null = not built
-  int64_t tstride;            // bytes per task
-  int64_t off_hh[MAX_LAYERS];  // byte offset of W_hh(l) in a task's images
-  int64_t off_ih[MAX_LAYERS];  // ... W_ih(l), l >= 1 (0 for l = 0: not built)
+  char* th = nullptr;               // null = not built
+  int64_t tstride = 0;              // bytes per task
+  int64_t off_hh[MAX_LAYERS] = {};  // byte offset of W_hh(l) in a task's images
+  int64_t off_ih[MAX_LAYERS] = {};  // ... W_ih(l), l >= 1 (0 for l = 0: not built)
 };
 struct Work {
-  int Z, B, M;
-  BwdImgs bimg;            // pre-split BPTT weight images (launch_split_bwd), small-grid BPTT only
-  const float* bimg_src;   // the parameter vector bimg.th was split from
-  const float* xg;         // small-grid forward: layer 0's input projection F . W_ih0^T for all steps
+  int Z = 0, B = 0, M = 0;
+  BwdImgs bimg{};           // pre-split BPTT weight images (launch_split_bwd), small-grid BPTT only
+  const float* bimg_src = nullptr; // the parameter vector bimg.th was split from
+  const float* xg = nullptr;       // small-grid forward: layer 0's input projection F . W_ih0^T for all steps
                            // [Z][T][M][4H] (run_lstm), or null: the layer-0 steps form it themselves
-  const float* xg_src;     // the parameter vector xg was formed with
-  GateImgs gimg;           // pre-split images of the weights the gate GEMMs read (launch_split_gate)
-  const float* gimg_src;   // the parameter vector gimg.th was split from (kernels use it only for that one)
-  const float* gimg_u_src; // ... and gimg.u (the sweep's tangent direction)
-  int64_t* vcount;         // [NVAR] launch counters (ctx-owned; may be null)
-  Knobs kn;
-  float *gcnA, *gcnB;      // [Z*B][T*N][Hc] ping-pong
-  float* F;                // [Z][T][M][Hc] LSTM layer-0 input
-  float *Hs, *Cs, *Gs;     // [L][Z][T][M][H] / [L][Z][T][M][H] / [L][Z][T][M][4H]
-  float* dG;               // BPTT output [L][Z][T][M][4H]: == Gs (in place) unless the step's
+  const float* xg_src = nullptr;   // the parameter vector xg was formed with
+  GateImgs gimg{};         // pre-split images of the weights the gate GEMMs read (launch_split_gate)
+  const float* gimg_src = nullptr; // the parameter vector gimg.th was split from (kernels use it only for that one)
+  const float* gimg_u_src = nullptr;// ... and gimg.u (the sweep's tangent direction)
+  int64_t* vcount = nullptr;       // [NVAR] launch counters (ctx-owned; may be null)
+  Knobs kn{};
+  float *gcnA = nullptr, *gcnB = nullptr;    // [Z*B][T*N][Hc] ping-pong
+  float* F = nullptr;              // [Z][T][M][Hc] LSTM layer-0 input
+  float *Hs = nullptr, *Cs = nullptr, *Gs = nullptr;   // [L][Z][T][M][H] / [L][Z][T][M][H] / [L][Z][T][M][4H]
+  float* dG = nullptr;             // BPTT output [L][Z][T][M][4H]: == Gs (in place) unless the step's
                            // primal is kept for the second-order sweep (then its own slab)
-  float* dh;               // optional: the BPTT's dh [L][Z][T][M][H] (kept for the SO sweep)
-  int primal_kept;         // SO sweep: Hs/Cs/Gs/dG/dh hold this step's primal (tangent-only kernels)
-  float *dH, *dc;          // head's dh_T [Z][M][H]; cell-state carry per layer [L][Z][M][H]
+  float* dh = nullptr;             // optional: the BPTT's dh [L][Z][T][M][H] (kept for the SO sweep)
+  int primal_kept = 0;       // SO sweep: Hs/Cs/Gs/dG/dh hold this step's primal (tangent-only kernels)
+  float *dH = nullptr, *dc = nullptr;        // head's dh_T [Z][M][H]; cell-state carry per layer [L][Z][M][H]
                            // (the BPTT writes dG in place over Gs: [L][Z][T][M][4H])
-  float *pred, *dpred;     // [Z][M][HfC]
-  float* wpart;            // split-K partial slabs
-  int64_t wpart_floats;
-  float* lpart;            // loss partials [Z][lblocks]
-  int lblocks;
-  double* sqpart;          // [Z][SQB]
+  float *pred = nullptr, *dpred = nullptr;   // [Z][M][HfC]
+  float* wpart = nullptr;          // split-K partial slabs
+  int64_t wpart_floats = 0;
+  float* lpart = nullptr;          // loss partials [Z][lblocks]
+  int lblocks = 0;
+  double* sqpart = nullptr;        // [Z][SQB]
   // second-order (tangent) buffers; null unless reserved with so = true
-  float *RHs, *RCs, *RGs;  // like Hs, Cs, Gs
-  float *RdH, *Rdc;        // like dH, dc (R(dG) is written in place over RGs)
-  float* Rdpred;           // like dpred
+  float *RHs = nullptr, *RCs = nullptr, *RGs = nullptr;// like Hs, Cs, Gs
+  float *RdH = nullptr, *Rdc = nullptr;      // like dH, dc (R(dG) is written in place over RGs)
+  float* Rdpred = nullptr;         // like dpred
   // dropout (zero thresholds: off) and the masked head inputs drop(h_T), drop(R h_T) [Z][M][H]
-  Drop drop;
-  float *hTd, *RhTd;
+  Drop drop{};
+  float *hTd = nullptr, *RhTd = nullptr;
 };
 
 inline void count_variant(const Work& w, Variant v) {
@@ -233,9 +236,9 @@ constexpr int SQB = 64;  // blocks per task for squared-norm partials
 // Release: the block's stores are made visible before it arrives; acquire: the waiting lane's
 // agent-scope load invalidates this CU's L1, so the block then reads the other blocks' results.
 struct GridBar {
-  unsigned* w;        // device words [3]
-  int* host_err;      // pinned, device-mapped flag (may be null)
-  uint64_t timeout;   // wall_clock64 ticks a waiter spins before giving up
+  unsigned* w = nullptr;     // device words [3]
+  int* host_err = nullptr;   // pinned, device-mapped flag (may be null)
+  uint64_t timeout = 0;      // wall_clock64 ticks a waiter spins before giving up
 };
 __device__ __forceinline__ bool grid_barrier(const GridBar& gb, unsigned nb) {
   __shared__ int ok_s;
@@ -272,9 +275,9 @@ __device__ __forceinline__ bool grid_barrier(const GridBar& gb, unsigned nb) {
 // grid barrier (nb blocks, each looping over items), else the two phases as two launches of the same
 // kernel (same partition and summation order: bitwise-equal results).
 struct BarPlan {
-  GridBar gb;
-  int fused;     // 1: grid-barrier launch
-  int oversize;  // debug: > 0 launches oversize x the resident capacity + 1 blocks (never co-resident)
+  GridBar gb{};
+  int fused = 0;     // 1: grid-barrier launch
+  int oversize = 0;  // debug: > 0 launches oversize x the resident capacity + 1 blocks (never co-resident)
 };
 // Grid of a grid-barrier launch over `items` items given the kernel's resident capacity `cap` (blocks
 // the device holds at once): min(items, cap / 4) -- a quarter, so up to four processes sharing the GPU
@@ -302,18 +305,18 @@ int grid_barrier_capacity(const void* fn);  // resident blocks of fn on the curr
 // to L times wider (fills the chip when a rank holds few tasks). Problem p owns blocks
 // [off[p], off[p+1]) (multiples of 8, keeping the XCD-aware gate tile mapping).
 struct FwdWave {
-  int n;
-  int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
-  LayerOff lo[MAX_LAYERS];
+  int n = 0;
+  int l[MAX_LAYERS] = {}, t[MAX_LAYERS] = {}, off[MAX_LAYERS + 1] = {};
+  LayerOff lo[MAX_LAYERS] = {};
 };
 // Backward counterpart: problems (l, t) with (L-1-l) + (T-1-t) = e. Step (l, t) forms
 //   dh = [dG(l+1, t) | dG(l, t+1)] . [W_ih(l+1) ; W_hh(l)]   (one K = 8H GEMM; the dX of the
 // layer above is fused here instead of a separate GEMM), reading only the previous diagonal.
 struct BwdWave {
-  int n;
-  int l[MAX_LAYERS], t[MAX_LAYERS], off[MAX_LAYERS + 1];
-  LayerOff lo[MAX_LAYERS];
-  int64_t wih_up[MAX_LAYERS];  // W_ih offset of layer l+1 (unused at the top layer)
+  int n = 0;
+  int l[MAX_LAYERS] = {}, t[MAX_LAYERS] = {}, off[MAX_LAYERS + 1] = {};
+  LayerOff lo[MAX_LAYERS] = {};
+  int64_t wih_up[MAX_LAYERS] = {};  // W_ih offset of layer l+1 (unused at the top layer)
 };
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv);
@@ -334,9 +337,9 @@ void launch_gcn_layer(hipStream_t s, const Dims& d, int layer, int Zb, int B, co
 // Exact unsigned division by a run-time invariant d for n < 2^31 (one 64-bit multiply):
 // m = ceil(2^(32+s) / d), s = ceil(log2 d)  =>  n / d == (n * m) >> (32 + s).
 struct FastDiv {
-  uint64_t m;
-  uint32_t s;
-  uint32_t d;
+  uint64_t m = 0;
+  uint32_t s = 0;
+  uint32_t d = 0;
   FastDiv() = default;
   __host__ explicit FastDiv(uint32_t dd) : d(dd) {
     s = 0;
@@ -354,20 +357,20 @@ void launch_split_gate(hipStream_t s, const Dims& d, const ParamOff& po, const f
 
 // ---- fused GCN stack for the rows t >= 1 (kernels_gcn.hip) ----
 struct GcnWOff {  // offsets of conv{1..4}.lin.weight / conv{1..4}.bias in the GCN parameter vector
-  int64_t w[4], b[4];
+  int64_t w[4] = {}, b[4] = {};
 };
 struct GcnMlpArgs {
-  const float* const* xtab;  // [Z*B] sample window pointers ([T*N][Cin0] each)
-  const float* gcn;          // GCN parameter vector (biases)
-  GcnWOff wo;
-  const char* wimg;          // pre-split W images (launch_gcn_wsplit)
-  float* F;                  // [Z][T][B*N][Hc]
-  int64_t R1, M;             // rows t >= 1 over all samples; B*N
-  FastDiv rows_div, b_div, n_div;
-  int rows1, N, T, B, cin0;
-  int dedup;                 // 1: every task's B windows are consecutive; rows1 = (B + T - 2) * N distinct
+  const float* const* xtab = nullptr;  // [Z*B] sample window pointers ([T*N][Cin0] each)
+  const float* gcn = nullptr;          // GCN parameter vector (biases)
+  GcnWOff wo{};
+  const char* wimg = nullptr;          // pre-split W images (launch_gcn_wsplit)
+  float* F = nullptr;                  // [Z][T][B*N][Hc]
+  int64_t R1 = 0, M = 0;               // rows t >= 1 over all samples; B*N
+  FastDiv rows_div{}, b_div{}, n_div{};
+  int rows1 = 0, N = 0, T = 0, B = 0, cin0 = 0;
+  int dedup = 0;                       // 1: every task's B windows are consecutive; rows1 = (B + T - 2) * N distinct
                              // time steps per task, each row written to every (sample, t >= 1) holding it
-  Drop dr;
+  Drop dr{};
 };
 bool gcn_mlp_supported(const Dims& d);
 void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F);
@@ -409,6 +412,8 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 // kernels_small.hip: the small-grid (batch-1) forward / BPTT diagonal as one launch with the K
 // reduction split over the waves of a workgroup (used where the split-K pair would run)
 bool small_kw_ok(const Dims& d, const Work& w);
+// launch_lstm_fwd_wave runs diagonal `diag` as the kw kernel (the only forward form that reads w.xg)
+bool fwd_wave_kw(const Dims& d, const Work& w, const ParamOff& po, int diag);
 int64_t bwd_img_bytes(const Dims& d, BwdImgs* bi);  // per task; fills bi's offsets / tstride
 void launch_split_bwd(hipStream_t s, const Dims& d, const ParamOff& po, const float* theta, int64_t tstride, int Z,
                       const BwdImgs& bi);
@@ -424,20 +429,20 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
 // launch_wgrad split in its two launches (the GEMM into split-K partial slabs, then the
 // fixed-order reduce into the flat gradient), so each can be timed on its own.
 struct WgradPlan {
-  const float* A;
-  int64_t a_zstride;
-  int Mrows;
-  const float *B1, *B2;
-  int c1, c2;
-  int64_t K, Mshift;
-  int64_t b1_zstride, b2_zstride;
-  float* grad;
-  int64_t P, off_w1, off_w2, off_b1, off_b2;
-  bool with_bias, accumulate;
-  int Z;
-  float* part;
-  int ldp, ntm, ntn, nsplit;
-  int64_t kchunk;
+  const float* A = nullptr;
+  int64_t a_zstride = 0;
+  int Mrows = 0;
+  const float *B1 = nullptr, *B2 = nullptr;
+  int c1 = 0, c2 = 0;
+  int64_t K = 0, Mshift = 0;
+  int64_t b1_zstride = 0, b2_zstride = 0;
+  float* grad = nullptr;
+  int64_t P = 0, off_w1 = -1, off_w2 = -1, off_b1 = -1, off_b2 = -1;
+  bool with_bias = false, accumulate = false;
+  int Z = 0;
+  float* part = nullptr;
+  int ldp = 0, ntm = 0, ntn = 0, nsplit = 0;
+  int64_t kchunk = 0;
   Drop drop{};          // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
   int drop_layer = -1;  // (defaults: no dropout -- launch_wgrad's callers never set these)
   bool wide = false;    // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
@@ -459,9 +464,9 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
 // Several plans (same Z) in one GEMM launch + one reduce launch; their nsplit / kchunk / part are
 // re-planned for about target_wgs workgroups in total (partial slabs must fit w.wpart).
 struct WgMulti {
-  int n;
-  int blk[MAX_LAYERS], rblk[MAX_LAYERS];
-  WgradPlan p[MAX_LAYERS];
+  int n = 0;
+  int blk[MAX_LAYERS] = {}, rblk[MAX_LAYERS] = {};
+  WgradPlan p[MAX_LAYERS] = {};
 };
 void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs);
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);

@@ -650,6 +650,23 @@ static int small_grid_splits(int64_t tiles, int K, int bk, int64_t per_split_flo
   return S;
 }
 
+// Split count of diagonal `diag`'s small-grid (CfgGateP) form: > 1 = the split-K pair or the kw kernel.
+static int fwd_wave_splits(const Dims& d, const Work& w, const ParamOff& po, int diag) {
+  const int ntmP = (w.M + CfgGateP::BM - 1) / CfgGateP::BM;
+  const int ngrpP = (d.H + 32 * CfgGateP::WAVES_N - 1) / (32 * CfgGateP::WAVES_N);
+  FwdWave wvP{};
+  fwd_wave(d, w, po, diag, gate_blocks(ntmP, ngrpP), false, wvP);
+  int kmax = 0;
+  for (int q = 0; q < wvP.n; ++q) kmax = std::max(kmax, wvP.lo[q].cin + (wvP.t[q] > 0 ? d.H : 0));
+  const int64_t per = (int64_t)wvP.off[wvP.n] * w.Z * CfgGateP::NTH * CfgGateP::WTM * CfgGateP::WTN * 16;
+  return small_grid_splits((int64_t)wvP.n * ntmP * ngrpP * w.Z, kmax, CfgGateP::BK, per, w.wpart_floats,
+                           w.kn.split_max);
+}
+
+bool fwd_wave_kw(const Dims& d, const Work& w, const ParamOff& po, int diag) {
+  return !w.drop.lstm() && small_kw_ok(d, w) && fwd_wave_splits(d, w, po, diag) > 1;
+}
+
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
@@ -673,11 +690,7 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     FwdWave wvP{};
     fwd_wave(d, w, po, diag, gate_blocks(ntmP, ngrpP), false, wvP);
     const dim3 gridP(wvP.off[wvP.n], 1, w.Z);
-    int kmax = 0;
-    for (int q = 0; q < wvP.n; ++q) kmax = std::max(kmax, wvP.lo[q].cin + (wvP.t[q] > 0 ? d.H : 0));
-    const int64_t per = (int64_t)gridP.x * gridP.z * CfgGateP::NTH * CfgGateP::WTM * CfgGateP::WTN * 16;
-    const int S = small_grid_splits((int64_t)wvP.n * ntmP * ngrpP * w.Z, kmax, CfgGateP::BK, per, w.wpart_floats,
-                                    w.kn.split_max);
+    const int S = fwd_wave_splits(d, w, po, diag);
     if (S > 1 && small_kw_ok(d, w)) {
       launch_lstm_fwd_kw(s, d, w, diag, theta, tstride, po);
       return;

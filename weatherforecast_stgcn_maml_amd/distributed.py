@@ -43,14 +43,16 @@ def reduce_meta(buf: torch.Tensor, group=None):
     dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
 
 
-def capi_comm_check(ctx, n: int, iters: int = 10) -> dict:
+def capi_comm_check(ctx, n: int, iters: int = 10, init_timeout_ms: int = 60000) -> dict:
     """Drive the C ABI's own RCCL communicator (``smaml_comm_*``, include/smaml.h: the
     collective a non-torch host binds for train_hybrid_maml_v5.py:174-179's outer step) across
     the ranks of the initialised torch.distributed group, one GPU per rank: rank 0's unique id
     travels over the torch group, every rank all-reduces a length-``n`` f32 buffer holding
     rank + 1 through the C ABI, and the result must be world * (world + 1) / 2 everywhere.
     Returns {"status", "world", "elements", "allreduce_ms"} (status "ok" or the error text).
-    RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so this needs world GPUs."""
+    RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so this needs world GPUs.
+    Never hangs on a failed init: smaml_comm_init waits at most ``init_timeout_ms`` for the other
+    ranks, and the ranks agree on every rank's init status before any collective runs."""
     from . import _capi
 
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -69,7 +71,17 @@ def capi_comm_check(ctx, n: int, iters: int = 10) -> dict:
                 "world": world}
     box = [uid]
     dist.broadcast_object_list(box, src=0, device=dev)
-    ctx.comm_init(rank, world, box[0])
+    ctx.set_option("comm_timeout_ms", int(init_timeout_ms))
+    try:
+        ctx.comm_init(rank, world, box[0])
+        ok, err = 1, ""
+    except Exception as e:  # noqa: BLE001 - bounded init failed here (or timed out): agree, then report
+        ok, err = 0, str(e)
+    flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not int(flag.item()):
+        ctx.comm_destroy()
+        return {"status": f"error: smaml_comm_init failed on some rank ({err or 'other rank'})", "world": world}
     try:
         s = torch.cuda.current_stream(dev)
         buf = torch.full((n,), float(rank + 1), dtype=torch.float32, device=dev)

@@ -35,23 +35,27 @@ class _GraphMemo:
     """Remembers one edge_index tensor (by identity and autograd version counter, which every in-place
     write to it or to a view of it bumps) together with what was derived from it on the host, so a
     caller that passes the same unchanged tensor every step (train_hybrid_maml_v5.py:129-139) pays
-    no device-to-host copy or sync after the first call."""
+    no device-to-host copy or sync after the first call. Storage swaps (``t.data = other``) are noticed
+    through the data pointer; an in-place write through ``t.data`` is invisible to both checks -- pass a
+    new tensor (or write without ``.data``) when the graph changes."""
 
-    __slots__ = ("ref", "version", "value")
+    __slots__ = ("ref", "version", "ptr", "value")
 
     def __init__(self):
         self.ref = None
         self.version = -1
+        self.ptr = 0
         self.value = None
 
     def get(self, t: torch.Tensor):
-        if self.ref is not None and self.ref() is t and t._version == self.version:
+        if self.ref is not None and self.ref() is t and t._version == self.version and t.data_ptr() == self.ptr:
             return self.value
         return None
 
     def put(self, t: torch.Tensor, value):
         self.ref = weakref.ref(t)
         self.version = t._version
+        self.ptr = t.data_ptr()  # (`t.data = other` swaps the storage without a version bump)
         self.value = value
         return value
 
@@ -122,6 +126,21 @@ class GCNConv(nn.Module):
         return f"GCNConv({self.in_channels}, {self.out_channels})"
 
 
+def _conv_backward(lib_ctx, st, x, w, dz, dx, flags=0):
+    """smaml_gcn_conv_backward for any out-channel count: its GEMMs take cout in multiples of 4, so a
+    ragged cout (e.g. out_channels * forecast_horizon = 3) runs with zero-padded dz columns / W rows,
+    whose products are exact zeros (dx unchanged; the padded dW rows and db entries are dropped).
+    Returns (dW, db)."""
+    cout = w.shape[0]
+    c4 = -(-cout // 4) * 4
+    if c4 != cout:
+        dz = torch.nn.functional.pad(dz, (0, c4 - cout))
+        w = torch.nn.functional.pad(w, (0, 0, 0, c4 - cout))
+    dwb = torch.empty(w.numel() + c4, device=x.device, dtype=torch.float32)
+    lib_ctx.gcn_conv_backward(st, x, w, dz, dx=dx, dwb=dwb, flags=flags)
+    return dwb[:w.numel()].view(c4, -1)[:cout], dwb[w.numel():w.numel() + cout]
+
+
 class _GCNConvFn(torch.autograd.Function):
     """out = A_hat x W^T + b with its backward on the HIP path (smaml_gcn_conv_backward): dx = A_hat^T dz W,
     dW = dz^T (A_hat x), db = sum dz (PyG GCNConv's autograd, model.py:23-26)."""
@@ -141,9 +160,31 @@ class _GCNConvFn(torch.autograd.Function):
         dz = gout.contiguous().float()
         need_x = fctx.needs_input_grad[0]
         dx = torch.empty_like(x) if need_x else None
-        dwb = torch.empty(w.numel() + w.shape[0], device=x.device, dtype=torch.float32)
-        fctx.lib_ctx.gcn_conv_backward(_capi.stream_ptr(torch), x, w, dz, dx=dx, dwb=dwb)
-        return dx, None, dwb[:w.numel()].view_as(w), dwb[w.numel():]
+        dw, db = _conv_backward(fctx.lib_ctx, _capi.stream_ptr(torch), x, w, dz, dx)
+        return dx, None, dw, db
+
+
+def _stgcn_run(x, ctxs, dctx, p, seed, num_nodes, params):
+    """STGCN.forward (model.py:30-52) in libsmaml: conv1..conv4 each with its ReLU fused into the GCN
+    kernel's epilogue (smaml_gcn_conv_ex GCN_RELU), train-mode dropout after each (smaml_dropout,
+    counter-based masks; p = 0: none), the last time block through output_layer (smaml_gcn_conv_ex
+    GCN_PLAIN: x W^T + b, no aggregation). Returns (out [num_nodes, out*horizon], [x, h1..h4])."""
+    st = _capi.stream_ptr(torch)
+    hs = [x]
+    h = x
+    for k in range(4):
+        w, b = params[2 * k].detach().contiguous(), params[2 * k + 1].detach().contiguous()
+        out = torch.empty(h.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
+        ctxs[k].gcn_conv_ex(st, h, w, b, out, flags=_capi.GCN_RELU)
+        if p > 0.0:
+            dctx.dropout(st, out, p, seed, k)
+        hs.append(out)
+        h = out
+    wo, bo = params[8].detach().contiguous(), params[9].detach().contiguous()
+    last = h[-num_nodes:]
+    out = torch.empty(num_nodes, wo.shape[0], device=x.device, dtype=torch.float32)
+    ctxs[3].gcn_conv_ex(st, last, wo, bo, out, flags=_capi.GCN_PLAIN)
+    return out, hs
 
 
 class _STGCNFn(torch.autograd.Function):
@@ -155,24 +196,10 @@ class _STGCNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(fctx, x, convs, ctxs, dctx, p, seed, num_nodes, *params):
-        st = _capi.stream_ptr(torch)
-        hs = [x]
-        h = x
-        for k in range(4):
-            w, b = params[2 * k].detach().contiguous(), params[2 * k + 1].detach().contiguous()
-            out = torch.empty(h.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
-            ctxs[k].gcn_conv_ex(st, h, w, b, out, flags=_capi.GCN_RELU)
-            if p > 0.0:
-                dctx.dropout(st, out, p, seed, k)
-            hs.append(out)
-            h = out
-        wo, bo = params[8].detach().contiguous(), params[9].detach().contiguous()
-        last = h[-num_nodes:]
-        out = torch.empty(num_nodes, wo.shape[0], device=x.device, dtype=torch.float32)
-        ctxs[3].gcn_conv_ex(st, last, wo, bo, out, flags=_capi.GCN_PLAIN)
+        out, hs = _stgcn_run(x, ctxs, dctx, p, seed, num_nodes, params)
         fctx.save_for_backward(*hs)
         fctx.ctxs, fctx.dctx, fctx.p, fctx.seed, fctx.num_nodes = ctxs, dctx, p, seed, num_nodes
-        fctx.ws = [params[2 * k].detach().contiguous() for k in range(4)] + [wo]
+        fctx.ws = [params[2 * k].detach().contiguous() for k in range(4)] + [params[8].detach().contiguous()]
         return out
 
     @staticmethod
@@ -183,11 +210,9 @@ class _STGCNFn(torch.autograd.Function):
         grads = [None] * 10
         h4 = hs[4]
         wo = ws[4]
-        dwb = torch.empty(wo.numel() + wo.shape[0], device=h4.device, dtype=torch.float32)
         dlast = torch.empty(N, h4.shape[1], device=h4.device, dtype=torch.float32)
-        ctxs[3].gcn_conv_backward(st, h4[-N:], wo, gout.contiguous().float(), dx=dlast, dwb=dwb,
-                                  flags=_capi.GCN_PLAIN)
-        grads[8], grads[9] = dwb[:wo.numel()].view_as(wo), dwb[wo.numel():]
+        grads[8], grads[9] = _conv_backward(ctxs[3], st, h4[-N:], wo, gout.contiguous().float(), dlast,
+                                            flags=_capi.GCN_PLAIN)
         g = torch.zeros_like(h4)
         g[-N:] = dlast
         need_x = fctx.needs_input_grad[0]
@@ -195,11 +220,8 @@ class _STGCNFn(torch.autograd.Function):
             if fctx.p > 0.0:
                 fctx.dctx.dropout(st, g, fctx.p, fctx.seed, k)  # same masks: d dropout(y) = dropout(d)
             ctxs[k].relu_mask(st, g, hs[k + 1])
-            w = ws[k]
-            dwb = torch.empty(w.numel() + w.shape[0], device=h4.device, dtype=torch.float32)
             dx = torch.empty_like(hs[k]) if (k > 0 or need_x) else None
-            ctxs[k].gcn_conv_backward(st, hs[k], w, g, dx=dx, dwb=dwb)
-            grads[2 * k], grads[2 * k + 1] = dwb[:w.numel()].view_as(w), dwb[w.numel():]
+            grads[2 * k], grads[2 * k + 1] = _conv_backward(ctxs[k], st, hs[k], ws[k], g, dx)
             g = dx
         return (g if need_x else None, None, None, None, None, None, None, *grads)
 
@@ -241,26 +263,18 @@ class STGCN(nn.Module):
 
     def forward(self, x, edge_index):
         p = float(self.dropout.p) if self.training else 0.0
+        dctx, seed = None, 0
         if p > 0.0:
             from .hybrid_model import draw_dropout_seed
             seed = draw_dropout_seed()
             dctx = _any_context(x.device)
         params = self._params()
+        x = x.contiguous().float()
+        convs = (self.conv1, self.conv2, self.conv3, self.conv4)
+        ctxs = [cv.graph_context(x, edge_index) for cv in convs]
+        num_nodes = x.shape[0] // self.window_size
         if torch.is_grad_enabled() and (x.requires_grad or any(q.requires_grad for q in params)):
-            x = x.contiguous().float()
-            convs = (self.conv1, self.conv2, self.conv3, self.conv4)
-            ctxs = [cv.graph_context(x, edge_index) for cv in convs]
-            num_nodes = x.shape[0] // self.window_size
-            out = _STGCNFn.apply(x, convs, ctxs, dctx if p > 0.0 else None, p, seed if p > 0.0 else 0, num_nodes,
-                                 *params)
-            return out.view(num_nodes, self.forecast_horizon, self.out_channels).reshape(-1, self.out_channels)
-        with torch.no_grad():
-            h = x
-            for k, conv in enumerate((self.conv1, self.conv2, self.conv3, self.conv4)):
-                h = torch.relu_(conv(h, edge_index))
-                if p > 0.0:
-                    dctx.dropout(_capi.stream_ptr(torch), h, p, seed, k)
-            num_nodes = h.shape[0] // self.window_size
-            h = h[-num_nodes:]
-            out = torch.nn.functional.linear(h, self.output_layer.weight, self.output_layer.bias)
+            out = _STGCNFn.apply(x, convs, ctxs, dctx, p, seed, num_nodes, *params)
+        else:  # no_grad: the same launches, nothing saved
+            out, _ = _stgcn_run(x, ctxs, dctx, p, seed, num_nodes, params)
         return out.view(num_nodes, self.forecast_horizon, self.out_channels).reshape(-1, self.out_channels)

@@ -46,12 +46,15 @@ def pack(named, dims, which=0, device=None, out=None):
     lay, total = _layout(dims, which)
     if out is None:
         out = torch.zeros(total, dtype=torch.float32, device=device)
+    dst, src = [], []
     for name, shape, off in lay:
         v = named[name]
         if not torch.is_tensor(v):
             v = torch.from_numpy(np.ascontiguousarray(v))
         n = int(np.prod(shape))
-        out[off:off + n].copy_(v.reshape(-1).to(out.device, torch.float32))
+        dst.append(out[off:off + n])
+        src.append(v.reshape(-1).to(out.device, torch.float32))
+    torch._foreach_copy_(dst, src)  # one multi-tensor launch on a device (the module API packs per forward)
     return out
 
 
