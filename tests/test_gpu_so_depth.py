@@ -153,6 +153,42 @@ def test_second_order_cfg5_gcn_dedup_against_oracle():
     check(res, ml, ref, d, names, 1, cfg.inner_steps)
 
 
+def test_xg_dedup_against_oracle_and_off():
+    """Layer 0's input projection once per distinct stream row (option xg_dedup, kernels.h XgDedup): with
+    B consecutive windows per task, stream row s feeds window b's step s - b, so F_s . W_ih0^T (and, in the
+    second-order sweep, F_s . U_ih0^T) is formed once per row by k_xg_dedup and the big-tile gate kernels
+    run layer 0's K loop over the recurrent segment only (hybrid_model.py:93-102 restated; dataset.py:30-37
+    for the windows). Config-2 shapes, 2 tasks x B = 8 x K = 2, second order: the option on runs the tables
+    on every step (inner steps, query, every sweep step) and matches the oracle at the parity tolerances
+    and the option off (which forms the projection inside each window's K loop) to f32 rounding."""
+    d = CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=8, order=2)
+    P = synth.init_params(26, d, gcn_bias_scale=0.1)
+    theta, gcn, names = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(2600 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2)]
+    out = {}
+    for on in (1, 0):
+        ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=None)
+        ml.set_tasks(feats)
+        ml.ctx.set_option("xg_dedup", on)
+        ml.ctx.variant_counts(reset=True)
+        res = ml.meta_step()
+        vc = ml.ctx.variant_counts()
+        K = cfg.inner_steps
+        # primal tables: K inner steps + the query; tangent tables: K sweep steps (all kept: tangent only)
+        assert vc["xg_dedup"] == ((K + 1) + K if on else 0), vc
+        assert vc["fwd_kw"] == vc["fwd_split"] == 0, vc
+        out[on] = (res, ml.meta_grad.cpu().clone(), ml)
+        if on:
+            ref = oracle("xg-dedup", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
+            check(res, ml, ref, d, names, 2, K)
+    (r1, g1, _), (r0, g0, _) = out[1], out[0]
+    assert rel(r1.losses.cpu().numpy(), r0.losses.cpu().numpy()) < 1e-6
+    assert rel(r1.norms.cpu().numpy(), r0.norms.cpu().numpy()) < 1e-6
+    assert rel(g1.numpy(), g0.numpy()) < 1e-5
+
+
 # ----------------------------------------------------------------------------- (c) the benched step
 def test_bench_configuration_properties_and_determinism():
     """The bench's own meta-step: BASELINE config 2 (15 tasks x B=32 x T=24 x N=441, K=5, second

@@ -29,6 +29,7 @@ CATEGORIES = {
     "wgrad_reduce": r"k_wgrad_reduce",
     "head_dh": r"k_gemm_nn",
     "head_loss": r"k_head_(loss|dual)",
+    "xg_proj": r"k_xg_dedup|k_gemm_nt",
 }
 
 

@@ -127,7 +127,7 @@ int build_ell(const int64_t* ei, int64_t E, int N, std::vector<int32_t>& cols, s
 }
 
 // one kernel per timing category (bench roofline = one kernel's launches)
-enum Cat { C_GCN = 0, C_FWD, C_FWD_DUAL, C_HEAD, C_HEAD_DH, C_BWD, C_BWD_DUAL, C_WGRAD, C_WGRAD_RED, C_MISC, NCAT };
+enum Cat { C_GCN = 0, C_FWD, C_FWD_DUAL, C_HEAD, C_HEAD_DH, C_BWD, C_BWD_DUAL, C_WGRAD, C_WGRAD_RED, C_MISC, C_XG, NCAT };
 
 // Live per-category kernel timing with HIP events on the launch stream (bench roofline).
 struct Timer {
@@ -230,7 +230,8 @@ struct smaml_ctx {
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1};
+           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
+           SMAML_XG_DEDUP_DEFAULT};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -254,6 +255,8 @@ struct smaml_ctx {
   int64_t bimg_cap = 0;
   float* xg_buf = nullptr;    // small-grid forward: layer 0's hoisted input projection (run_lstm)
   int64_t xg_cap = 0;
+  float* xgd_buf = nullptr;   // big-tile forward: layer 0's projection per distinct stream row (prep_xg_dedup)
+  int64_t xgd_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
   // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
   unsigned* bar = nullptr;
@@ -773,11 +776,65 @@ int prep_bwd_images(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tst
   return SMAML_OK;
 }
 
-// LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront).
-int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
+// Layer 0's input projection of a step whose every task reads B consecutive windows, once per distinct
+// stream row (kernels.h XgDedup, k_xg_dedup): the XG table of theta (want_xg) and / or of the sweep's
+// tangent direction U, into w.xgd. Returns whether the tables were formed (no room, dropout, a batch of
+// one or the option off: the gate kernels form the projection in their own K loops).
+bool prep_xg_dedup(smaml_ctx* c, hipStream_t s, bool consec, const float* theta, const float* U, int64_t tstride,
+                   bool want_xg) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  w.xgd = XgDedup{};
+  if (!consec || !c->kn.xg_dedup || w.B <= 1 || w.drop.gcn() || w.drop.lstm() || (!want_xg && !U)) return false;
+  const int64_t per = xg_dedup_rows(w.B, d.T, d.N) * 4 * d.H;
+  const int64_t need = per * w.Z * ((want_xg ? 1 : 0) + (U ? 1 : 0));
+  if (need > c->xgd_cap) {
+    if (c->xgd_buf) HIP_TRY(hipFree(c->xgd_buf));
+    c->xgd_buf = nullptr;
+    c->xgd_cap = 0;
+    if (hipMalloc((void**)&c->xgd_buf, need * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    c->xgd_cap = need;
+  }
+  XgDedup xd{};
+  xd.zstride = per;
+  xd.N = d.N;
+  w.xgd = xd;  // (zstride read by the launcher)
+  const double fl = 2.0 * w.Z * xg_dedup_rows(w.B, d.T, d.N) * 4 * d.H * c->po.lay[0].cin;
+  float* dst = c->xgd_buf;
+  if (want_xg) {
+    const bool img = w.gimg.th && w.gimg_src == theta;
+    TIMED(c, s, C_XG, fl,
+          launch_xg_dedup(s, d, w, theta, tstride, c->po, img ? w.gimg.th : nullptr, w.gimg.tstride,
+                          w.gimg.off[0][0], dst));
+    xd.xg = dst;
+    xd.src = theta;
+    dst += per * w.Z;
+  }
+  if (U) {
+    const bool img = w.gimg.u && w.gimg_u_src == U;
+    TIMED(c, s, C_XG, fl,
+          launch_xg_dedup(s, d, w, U, tstride, c->po, img ? w.gimg.u : nullptr, w.gimg.tstride, w.gimg.off[0][0],
+                          dst));
+    xd.rxg = dst;
+    xd.u_src = U;
+  }
+  w.xgd = xd;
+  return true;
+}
+
+// LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront). consec: every task
+// of this step reads B consecutive windows (layer 0's projection may then run once per stream row).
+int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, bool consec = false) {
   const Dims& d = c->d;
   Work& w = c->w;
   TRY(prep_gate_images(c, s, theta, tstride));
+  // big-tile steps (the meta-step's batches): the XG table when every layer-0 diagonal runs big tiles
+  bool xgd_ok = consec;
+  for (int diag = 0; xgd_ok && diag < d.T; ++diag) xgd_ok = fwd_wave_big(d, w, c->po, diag);
+  const bool use_xgd = xgd_ok && prep_xg_dedup(c, s, true, theta, nullptr, tstride, true);
   // Batch-1 sizes (the small-grid steps): layer 0's input projection F . W_ih0^T does not depend on the
   // recurrence, so it runs for all T steps as one throughput-bound GEMM before the wavefront and the
   // layer-0 steps' latency-bound K loops cover only the recurrent segment (kernels_small.hip).
@@ -798,7 +855,7 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
         (void)hipGetLastError();  // no room: the layer-0 steps form the projection themselves
     }
     if (c->xg_buf) {
-      TIMED(c, s, C_FWD, 2.0 * w.Z * d.T * w.M * 4 * d.H * d.Hc,
+      TIMED(c, s, C_XG, 2.0 * w.Z * d.T * w.M * 4 * d.H * d.Hc,
             launch_gemm_nt(s, w.F, (int64_t)d.T * w.M * d.Hc, d.T * w.M, d.Hc, theta + c->po.lay[0].wih, tstride,
                            4 * d.H, c->xg_buf, per, w.Z));
       w.xg = c->xg_buf;
@@ -808,13 +865,14 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride) {
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
-    if (w.xg && fwd_wave_kw(d, w, c->po, diag))  // (the hoisted projection's flops are counted above)
+    if ((w.xg && fwd_wave_kw(d, w, c->po, diag)) || use_xgd)  // (the projection's flops are counted above)
       for (int q = 0; q < wv.n; ++q)
         if (wv.l[q] == 0) fl -= 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
     TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
   }
   w.xg = nullptr;
   w.xg_src = nullptr;
+  w.xgd = XgDedup{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -829,7 +887,7 @@ static void ad_cache_drop(smaml_ctx* c) {
 int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev,
                 const float* const* first_tab = nullptr) {
   TRY(run_gcn(c, s, xtab_dev, first_tab));
-  return run_lstm(c, s, theta, tstride);
+  return run_lstm(c, s, theta, tstride, first_tab != nullptr);
 }
 
 int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, float* grad);
@@ -904,12 +962,18 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   Work& w = c->w;
   if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, first_tab));
   TRY(prep_gate_images(c, s, theta, tstride, U));
+  // layer 0's tangent projection F U_ih0^T (and, unless the primal is kept, F W_ih0^T) once per stream row
+  const bool use_xgd = prep_xg_dedup(c, s, first_tab != nullptr, theta, U, tstride, !w.primal_kept);
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
     if (w.primal_kept) fl -= fwd_wave(d, w, c->po, diag, 0, false, wv);  // tangent pass only
+    if (use_xgd)  // (counted in C_XG)
+      for (int q = 0; q < wv.n; ++q)
+        if (wv.l[q] == 0) fl -= (w.primal_kept ? 1.0 : 2.0) * 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
     TIMED(c, s, C_FWD_DUAL, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
   }
+  w.xgd = XgDedup{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1120,6 +1184,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->gimg_buf) (void)hipFree(c->gimg_buf);
   if (c->bimg_buf) (void)hipFree(c->bimg_buf);
   if (c->xg_buf) (void)hipFree(c->xg_buf);
+  if (c->xgd_buf) (void)hipFree(c->xgd_buf);
   if (c->bar) (void)hipFree(c->bar);
   if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);
@@ -1681,6 +1746,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.small_kw = (int)value;
   } else if (k == "gcn_dedup" && (value == 0 || value == 1)) {
     c->kn.gcn_dedup = (int)value;
+  } else if (k == "xg_dedup" && (value == 0 || value == 1)) {
+    c->kn.xg_dedup = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
     c->ad_gcn_batch = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {

@@ -99,6 +99,7 @@ enum Variant {
   V_FWD_KW,          // k_lstm_fwd_kw (small grids: K split over the waves of one workgroup)
   V_BWD_KW,          // k_lstm_bwd_kw (same, BPTT)
   V_GCN_DEDUP,       // k_gcn_mlp once per distinct stream row of consecutive windows
+  V_XG_DEDUP,        // k_xg_dedup: layer 0's input projection once per distinct stream row (big-tile forward)
   NVAR
 };
 
@@ -130,6 +131,8 @@ struct Knobs {
   int small_kw = 0;              // small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip):
                              // 1 = on, 2 = on with pre-split BPTT weight images (launch_split_bwd), 0 = split-K pairs
   int gcn_dedup = 0;             // 1: batches of consecutive windows run the fused GCN rows once per distinct stream row
+  int xg_dedup = 0;              // 1: ... and layer 0's input projection F . W_ih0^T (and its tangent) once per
+                                 // distinct stream row (k_xg_dedup), added to the gate accumulators
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -145,6 +148,9 @@ struct Knobs {
 #endif                              // time-neutral (3-round A/B 1785.6 -> 1784.5 ms per meta-step)
 #ifndef SMAML_SMALL_KW
 #define SMAML_SMALL_KW 1
+#endif
+#ifndef SMAML_XG_DEDUP_DEFAULT
+#define SMAML_XG_DEDUP_DEFAULT 1
 #endif
 #ifndef SMAML_WGRAD_PAIR
 #define SMAML_WGRAD_PAIR 1
@@ -180,6 +186,25 @@ struct BwdImgs {
   int64_t off_hh[MAX_LAYERS] = {};  // byte offset of W_hh(l) in a task's images
   int64_t off_ih[MAX_LAYERS] = {};  // ... W_ih(l), l >= 1 (0 for l = 0: not built)
 };
+// Layer 0's input projection of a step whose every task reads B consecutive windows, formed once per
+// distinct stream row by k_xg_dedup (launch_xg_dedup): per task [(2B + T - 2) N][4H] floats -- rows
+// [0, B N) the t = 0 rows (row b N + n: their GCN features see the graph, so each window's are its own),
+// then stream rows s = 1 .. B + T - 2 (row B N + (s - 1) N + n). Window b's step t >= 1 reads stream row
+// b + t, i.e. row M + (t - 1) N + m with m = b N + n: one fixed shift per step, contiguous in m. The gate
+// kernels start layer 0's accumulators from these rows (no bias) and run their K loop over the
+// recurrent segment only.
+struct XgDedup {
+  const float* xg = nullptr;     // F . W_ih0^T of src, or null
+  const float* rxg = nullptr;    // F . U_ih0^T of u_src (second-order sweep), or null
+  const float* src = nullptr;    // the parameter vectors they were formed from (launchers check them)
+  const float* u_src = nullptr;
+  int64_t zstride = 0;           // floats per task
+  int N = 0;
+};
+__host__ __device__ inline int64_t xg_dedup_rows(int B, int T, int N) { return (int64_t)(2 * B + T - 2) * N; }
+// first row of step t's block of window rows in a task's XgDedup table (M = B N)
+__host__ __device__ inline int64_t xg_dedup_row0(int t, int M, int N) { return t == 0 ? 0 : (int64_t)M + (int64_t)(t - 1) * N; }
+
 struct Work {
   int Z = 0, B = 0, M = 0;
   BwdImgs bimg{};           // pre-split BPTT weight images (launch_split_bwd), small-grid BPTT only
@@ -187,6 +212,7 @@ struct Work {
   const float* xg = nullptr;       // small-grid forward: layer 0's input projection F . W_ih0^T for all steps
                            // [Z][T][M][4H] (run_lstm), or null: the layer-0 steps form it themselves
   const float* xg_src = nullptr;   // the parameter vector xg was formed with
+  XgDedup xgd{};                   // big-tile forward: layer 0's projection once per distinct stream row
   GateImgs gimg{};         // pre-split images of the weights the gate GEMMs read (launch_split_gate)
   const float* gimg_src = nullptr; // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src = nullptr;// ... and gimg.u (the sweep's tangent direction)
@@ -380,6 +406,11 @@ void launch_gcn_wsplit(hipStream_t s, const Dims& d, const float* gcn, const Gcn
 // time steps) and there is no GCN dropout -- see k_gcn_mlp
 void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
                     const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup = false);
+// out[z] = layer-0 input projection of every distinct stream row of task z's consecutive windows
+// (XgDedup layout) with the gate weights W_ih0 of `params` (theta or the tangent direction U); the
+// weights come from the pre-split images `img` when given (w.gimg.th / .u), else from `params`
+void launch_xg_dedup(hipStream_t s, const Dims& d, const Work& w, const float* params, int64_t tstride,
+                     const ParamOff& po, const char* img, int64_t img_tstride, int64_t img_off, float* out);
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
@@ -414,6 +445,8 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
 bool small_kw_ok(const Dims& d, const Work& w);
 // launch_lstm_fwd_wave runs diagonal `diag` as the kw kernel (the only forward form that reads w.xg)
 bool fwd_wave_kw(const Dims& d, const Work& w, const ParamOff& po, int diag);
+// ... as the big-tile k_lstm_fwd_step (the only primal form that reads w.xgd)
+bool fwd_wave_big(const Dims& d, const Work& w, const ParamOff& po, int diag);
 int64_t bwd_img_bytes(const Dims& d, BwdImgs* bi);  // per task; fills bi's offsets / tstride
 void launch_split_bwd(hipStream_t s, const Dims& d, const ParamOff& po, const float* theta, int64_t tstride, int Z,
                       const BwdImgs& bi);

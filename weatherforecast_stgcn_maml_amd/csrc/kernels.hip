@@ -290,11 +290,13 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
 }
 
 // fwd_cell through the transposed epilogue (loaders.h gate_epilogue_t): per item (row, 4 units)
-// one 16-B c_{t-1} load and six 16-B stores (i, f, g, o, c, h).
-template <int H, class CG>
+// one 16-B c_{t-1} load and six 16-B stores (i, f, g, o, c, h). XG: the pre-activations also get the
+// row's XgDedup entries (layer 0's input projection, xg = the step's block of window rows): four more
+// 16-B loads per item.
+template <int H, class CG, bool XG = false>
 __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __restrict__ th, const LayerOff& lo,
                                            float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
-                                           int m0, int ug, int t, int M, float* smem) {
+                                           int m0, int ug, int t, int M, float* smem, const float* xg = nullptr) {
   const int j = ug * 32 + (int)(threadIdx.x & 31);
   float bsum[4];
 #pragma unroll
@@ -314,10 +316,19 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
         coords(ml, u, m, jq);
         return ldo(Cz, 4u * ((tM + (uint32_t)m) * H - pM + (uint32_t)jq));  // c_{t-1} (t = 0: selected out)
       },
-      [&](int ml, int u, const float4 (&pre)[4], const float4& cpv) {
+      [&](int ml, int u, const float4 (&pre0)[4], const float4& cpv) {
         if ((!full && m0 + ml >= M) || ug * 32 + u >= H) return;
         const uint32_t row = tM + (uint32_t)(m0 + ml), jq = (uint32_t)(ug * 32 + u);
         const float4 cp = sel4(past, cpv);
+        float4 pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          pre[g] = pre0[g];
+          if (XG && xg) {
+            const float4 x = ldo(xg, 4u * ((uint32_t)(m0 + ml) * (4 * H) + (uint32_t)(g * H) + jq));
+            pre[g] = make_float4(pre[g].x + x.x, pre[g].y + x.y, pre[g].z + x.z, pre[g].w + x.w);
+          }
+        }
         float4 gi, gf, gg, go, c, hh;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -341,11 +352,14 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
       });
 }
 
+// XG (xg != null): layer 0's input projection of this step's windows comes from the XgDedup table
+// (launch_xg_dedup): the accumulators start from it and the K loop covers the recurrent segment only.
 template <int H, bool DROP, bool IMG = false>
 __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                               float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
                                               const float* __restrict__ theta, int64_t tstride, FwdWave wv, int T,
-                                              int M, const Drop& dr, float* smem, const GateImgs* gi = nullptr) {
+                                              int M, const Drop& dr, float* smem, const GateImgs* gi = nullptr,
+                                              const float* xg = nullptr, int64_t xg_zstride = 0, int xg_N = 0) {
   int l, t, b0;
   LayerOff lo;
   const Blk bk = xcd_block();
@@ -369,7 +383,12 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     return;
   const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
+  int kbeg = 0;  // (XG: the K loop starts past the input segment)
   acc.zero();
+  // (the table is added in the epilogue: loading it into the accumulators before the K loop keeps 64 more
+  // registers live through the loop's prologue and spills)
+  const float* xgt = !DROP && xg && l == 0 ? xg + (int64_t)z * xg_zstride + xg_dedup_row0(t, M, xg_N) * (4 * H) : nullptr;
+  if (xgt) kbeg = cin;
   if (DROP && l > 0) {
     // nn.LSTM inter-layer dropout: layer l reads drop(h_{l-1, t})
     const XDrop xd{drop_site(dr.seed, 2, dr.step, l - 1), dr.thr_lstm, dr.sc_lstm,
@@ -388,17 +407,20 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
           o1 = gi->off[q][1];
         }
       const SegGateImg<2> lbi{{ib + o0, ib + o1}, {cin, H}};
-      gemm_mainloop<CfgGate>(la, lbi, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+      gemm_mainloop<CfgGate>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
     } else {
       const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
-      gemm_mainloop<CfgGate>(la, lbt, m0, n0, 0, cin + (t > 0 ? H : 0), acc, smem);
+      gemm_mainloop<CfgGate>(la, lbt, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
     }
   }
 
-  if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1)
-    fwd_cell_t<H, CfgGate>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem);
-  else
+  if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1) {
+    fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
+  } else {
+    static_assert(!SMAML_XG_DEDUP_DEFAULT || (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1),
+                  "the XG table is added by the transposed epilogue");
     fwd_cell<H, SMAML_EPI_PRELOAD_FWD != 0>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M);
+  }
 }
 
 double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int blocks_per_problem, bool dual,
@@ -431,10 +453,87 @@ template <int H, bool IMG>
 __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                                       float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi) {
+                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi, XgDedup xd) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
-  lstm_fwd_step<H, false, IMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi);
+  lstm_fwd_step<H, false, IMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi, xd.xg, xd.zstride,
+                               xd.N);
 }
+
+// Layer 0's input projection of a step whose every task reads B consecutive windows, once per distinct
+// stream row (kernels.h XgDedup): out[z][r][g H + j] = F_row(r) . W_ih0[g H + j] with the gate GEMM's own
+// tile (CfgGate), column mapping, K order and weight images, so the gate kernel that starts its
+// accumulators from these rows and adds the recurrent segment computes bitwise what it computes
+// with the input segment in its own K loop. Compact row r: r < M -> F[0][r] (the t = 0 rows, window
+// b = r / N); else stream row s = (r - M) / N + 1, read from the (window, step) slot (s - t, t) with
+// t = min(s, T - 1) (the GCN wrote every slot of that stream row with the same features).
+struct XgRowsA {
+  const float* F;  // [T][M][cin] (one task)
+  int M, N, T, cin, rows;
+  FastDiv ndiv;
+  __device__ __forceinline__ float4 operator()(int r, int k) const {
+    r = min(r, rows - 1);
+    int64_t row = r;
+    if (r >= M) {
+      const int rr = r - M;
+      const int s1 = (int)ndiv.div((uint32_t)rr);
+      const int s = s1 + 1, t = min(s, T - 1);
+      row = (int64_t)t * M + (int64_t)(s - t) * N + (rr - s1 * N);
+    }
+    return ld4(F + row * cin + k);
+  }
+};
+template <int H, bool IMG>
+__global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_xg_dedup(const float* __restrict__ F, int64_t f_zstride,
+                                                                        XgRowsA a, const float* __restrict__ W,
+                                                                        int64_t w_zstride, const char* __restrict__ img,
+                                                                        int64_t img_zstride, float* __restrict__ out,
+                                                                        int64_t o_zstride) {
+  __shared__ float smem[CfgGate::SMEM_FLOATS];
+  const int z = blockIdx.z;
+  constexpr int UPB = CfgGate::WAVES_N;
+  int tm, ug;
+  if (!gate_tile((int)blockIdx.x, (a.rows + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+    return;
+  const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
+  a.F = F + (int64_t)z * f_zstride;
+  Acc<CfgGate> acc;
+  acc.zero();
+  if constexpr (IMG)
+    gemm_mainloop<CfgGate>(a, SegGateImg<1>{{img + (int64_t)z * img_zstride}, {a.cin}}, m0, n0, 0, a.cin, acc, smem);
+  else
+    gemm_mainloop<CfgGate>(a, SegGateBt<1>{{W + (int64_t)z * w_zstride}, {a.cin}, H}, m0, n0, 0, a.cin, acc, smem);
+  float* o = out + (int64_t)z * o_zstride;
+  const float zero[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool full = m0 + CfgGate::BM <= a.rows;
+  gate_epilogue_t<CfgGate>(
+      acc, zero, smem, [&](int, int) { return 0; },
+      [&](int ml, int u, const float4 (&pre)[4], int) {
+        if ((!full && m0 + ml >= a.rows) || ug * 32 + u >= H) return;
+        const uint32_t row = (uint32_t)(m0 + ml), jq = (uint32_t)(ug * 32 + u);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) sto(o, 4u * (row * (4 * H) + g * H + jq), pre[g]);
+      });
+}
+
+void launch_xg_dedup(hipStream_t s, const Dims& d, const Work& w, const float* params, int64_t tstride,
+                     const ParamOff& po, const char* img, int64_t img_tstride, int64_t img_off, float* out) {
+  const int rows = (int)xg_dedup_rows(w.B, d.T, d.N);
+  const int ntm = (rows + CfgGate::BM - 1) / CfgGate::BM;
+  const int ngrp = (d.H + 32 * CfgGate::WAVES_N - 1) / (32 * CfgGate::WAVES_N);
+  dim3 grid(gate_blocks(ntm, ngrp), 1, w.Z);
+  const int cin = po.lay[0].cin;
+  const XgRowsA a{nullptr, w.M, d.N, d.T, cin, rows, FastDiv((uint32_t)d.N)};
+  const int64_t fz = (int64_t)d.T * w.M * cin;
+  count_variant(w, V_XG_DEDUP);
+  if (img) {
+    SMAML_DISPATCH_H(d.H, (k_xg_dedup<HT, true><<<grid, CfgGate::NTH, 0, s>>>(
+                              w.F, fz, a, nullptr, 0, img + img_off, img_tstride, out, w.xgd.zstride)));
+  } else {
+    SMAML_DISPATCH_H(d.H, (k_xg_dedup<HT, false><<<grid, CfgGate::NTH, 0, s>>>(
+                              w.F, fz, a, params + po.lay[0].wih, tstride, nullptr, 0, out, w.xgd.zstride)));
+  }
+}
+
 template <int H>
 __global__ __attribute__((amdgpu_waves_per_eu(3))) __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step_drop(
     const float* __restrict__ F, float* __restrict__ HsAll, float* __restrict__ CsAll, float* __restrict__ GsAll,
@@ -667,6 +766,10 @@ bool fwd_wave_kw(const Dims& d, const Work& w, const ParamOff& po, int diag) {
   return !w.drop.lstm() && small_kw_ok(d, w) && fwd_wave_splits(d, w, po, diag) > 1;
 }
 
+bool fwd_wave_big(const Dims& d, const Work& w, const ParamOff& po, int diag) {
+  return !w.drop.lstm() && fwd_wave_splits(d, w, po, diag) <= 1;
+}
+
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
                           int64_t tstride, const ParamOff& po, double* flops) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
@@ -712,13 +815,15 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
     }
   }
   count_variant(w, V_FWD);
+  XgDedup xd = w.xgd;
+  if (xd.src != theta) xd.xg = nullptr;  // (a table of other weights is never read)
   if (w.gimg.th && w.gimg_src == theta) {
     count_variant(w, V_FWD_IMG);
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, true><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg)));
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd)));
   } else {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, false><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg)));
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd)));
   }
 }
 

@@ -166,6 +166,9 @@ __device__ __forceinline__ void fwd_dual_tangent_epi_t(const Acc<CfgGateD>& at, 
 }
 
 // IMG: the weight tiles of theta and U come from their pre-split images (launch_split_gate).
+// xd.xg / xd.rxg (layer 0, set by the launcher only for this step's theta / U): layer 0's input
+// projections F W_ih0^T and F U_ih0^T of the step's consecutive windows (kernels.h XgDedup) start the
+// primal / tangent accumulators, whose K loops then skip the input segment (R x = 0 at layer 0).
 template <int H, bool KEPT, bool DROP, bool IMG>
 __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dual(const float* __restrict__ F,
                                                       float* __restrict__ HsAll, float* __restrict__ CsAll,
@@ -173,7 +176,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
                                                       float* __restrict__ RCsAll, float* __restrict__ RGsAll,
                                                       int64_t lsz, const float* __restrict__ theta,
                                                       const float* __restrict__ U, int64_t tstride, FwdWave wv,
-                                                      int T, int M, Drop dr, GateImgs gi) {
+                                                      int T, int M, Drop dr, GateImgs gi, XgDedup xd) {
   __shared__ float smem[CfgGateD::SMEM_FLOATS];
   constexpr int G4 = 4 * H;
   int l, t, b0;
@@ -220,10 +223,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   if (!gate_tile(bk.x - b0, (M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
     return;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
-  XDrop xd{};
+  XDrop xdr{};
   if (DROP && l > 0)
-    xd = XDrop{drop_site(dr.seed, 2, dr.step, l - 1), dr.thr_lstm, dr.sc_lstm,
-               ((uint64_t)dr.task_id[z] * T + t) * M * H, H};
+    xdr = XDrop{drop_site(dr.seed, 2, dr.step, l - 1), dr.thr_lstm, dr.sc_lstm,
+                ((uint64_t)dr.task_id[z] * T + t) * M * H, H};
 
   // Register diet: the primal epilogue runs between the two passes (its accumulators die
   // there), and the tangent epilogue re-reads the gates / cell it needs from the lines this
@@ -233,19 +236,27 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   const int rb = m0 + acc_row<CfgGateD>(0, 0);
   const bool full = m0 + CfgGateD::BM <= M;
   const uint32_t tM = (uint32_t)t * (uint32_t)M;
+  const bool xg0 = !DROP && l == 0;  // (the XgDedup tables hold layer 0's rows; no dropout variant reads them)
+  const int64_t xgo = (int64_t)z * xd.zstride + xg_dedup_row0(t, M, xd.N) * G4;
   if (!KEPT) {
     Acc<CfgGateD> ap;
-    ap.zero();
+    int kb = 0;
+    if (xg0 && xd.xg) {
+      acc_load_gates<CfgGateD, H>(ap, xd.xg + xgo, m0, ug, M);
+      kb = cin;
+    } else {
+      ap.zero();
+    }
     SegKC la{{xt, hp, nullptr, nullptr}, {cin, wh, 0, 0}, M};
     SegGateB lb{{th + lo.wih, th + lo.whh, nullptr, nullptr}, {cin, wh, 0, 0}, H};
     if (DROP && l > 0)
-      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh, ap, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xdr}, lb, m0, n0, 0, cin + wh, ap, smem);
     else if constexpr (IMG)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M}, SegGateImg<2>{{ith + io0, ith + io1}, {cin, wh}},
-                                          m0, n0, 0, cin + wh, ap, smem);
+                                          m0, n0, kb, cin + wh, ap, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
-                                          SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, 0,
+                                          SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, kb,
                                           cin + wh, ap, smem);
     if (j < H) {
       float bp[4];
@@ -274,22 +285,28 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     }
   }
   Acc<CfgGateD> at;
-  at.zero();
+  int kb = 0;
+  if (xg0 && xd.rxg) {
+    acc_load_gates<CfgGateD, H>(at, xd.rxg + xgo, m0, ug, M);
+    kb = cin;
+  } else {
+    at.zero();
+  }
   {
     const int wrx = rxt ? cin : 0;
     SegKC la{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M};
     SegGateB lb{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh}, {cin, wh, wrx, wh}, H};
     if (DROP && l > 0)
-      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xd}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xdr}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else if constexpr (IMG)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
                                           SegGateImg<4>{{iu + io0, iu + io1, ith + io0, ith + io1}, {cin, wh, wrx, wh}},
-                                          m0, n0, 0, cin + wh + wrx + wh, at, smem);
+                                          m0, n0, kb, cin + wh + wrx + wh, at, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
                                           SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},
                                                        {cin, wh, wrx, wh}, H},
-                                          m0, n0, 0, cin + wh + wrx + wh, at, smem);
+                                          m0, n0, kb, cin + wh + wrx + wh, at, smem);
   }
   if constexpr (KEPT && SMAML_FWD_EPI_T && CfgGateD::WAVES_N == 1) {
     // (KEPT: the primal gates come from memory; the non-kept path re-reads the gates this lane itself
@@ -324,15 +341,18 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   count_variant(w, kept ? V_FWDD_KEPT : V_FWDD);
   const bool img = !drop && w.gimg.th && w.gimg.u && w.gimg_src == theta && w.gimg_u_src == U;
   if (img) count_variant(w, V_FWDD_IMG);
+  XgDedup xd = w.xgd;  // (tables of other weights are never read)
+  if (xd.src != theta || kept) xd.xg = nullptr;
+  if (xd.u_src != U) xd.rxg = nullptr;
 #define SMAML_FWD_DUAL(K_, D_)                                                                  \
   if (img)                                                                                      \
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_dual<HT, K_, D_, !(D_)><<<grid, CfgGateD::NTH, 0, s>>>(    \
                               w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
-                              d.T, w.M, w.drop, w.gimg)))                                       \
+                              d.T, w.M, w.drop, w.gimg, xd)))                                   \
   else                                                                                          \
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_dual<HT, K_, D_, false><<<grid, CfgGateD::NTH, 0, s>>>(    \
                               w.F, w.Hs, w.Cs, w.Gs, w.RHs, w.RCs, w.RGs, lsz, theta, U, tstride, wv, \
-                              d.T, w.M, w.drop, w.gimg)))
+                              d.T, w.M, w.drop, w.gimg, xd)))
   if (kept && drop) {
     SMAML_FWD_DUAL(true, true);
   } else if (kept) {

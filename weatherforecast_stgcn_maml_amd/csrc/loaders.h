@@ -666,6 +666,24 @@ __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (
 }
 
 
+// Gate accumulators of one gate tile (wave = 32 rows x 4 gates x 32 units, the layout fwd_cell reads)
+// loaded from rows of a [.][4H] pre-activation table x (XgDedup: layer 0's input projection), instead
+// of zeroed: the K loop then adds the recurrent segment on top. Rows past M load row M - 1 (never
+// stored); units past H read unit H - 1 (never stored).
+template <class C, int H>
+__device__ __forceinline__ void acc_load_gates(Acc<C>& acc, const float* __restrict__ x, int m0, int ug, int M) {
+  static_assert(C::WTM == 1 && C::WTN == 4, "wave = one 32-row tile of the 4 gates");
+  constexpr int UPB = C::WAVES_N;
+  const int j = min((ug * UPB + (int)(threadIdx.x >> 6) % UPB) * 32 + (int)(threadIdx.x & 31), H - 1);
+  const int rb = m0 + acc_row<C>(0, 0);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint32_t m = (uint32_t)min(rb + racc(r), M - 1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc.v[0][g][r] = ldb(x, 4u * (m * (4 * H) + (uint32_t)(g * H + j)));
+  }
+}
+
 // LSTM kernels are instantiated per hidden size (compile-time strides).
 #define SMAML_DISPATCH_H(HV, ...)                              \
   switch (HV) {                                                \
