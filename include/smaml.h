@@ -268,14 +268,15 @@ int smaml_timing(smaml_ctx* ctx, int32_t enable);
  * 1 lstm_fwd_step, 2 lstm_fwd_dual, 3 head_loss, 4 head_dh, 5 lstm_bwd_step, 6 lstm_bwd_dual,
  * 7 wgrad (split-K GEMM), 8 wgrad_reduce, 9 misc, 10 xg_proj (layer 0's input projection formed before
  * the wavefront: k_xg_dedup once per distinct stream row of consecutive windows, or the batch-1
- * k_gemm_nt). */
+ * k_gemm_nt), 11 dg_rowsum (k_dg_rowsum: layer 0's dG summed per distinct stream row before its
+ * input-weight gradient). */
 int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* count, int32_t cap);
 
 /* Launch counts per kernel variant (tile configuration) since the last reset, in the order of
  * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
  * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
  * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw, gcn_dedup,
- * xg_dedup.
+ * xg_dedup, wgrad_dedup.
  * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
  * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
@@ -325,7 +326,12 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "xg_dedup":                    the same steps form layer 0's input projection F . W_ih0^T (and, in the
  *                                  second-order sweep, F . U_ih0^T) once per distinct stream row
  *                                  (k_xg_dedup) and the big-tile gate kernels start layer 0's
- *                                  accumulators from it (1, the default; bitwise equal to 0). */
+ *                                  accumulators from it (1, the default; the forward adds it in the
+ *                                  epilogue: equal to 0 up to f32 rounding, the tangent bitwise);
+ *   "wgrad_dedup":                 the same steps form layer 0's input-weight gradient (and its tangent)
+ *                                  over the distinct stream rows: dG0 summed per stream row
+ *                                  (k_dg_rowsum) times the gathered F rows, (2B + T - 2) N rows
+ *                                  instead of T B N (1, the default; equal to 0 up to summation order). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -154,13 +154,15 @@ def test_second_order_cfg5_gcn_dedup_against_oracle():
 
 
 def test_xg_dedup_against_oracle_and_off():
-    """Layer 0's input projection once per distinct stream row (option xg_dedup, kernels.h XgDedup): with
-    B consecutive windows per task, stream row s feeds window b's step s - b, so F_s . W_ih0^T (and, in the
-    second-order sweep, F_s . U_ih0^T) is formed once per row by k_xg_dedup and the big-tile gate kernels
-    run layer 0's K loop over the recurrent segment only (hybrid_model.py:93-102 restated; dataset.py:30-37
-    for the windows). Config-2 shapes, 2 tasks x B = 8 x K = 2, second order: the option on runs the tables
-    on every step (inner steps, query, every sweep step) and matches the oracle at the parity tolerances
-    and the option off (which forms the projection inside each window's K loop) to f32 rounding."""
+    """Layer 0's input projection and input-weight gradient over the distinct stream rows (options
+    xg_dedup, wgrad_dedup; kernels.h XgDedup): with B consecutive windows per task, stream row s feeds
+    window b's step s - b, so F_s . W_ih0^T (and, in the second-order sweep, F_s . U_ih0^T) is formed once
+    per row by k_xg_dedup and the big-tile gate kernels run layer 0's K loop over the recurrent segment
+    only; dW_ih0 = sum_s (sum_b dG0(b, s - b))^T F_s (k_dg_rowsum + a gathered k_wgrad) and likewise its
+    tangent (hybrid_model.py:93-102 restated, train_hybrid_maml_v5.py:134; dataset.py:30-37 for the
+    windows). Config-2 shapes, 2 tasks x B = 8 x K = 2, second order: with the options on every step runs
+    them (inner steps, query, every sweep step) and matches the oracle at the parity tolerances and the
+    options off (every window's rows in the K loops) to f32 rounding."""
     d = CONFIG2
     cfg = MamlConfig(inner_steps=2, batch=8, order=2)
     P = synth.init_params(26, d, gcn_bias_scale=0.1)
@@ -172,12 +174,14 @@ def test_xg_dedup_against_oracle_and_off():
         ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=None)
         ml.set_tasks(feats)
         ml.ctx.set_option("xg_dedup", on)
+        ml.ctx.set_option("wgrad_dedup", on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()
         vc = ml.ctx.variant_counts()
         K = cfg.inner_steps
-        # primal tables: K inner steps + the query; tangent tables: K sweep steps (all kept: tangent only)
+        # primal: K inner steps + the query (forward and backward); tangent: K sweep steps (all kept)
         assert vc["xg_dedup"] == ((K + 1) + K if on else 0), vc
+        assert vc["wgrad_dedup"] == ((K + 1) + K if on else 0), vc
         assert vc["fwd_kw"] == vc["fwd_split"] == 0, vc
         out[on] = (res, ml.meta_grad.cpu().clone(), ml)
         if on:

@@ -30,6 +30,7 @@ CATEGORIES = {
     "head_dh": r"k_gemm_nn",
     "head_loss": r"k_head_(loss|dual)",
     "xg_proj": r"k_xg_dedup|k_gemm_nt",
+    "dg_rowsum": r"k_dg_rowsum",
 }
 
 

@@ -127,7 +127,8 @@ int build_ell(const int64_t* ei, int64_t E, int N, std::vector<int32_t>& cols, s
 }
 
 // one kernel per timing category (bench roofline = one kernel's launches)
-enum Cat { C_GCN = 0, C_FWD, C_FWD_DUAL, C_HEAD, C_HEAD_DH, C_BWD, C_BWD_DUAL, C_WGRAD, C_WGRAD_RED, C_MISC, C_XG, NCAT };
+enum Cat { C_GCN = 0, C_FWD, C_FWD_DUAL, C_HEAD, C_HEAD_DH, C_BWD, C_BWD_DUAL, C_WGRAD, C_WGRAD_RED, C_MISC, C_XG, C_DGSUM,
+           NCAT };
 
 // Live per-category kernel timing with HIP events on the launch stream (bench roofline).
 struct Timer {
@@ -231,7 +232,7 @@ struct smaml_ctx {
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
-           SMAML_XG_DEDUP_DEFAULT};
+           SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -636,6 +637,52 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
   return true;
 }
 
+// The XgDedup-row-order scratch (k_xg_dedup tables / k_dg_rowsum sums) with room for `floats`, or null.
+float* xgd_scratch(smaml_ctx* c, int64_t floats) {
+  if (floats > c->xgd_cap) {
+    if (c->xgd_buf) (void)hipFree(c->xgd_buf);
+    c->xgd_buf = nullptr;
+    c->xgd_cap = 0;
+    if (hipMalloc((void**)&c->xgd_buf, floats * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    c->xgd_cap = floats;
+  }
+  return c->xgd_buf;
+}
+
+// Whether this step's layer-0 input-weight gradient runs over distinct stream rows (wgrad_dedup).
+bool wgrad_dedup_ok(const smaml_ctx* c) {
+  const Work& w = c->w;
+  return w.consec && c->kn.wgrad_dedup && w.B > 1 && !w.drop.gcn() && !w.drop.lstm();
+}
+
+// dW_ih0 (or its tangent) = S^T F_rows over the distinct stream rows of the step's consecutive windows:
+// S = row sums of dGl (layer 0's dG or R(dG), k_dg_rowsum, in the scratch), then ONE gathered split-K
+// GEMM into grad's W_ih0 block (no bias; written, not accumulated). False: no scratch (the caller runs
+// the full-row form).
+bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float* grad) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  const int64_t rows = xg_dedup_rows(w.B, d.T, d.N), TM = (int64_t)d.T * w.M;
+  float* S = xgd_scratch(c, rows * 4 * d.H * w.Z);
+  if (!S) return false;
+  const LayerOff& lo = c->po.lay[0];
+  TIMED(c, s, C_DGSUM, 0, launch_dg_rowsum(s, d, w, dGl, TM * 4 * d.H, S));
+  WgradPlan p;
+  plan_wgrad(w, S, rows * 4 * d.H, 4 * d.H, w.F, TM * lo.cin, lo.cin, nullptr, 0, 0, rows, 0, grad, c->po.P, lo.wih, -1,
+             -1, -1, false, false, p);
+  p.ws = false;
+  p.gather = WgGather{w.M, d.N, d.T, FastDiv((uint32_t)d.N)};
+  count_variant(w, V_WGRAD);
+  count_variant(w, V_WGRAD_DEDUP);
+  if (p.wide) count_variant(w, V_WGRAD_WIDE);
+  TIMED(c, s, C_WGRAD, 2.0 * w.Z * rows * 4 * d.H * lo.cin, launch_wgrad_gemm(s, p));
+  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+  return true;
+}
+
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
 // rows t >= 1 (no neighbours, F3) run all four convs in one launch (k_gcn_mlp, activations kept in
 // registers), the t = 0 rows (ELL gather) four per-layer launches over N-row blocks.
@@ -887,6 +934,7 @@ static void ad_cache_drop(smaml_ctx* c) {
 int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev,
                 const float* const* first_tab = nullptr) {
   TRY(run_gcn(c, s, xtab_dev, first_tab));
+  c->w.consec = first_tab != nullptr;  // (read by the backward of these activations)
   return run_lstm(c, s, theta, tstride, first_tab != nullptr);
 }
 
@@ -946,6 +994,12 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       gfl += 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H);
       continue;
     }
+    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, w.dG, grad)) {
+      // W_hh0 and the bias over every row (h_{t-1} differs per window): [0 | h_{t-1}], no input columns
+      timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * d.H, w.dG, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.Hs, TM * d.H,
+                  d.H, TM, w.M, grad, po.P, -1, lo.whh, lo.bih, lo.bhh, true, false, -1);
+      continue;
+    }
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
                        w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
                        lo.bhh, true, false, l - 1);
@@ -961,6 +1015,7 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   const Dims& d = c->d;
   Work& w = c->w;
   if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, first_tab));
+  w.consec = first_tab != nullptr;
   TRY(prep_gate_images(c, s, theta, tstride, U));
   // layer 0's tangent projection F U_ih0^T (and, unless the primal is kept, F W_ih0^T) once per stream row
   const bool use_xgd = prep_xg_dedup(c, s, first_tab != nullptr, theta, U, tstride, !w.primal_kept);
@@ -1004,6 +1059,20 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
     const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
+    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, RdGl, HU)) {
+      // R(dW_ih0) = R(dG0)^T F (R x = 0 at layer 0) over distinct stream rows above; R(dW_hh0) =
+      // R(dG0)^T h + dG0^T R h and R(db) as one paired launch over every row
+      const double flp = 2.0 * 2.0 * w.Z * TM * 4 * d.H * d.H;
+      if (!(c->kn.wgrad_pair && timed_wgrad_pair(c, s, flp, RdGl, dGl, TM * 4 * d.H, 4 * d.H, nullptr, nullptr, 0, 0,
+                                                 w.Hs, w.RHs, TM * d.H, d.H, TM, w.M, HU, po.P, -1, lo.whh, lo.bih,
+                                                 lo.bhh, -1))) {
+        timed_wgrad(c, s, flp / 2, RdGl, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.Hs, TM * d.H, d.H, TM, w.M, HU, po.P,
+                    -1, lo.whh, lo.bih, lo.bhh, true, false, -1);
+        timed_wgrad(c, s, flp / 2, dGl, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.RHs, TM * d.H, d.H, TM, w.M, HU, po.P,
+                    -1, lo.whh, lo.bih, lo.bhh, false, true, -1);
+      }
+      continue;
+    }
     if (l > 0 && c->kn.wgrad_pair &&  // both passes 4H x (cin + H): one launch
         timed_wgrad_pair(c, s, 2.0 * 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, dGl, TM * 4 * d.H, 4 * d.H, X,
                          RX, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, w.RHs + (int64_t)l * lsz, TM * d.H, d.H,
@@ -1748,6 +1817,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.gcn_dedup = (int)value;
   } else if (k == "xg_dedup" && (value == 0 || value == 1)) {
     c->kn.xg_dedup = (int)value;
+  } else if (k == "wgrad_dedup" && (value == 0 || value == 1)) {
+    c->kn.wgrad_dedup = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
     c->ad_gcn_batch = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {

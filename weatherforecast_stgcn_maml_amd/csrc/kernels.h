@@ -100,6 +100,7 @@ enum Variant {
   V_BWD_KW,          // k_lstm_bwd_kw (same, BPTT)
   V_GCN_DEDUP,       // k_gcn_mlp once per distinct stream row of consecutive windows
   V_XG_DEDUP,        // k_xg_dedup: layer 0's input projection once per distinct stream row (big-tile forward)
+  V_WGRAD_DEDUP,     // layer 0's input-weight gradient over distinct stream rows (k_dg_rowsum + gathered k_wgrad)
   NVAR
 };
 
@@ -133,6 +134,8 @@ struct Knobs {
   int gcn_dedup = 0;             // 1: batches of consecutive windows run the fused GCN rows once per distinct stream row
   int xg_dedup = 0;              // 1: ... and layer 0's input projection F . W_ih0^T (and its tangent) once per
                                  // distinct stream row (k_xg_dedup), added to the gate accumulators
+  int wgrad_dedup = 0;           // 1: ... and layer 0's input-weight gradient (and its tangent) over the distinct
+                                 // stream rows: row sums of dG0 (k_dg_rowsum) times the gathered F rows
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -151,6 +154,9 @@ struct Knobs {
 #endif
 #ifndef SMAML_XG_DEDUP_DEFAULT
 #define SMAML_XG_DEDUP_DEFAULT 1
+#endif
+#ifndef SMAML_WGRAD_DEDUP_DEFAULT
+#define SMAML_WGRAD_DEDUP_DEFAULT 1
 #endif
 #ifndef SMAML_WGRAD_PAIR
 #define SMAML_WGRAD_PAIR 1
@@ -213,6 +219,7 @@ struct Work {
                            // [Z][T][M][4H] (run_lstm), or null: the layer-0 steps form it themselves
   const float* xg_src = nullptr;   // the parameter vector xg was formed with
   XgDedup xgd{};                   // big-tile forward: layer 0's projection once per distinct stream row
+  int consec = 0;                  // this step's tasks each read B consecutive windows (set by the forward)
   GateImgs gimg{};         // pre-split images of the weights the gate GEMMs read (launch_split_gate)
   const float* gimg_src = nullptr; // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src = nullptr;// ... and gimg.u (the sweep's tangent direction)
@@ -459,6 +466,11 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
                   int64_t b2_zstride, int c2, int64_t K, int Mshift, float* grad, int64_t P,
                   int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2, bool with_bias = true,
                   bool accumulate = false);
+// B-row gather of layer 0's input-weight gradient over distinct stream rows (WgBGather): M > 0 = on
+struct WgGather {
+  int M = 0, N = 0, T = 0;
+  FastDiv ndiv{};
+};
 // launch_wgrad split in its two launches (the GEMM into split-K partial slabs, then the
 // fixed-order reduce into the flat gradient), so each can be timed on its own.
 struct WgradPlan {
@@ -485,6 +497,7 @@ struct WgradPlan {
   const float* A2 = nullptr;
   const float *B1s = nullptr, *B2s = nullptr;
   int nsplit1 = 0;
+  WgGather gather{};  // M > 0: B1 rows through XgDedup's compact-row -> F-row map (no B2, no dropout)
 };
 // Turn a planned weight gradient into a pair with a second problem of the same shape (each problem
 // gets about half of the planned slices; one launch, one reduce, no accumulate pass). Returns false
@@ -503,6 +516,9 @@ struct WgMulti {
 };
 void launch_wgrad_multi(hipStream_t s, const Work& w, WgradPlan* ps, int n, int target_wgs);
 void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
+// S[z] = row sums of layer 0's dG slab (dG0 = [T][M][4H] per task, a_zstride floats apart) over the
+// (window, step) slots of each distinct stream row, in XgDedup's row order ([(2B + T - 2) N][4H] per task)
+void launch_dg_rowsum(hipStream_t s, const Dims& d, const Work& w, const float* dG0, int64_t a_zstride, float* S);
 bool wgrad_ws_ok(int Mrows, int c1, int c2);  // shapes the warp-specialised weight gradient takes
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
 // clip_grad_norm_ + SGD of every task as one grid-barrier kernel (k_inner_sgd), or its two phases as

@@ -1845,11 +1845,31 @@ struct WgPair {
   const float *B1s, *B2s;
   int nsplit1;
 };
-template <class C, bool DROP>
+// Layer 0's input-weight gradient over the distinct stream rows of consecutive windows (kernels.h
+// XgDedup row order): B row k = the F row of compact row k (XgRowsA's mapping), A = the row sums of dG0
+// (launch_dg_rowsum).
+struct WgBGather {
+  WgB b;
+  int M, N, T;
+  FastDiv ndiv;
+  __device__ __forceinline__ float4 operator()(int64_t k, int j) const {
+    if (k >= b.K || j >= b.c1) return f4zero();
+    int64_t row = k;
+    if (k >= M) {
+      const int rr = (int)(k - M);
+      const int s1 = (int)ndiv.div((uint32_t)rr);
+      const int s = s1 + 1, t = min(s, T - 1);
+      row = (int64_t)t * M + (int64_t)(s - t) * N + (rr - s1 * N);
+    }
+    return ld4(b.B1 + row * b.c1 + j);
+  }
+};
+template <class C, bool DROP, bool GATHER = false>
 __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
                                             int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn, int ntile,
                                             int nsplit, int ngroups, float* __restrict__ part, int ldp, int with_bias,
-                                            const Drop& dr, int drop_layer, float* smem, const WgPair& pr) {
+                                            const Drop& dr, int drop_layer, float* smem, const WgPair& pr,
+                                            const WgGather& ga = WgGather{}) {
   // XCD-aware: the ntile output tiles of one (split, task) group stream the same K rows of
   // A and B, so they are placed on one XCD (blocks 8 apart) to share its L2. Speed only.
   const int j = L >> 3;
@@ -1876,7 +1896,15 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
   ColSumHook<C> hook;
   // k indices exceed int range only in the loaders (int64 there); the mainloop
   // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
-  if (DROP) {
+  if constexpr (GATHER) {
+    const WgBGather bg{b, ga.M, ga.N, ga.T, ga.ndiv};
+    if (tn == 0 && with_bias) {
+      wgrad_mainloop<C>(la, bg, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
+    } else {
+      NoHook nh;
+      wgrad_mainloop<C>(la, bg, m0, n0, (int)kbeg, (int)kend, acc, smem, nh);
+    }
+  } else if (DROP) {
     const WgBDrop bd{b, XDrop{drop_site(dr.seed, 2, dr.step, drop_layer), dr.thr_lstm, dr.sc_lstm,
                               (uint64_t)dr.task_id[z] * (uint64_t)lb.K * lb.c1, lb.c1}};
     if (tn == 0 && with_bias) {
@@ -1922,14 +1950,58 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
   if (tn == 0) hook.store(P, m0, Mrows, ldp, ncols, with_bias != 0, smem);
 }
 
-template <class C, bool DROP>
+template <class C, bool DROP, bool GATHER = false>
 __global__ __launch_bounds__(C::NTH) void k_wgrad(const float* __restrict__ A, int64_t a_zstride, int Mrows,
                                               WgB lb, int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk,
                                               int ntn, int ntile, int nsplit, int ngroups, float* __restrict__ part,
-                                              int ldp, int with_bias, Drop dr, int drop_layer, WgPair pr) {
+                                              int ldp, int with_bias, Drop dr, int drop_layer, WgPair pr,
+                                              WgGather ga) {
   __shared__ float smem[wgrad_smem_floats<C>()];
-  wgrad_block<C, DROP>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile, nsplit,
-                    ngroups, part, ldp, with_bias, dr, drop_layer, smem, pr);
+  wgrad_block<C, DROP, GATHER>((int)blockIdx.x, A, a_zstride, Mrows, lb, b1_zstride, b2_zstride, kchunk, ntn, ntile,
+                               nsplit, ngroups, part, ldp, with_bias, dr, drop_layer, smem, pr, ga);
+}
+
+// Row sums of layer 0's dG over the (window, step) slots of each distinct stream row of consecutive
+// windows, in the XgDedup row order (kernels.h): row r < M is slot (t = 0, m = r) itself; stream row s
+// (r = M + (s - 1) N + n) sums slots (t = s - b, m = b N + n) for b = max(0, s - T + 1) .. min(B - 1, s - 1)
+// in ascending b. Then dW_ih0 = S^T F_rows over (2B + T - 2) N rows instead of T B N (F2: the GCN
+// features of a stream row are the same in every window). One thread per (row, 4 gate columns).
+__global__ __launch_bounds__(NT) void k_dg_rowsum(const float* __restrict__ dG, int64_t a_zstride, int M, int N, int B,
+                                                  int T, int G4, int rows, FastDiv ndiv, float* __restrict__ S,
+                                                  int64_t s_zstride) {
+  const int z = blockIdx.y;
+  const int q4 = G4 / 4;
+  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (e >= (int64_t)rows * q4) return;
+  const int r = (int)(e / q4), c = 4 * (int)(e - (int64_t)r * q4);
+  const float* g = dG + (int64_t)z * a_zstride + c;
+  float4 v;
+  if (r < M) {
+    v = ld4(g + (int64_t)r * G4);
+  } else {
+    const int rr = r - M;
+    const int s1 = (int)ndiv.div((uint32_t)rr);
+    const int s = s1 + 1, n = rr - s1 * N;
+    const int b0 = max(0, s - (T - 1)), b1 = min(B - 1, s - 1);
+    v = f4zero();
+    for (int b = b0; b <= b1; ++b) {
+      const float4 x = ld4(g + ((int64_t)(s - b) * M + (int64_t)b * N + n) * G4);
+      v.x += x.x;
+      v.y += x.y;
+      v.z += x.z;
+      v.w += x.w;
+    }
+  }
+  st4(S + (int64_t)z * s_zstride + (int64_t)r * G4 + c, v);
+}
+
+void launch_dg_rowsum(hipStream_t s, const Dims& d, const Work& w, const float* dG0, int64_t a_zstride, float* S) {
+  const int rows = (int)xg_dedup_rows(w.B, d.T, d.N);
+  const int G4 = 4 * d.H;
+  const int64_t n = (int64_t)rows * (G4 / 4);
+  dim3 grid((unsigned)((n + NT - 1) / NT), w.Z);
+  k_dg_rowsum<<<grid, NT, 0, s>>>(dG0, a_zstride, w.M, d.N, w.B, d.T, G4, rows, FastDiv((uint32_t)d.N), S,
+                                  (int64_t)rows * G4);
 }
 
 // ---- warp-specialised weight gradients (round 4) ---------------------------------------------
@@ -2198,7 +2270,7 @@ __device__ __forceinline__ void wgrad_reduce_elem(const float* __restrict__ part
   } else if (j < c1 + c2) {
     dst = g + off_w2 + (int64_t)i * c2 + (j - c1);
   } else {
-    if (accumulate) return;  // bias written by the first (bias-carrying) pass
+    if (accumulate || off_b1 < 0) return;  // bias written by the first (bias-carrying) pass / no bias here
     g[off_b1 + i] = v;
     if (off_b2 >= 0) g[off_b2 + i] = v;
     return;
@@ -2316,8 +2388,21 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
 #define SMAML_WGRAD_LAUNCH(CFG, D_)                                                                            \
   k_wgrad<CFG, D_><<<grid, CFG::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, \
                                              p.ntn, ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0, \
-                                             p.drop, D_ ? p.drop_layer : -1, WgPair{p.A2, p.B1s, p.B2s, p.nsplit1})
-  if (p.ws) {
+                                             p.drop, D_ ? p.drop_layer : -1, WgPair{p.A2, p.B1s, p.B2s, p.nsplit1}, \
+                                             WgGather{})
+  if (p.gather.M > 0) {  // (dropout-free by construction: plan_wgrad_gather)
+    const WgPair np{nullptr, nullptr, nullptr, 0};
+    if (p.wide)
+      k_wgrad<CfgTW, false, true><<<grid, CfgTW::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride,
+                                                              p.b2_zstride, p.kchunk, p.ntn, ntile, p.nsplit, ngroups,
+                                                              p.part, p.ldp, p.with_bias ? 1 : 0, p.drop, -1, np,
+                                                              p.gather);
+    else
+      k_wgrad<CfgTN, false, true><<<grid, CfgTN::NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride,
+                                                              p.b2_zstride, p.kchunk, p.ntn, ntile, p.nsplit, ngroups,
+                                                              p.part, p.ldp, p.with_bias ? 1 : 0, p.drop, -1, np,
+                                                              p.gather);
+  } else if (p.ws) {
     k_wgrad_ws<<<grid, WS_NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn,
                                        ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
                                        WgPair{p.A2, p.B1s, p.B2s, p.nsplit1});
