@@ -494,12 +494,14 @@ def test_stgcn_autograd_matches_oracle(d, p):
     assert rel(xg.grad.cpu(), xt.grad) < 1e-4
 
 
-@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers"])
+@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
     stored to every sample holding them; gcn_dedup_layers: the same on the per-layer GCN path,
-    gcn_fused 0, as one pseudo-sample of distinct stream rows per task expanded into F) leave every
+    gcn_fused 0, as one pseudo-sample of distinct stream rows per task expanded into F; bptt_streams /
+    fwd_streams: every BPTT / forward diagonal in two row chunks on side streams, always on the big tiles,
+    the weight gradients after the sweep) leave every
     row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
     kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
@@ -517,7 +519,11 @@ def test_order_only_knobs_bitwise(knob):
         ml.ctx.set_option("bwdd_big_min", 0)
         if knob == "gcn_dedup_layers":
             ml.ctx.set_option("gcn_fused", 0)
-        ml.ctx.set_option("gcn_dedup" if knob.startswith("gcn_dedup") else knob, on)
+        if knob.endswith("_streams"):
+            ml.ctx.set_option("bwd_big_min", 0)  # (chunked diagonals always run the big tiles: both arms do)
+            ml.ctx.set_option(knob, 2 if on else 1)
+        else:
+            ml.ctx.set_option("gcn_dedup" if knob.startswith("gcn_dedup") else knob, on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()
         vc = ml.ctx.variant_counts()

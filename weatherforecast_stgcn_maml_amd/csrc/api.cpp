@@ -232,7 +232,7 @@ struct smaml_ctx {
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
-           SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT};
+           SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT};
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -289,6 +289,9 @@ struct smaml_ctx {
   // activations of the last smaml_forward / smaml_lstm_forward (single task, act_B samples);
   // -1 once anything else has used the workspace (the backward consumes them: dG in place)
   int act_B = -1;
+  // side streams of the row-chunked BPTT (knob bptt_streams) and their fork / join events
+  hipStream_t cs[4] = {};
+  hipEvent_t fork_ev = nullptr, join_ev[4] = {};
   // RCCL communicator (smaml_comm_init), opaque; created non-blocking when the library allows it
   void* comm = nullptr;
   int comm_nb = 0;
@@ -637,6 +640,26 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
   return true;
 }
 
+// Side streams for row chunks of the BPTT (knob bptt_streams): each waits for the work already on s.
+int fork_streams(smaml_ctx* c, hipStream_t s, int n) {
+  if (!c->fork_ev) HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->fork_ev, s));
+  for (int i = 0; i < n; ++i) {
+    if (!c->cs[i]) HIP_TRY(hipStreamCreateWithFlags(&c->cs[i], hipStreamNonBlocking));
+    if (!c->join_ev[i]) HIP_TRY(hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming));
+    HIP_TRY(hipStreamWaitEvent(c->cs[i], c->fork_ev, 0));
+  }
+  return SMAML_OK;
+}
+// s waits for everything issued on the side streams
+int join_streams(smaml_ctx* c, hipStream_t s, int n) {
+  for (int i = 0; i < n; ++i) {
+    HIP_TRY(hipEventRecord(c->join_ev[i], c->cs[i]));
+    HIP_TRY(hipStreamWaitEvent(s, c->join_ev[i], 0));
+  }
+  return SMAML_OK;
+}
+
 // The XgDedup-row-order scratch (k_xg_dedup tables / k_dg_rowsum sums) with room for `floats`, or null.
 float* xgd_scratch(smaml_ctx* c, int64_t floats) {
   if (floats > c->xgd_cap) {
@@ -909,14 +932,24 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
       w.xg_src = theta;
     }
   }
+  // row chunks on side streams (knob fwd_streams; big sizes only, where every diagonal runs the big tiles)
+  const int nch = (int64_t)w.Z * w.M > c->kn.wgrad_group_max_rows && !w.xg ? c->kn.fwd_streams : 1;
+  if (nch > 1) TRY(fork_streams(c, s, nch));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
     if ((w.xg && fwd_wave_kw(d, w, c->po, diag)) || use_xgd)  // (the projection's flops are counted above)
       for (int q = 0; q < wv.n; ++q)
         if (wv.l[q] == 0) fl -= 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
-    TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
+    if (nch > 1) {
+      for (int ci = 0; ci < nch; ++ci)
+        TIMED(c, c->cs[ci], C_FWD, fl / nch,
+              launch_lstm_fwd_wave(c->cs[ci], d, w, diag, theta, tstride, c->po, nullptr, ci, nch));
+    } else {
+      TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
+    }
   }
+  if (nch > 1) TRY(join_streams(c, s, nch));
   w.xg = nullptr;
   w.xg_src = nullptr;
   w.xgd = XgDedup{};
@@ -976,12 +1009,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   TRY(prep_bwd_images(c, s, theta, tstride));
   WgradPlan plans[MAX_LAYERS];
   double gfl = 0.0;
-  for (int e = 0; e < d.T + d.L - 1; ++e) {
-    BwdWave wv{};
-    const double fl = bwd_wave(d, w, po, e, 0, false, wv);
-    TIMED(c, s, C_BWD, fl, launch_lstm_bwd_wave(s, d, w, e, theta, tstride, po));
-    const int l = d.L - 1 - (e - (d.T - 1));
-    if (e < d.T - 1 || l < 0) continue;
+  auto layer_wgrad = [&](int l) {
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     if (grouped) {
@@ -992,17 +1020,38 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       p.drop = w.drop;
       p.drop_layer = l - 1;
       gfl += 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H);
-      continue;
+      return;
     }
     if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, w.dG, grad)) {
       // W_hh0 and the bias over every row (h_{t-1} differs per window): [0 | h_{t-1}], no input columns
       timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * d.H, w.dG, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.Hs, TM * d.H,
                   d.H, TM, w.M, grad, po.P, -1, lo.whh, lo.bih, lo.bhh, true, false, -1);
-      continue;
+      return;
     }
-    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
-                       w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh, lo.bih,
-                       lo.bhh, true, false, l - 1);
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X,
+                TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh,
+                lo.bih, lo.bhh, true, false, l - 1);
+  };
+  // row chunks on side streams (knob bptt_streams): every diagonal's big-tile launch split by rows, the
+  // weight gradients after the sweep on the caller's stream
+  const int nch = grouped ? 1 : c->kn.bptt_streams;
+  if (nch > 1) TRY(fork_streams(c, s, nch));
+  for (int e = 0; e < d.T + d.L - 1; ++e) {
+    BwdWave wv{};
+    const double fl = bwd_wave(d, w, po, e, 0, false, wv);
+    if (nch > 1) {
+      for (int ci = 0; ci < nch; ++ci)
+        TIMED(c, c->cs[ci], C_BWD, fl / nch, launch_lstm_bwd_wave(c->cs[ci], d, w, e, theta, tstride, po, ci, nch));
+    } else {
+      TIMED(c, s, C_BWD, fl, launch_lstm_bwd_wave(s, d, w, e, theta, tstride, po));
+    }
+    const int l = d.L - 1 - (e - (d.T - 1));
+    if (e < d.T - 1 || l < 0 || nch > 1) continue;
+    layer_wgrad(l);
+  }
+  if (nch > 1) {
+    TRY(join_streams(c, s, nch));
+    for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
   HIP_TRY(hipGetLastError());
@@ -1019,6 +1068,8 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   TRY(prep_gate_images(c, s, theta, tstride, U));
   // layer 0's tangent projection F U_ih0^T (and, unless the primal is kept, F W_ih0^T) once per stream row
   const bool use_xgd = prep_xg_dedup(c, s, first_tab != nullptr, theta, U, tstride, !w.primal_kept);
+  const int nch = (int64_t)w.Z * w.M > c->kn.wgrad_group_max_rows ? c->kn.fwd_streams : 1;  // (row chunks)
+  if (nch > 1) TRY(fork_streams(c, s, nch));
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
@@ -1026,8 +1077,15 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
     if (use_xgd)  // (counted in C_XG)
       for (int q = 0; q < wv.n; ++q)
         if (wv.l[q] == 0) fl -= (w.primal_kept ? 1.0 : 2.0) * 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
-    TIMED(c, s, C_FWD_DUAL, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
+    if (nch > 1) {
+      for (int ci = 0; ci < nch; ++ci)
+        TIMED(c, c->cs[ci], C_FWD_DUAL, fl / nch,
+              launch_lstm_fwd_dual_wave(c->cs[ci], d, w, diag, theta, U, tstride, c->po, nullptr, ci, nch));
+    } else {
+      TIMED(c, s, C_FWD_DUAL, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
+    }
   }
+  if (nch > 1) TRY(join_streams(c, s, nch));
   w.xgd = XgDedup{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -1048,12 +1106,7 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false);
   timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, RhT, hz, d.H, nullptr, 0, 0,
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true);
-  for (int e = 0; e < d.T + d.L - 1; ++e) {
-    BwdWave wv{};
-    const double fl = bwd_wave(d, w, po, e, 0, true, wv) * (w.primal_kept ? 2.0 / 3.0 : 1.0);
-    TIMED(c, s, C_BWD_DUAL, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
-    const int l = d.L - 1 - (e - (d.T - 1));
-    if (e < d.T - 1 || l < 0) continue;
+  auto layer_wgrad = [&](int l) {
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
@@ -1071,18 +1124,39 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
         timed_wgrad(c, s, flp / 2, dGl, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.RHs, TM * d.H, d.H, TM, w.M, HU, po.P,
                     -1, lo.whh, lo.bih, lo.bhh, false, true, -1);
       }
-      continue;
+      return;
     }
     if (l > 0 && c->kn.wgrad_pair &&  // both passes 4H x (cin + H): one launch
         timed_wgrad_pair(c, s, 2.0 * 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, dGl, TM * 4 * d.H, 4 * d.H, X,
                          RX, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, w.RHs + (int64_t)l * lsz, TM * d.H, d.H,
                          TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, l - 1))
-      continue;
-    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz,
-                       TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false, l - 1);
-    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX, TM * lo.cin, l > 0 ? lo.cin : 0,
-                       w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh,
-                       false, true, l - 1);
+      return;
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), RdGl, TM * 4 * d.H, 4 * d.H, X, TM * lo.cin, lo.cin,
+                w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih, lo.whh, lo.bih, lo.bhh, true, false,
+                l - 1);
+    timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX,
+                TM * lo.cin, l > 0 ? lo.cin : 0, w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih,
+                lo.whh, lo.bih, lo.bhh, false, true, l - 1);
+  };
+  const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows ? 1 : c->kn.bptt_streams;
+  if (nch > 1) TRY(fork_streams(c, s, nch));
+  for (int e = 0; e < d.T + d.L - 1; ++e) {
+    BwdWave wv{};
+    const double fl = bwd_wave(d, w, po, e, 0, true, wv) * (w.primal_kept ? 2.0 / 3.0 : 1.0);
+    if (nch > 1) {
+      for (int ci = 0; ci < nch; ++ci)
+        TIMED(c, c->cs[ci], C_BWD_DUAL, fl / nch,
+              launch_lstm_bwd_dual_wave(c->cs[ci], d, w, e, theta, U, tstride, po, ci, nch));
+    } else {
+      TIMED(c, s, C_BWD_DUAL, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
+    }
+    const int l = d.L - 1 - (e - (d.T - 1));
+    if (e < d.T - 1 || l < 0 || nch > 1) continue;
+    layer_wgrad(l);
+  }
+  if (nch > 1) {
+    TRY(join_streams(c, s, nch));
+    for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -1255,6 +1329,11 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->xg_buf) (void)hipFree(c->xg_buf);
   if (c->xgd_buf) (void)hipFree(c->xgd_buf);
   if (c->bar) (void)hipFree(c->bar);
+  for (int i = 0; i < 4; ++i) {
+    if (c->cs[i]) (void)hipStreamDestroy(c->cs[i]);
+    if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
+  }
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
   if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
@@ -1819,6 +1898,10 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.xg_dedup = (int)value;
   } else if (k == "wgrad_dedup" && (value == 0 || value == 1)) {
     c->kn.wgrad_dedup = (int)value;
+  } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
+    c->kn.bptt_streams = (int)value;
+  } else if (k == "fwd_streams" && value >= 1 && value <= 4) {
+    c->kn.fwd_streams = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
     c->ad_gcn_batch = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {

@@ -136,6 +136,10 @@ struct Knobs {
                                  // distinct stream row (k_xg_dedup), added to the gate accumulators
   int wgrad_dedup = 0;           // 1: ... and layer 0's input-weight gradient (and its tangent) over the distinct
                                  // stream rows: row sums of dG0 (k_dg_rowsum) times the gathered F rows
+  int bptt_streams = 1;          // > 1: the big-tile BPTT diagonals (primal and tangent) split into this many row
+                                 // chunks on side streams (a chunk's rows depend on nothing else), so one
+                                 // chunk's next diagonal fills the other's tail; weight gradients after the sweep
+  int fwd_streams = 1;           // the same for the big-tile forward diagonals (primal and tangent)
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -157,6 +161,12 @@ struct Knobs {
 #endif
 #ifndef SMAML_WGRAD_DEDUP_DEFAULT
 #define SMAML_WGRAD_DEDUP_DEFAULT 1
+#endif
+#ifndef SMAML_BPTT_STREAMS_DEFAULT
+#define SMAML_BPTT_STREAMS_DEFAULT 1
+#endif
+#ifndef SMAML_FWD_STREAMS_DEFAULT
+#define SMAML_FWD_STREAMS_DEFAULT 1
 #endif
 #ifndef SMAML_WGRAD_PAIR
 #define SMAML_WGRAD_PAIR 1
@@ -341,6 +351,7 @@ struct FwdWave {
   int n = 0;
   int l[MAX_LAYERS] = {}, t[MAX_LAYERS] = {}, off[MAX_LAYERS + 1] = {};
   LayerOff lo[MAX_LAYERS] = {};
+  int tm0 = 0, ntm = 0;  // big-tile gate kernels: row tiles [tm0, tm0 + ntm) (ntm 0 = all of them)
 };
 // Backward counterpart: problems (l, t) with (L-1-l) + (T-1-t) = e. Step (l, t) forms
 //   dh = [dG(l+1, t) | dG(l, t+1)] . [W_ih(l+1) ; W_hh(l)]   (one K = 8H GEMM; the dX of the
@@ -350,6 +361,7 @@ struct BwdWave {
   int l[MAX_LAYERS] = {}, t[MAX_LAYERS] = {}, off[MAX_LAYERS + 1] = {};
   LayerOff lo[MAX_LAYERS] = {};
   int64_t wih_up[MAX_LAYERS] = {};  // W_ih offset of layer l+1 (unused at the top layer)
+  int tm0 = 0;  // big-tile kernels: first row tile of this launch (row chunks on separate streams)
 };
 double bwd_wave(const Dims& d, const Work& w, const ParamOff& po, int e, int blocks_per_problem, bool dual,
                 BwdWave& wv);
@@ -418,8 +430,9 @@ void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* co
 // weights come from the pre-split images `img` when given (w.gimg.th / .u), else from `params`
 void launch_xg_dedup(hipStream_t s, const Dims& d, const Work& w, const float* params, int64_t tstride,
                      const ParamOff& po, const char* img, int64_t img_tstride, int64_t img_off, float* out);
+// chunk / nch: row chunks as in launch_lstm_bwd_wave (nch > 1: every diagonal on the big tiles)
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
-                          int64_t tstride, const ParamOff& po, double* flops);
+                          int64_t tstride, const ParamOff& po, double* flops, int chunk = 0, int nch = 1);
 void launch_head_loss(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                       const ParamOff& po, const float* const* xtab, float dscale, bool want_loss);
 void launch_head_loss_y(hipStream_t s, const Dims& d, const Work& w, const float* hT, const float* theta,
@@ -445,8 +458,11 @@ void launch_dropout_inplace(hipStream_t s, float* x, int64_t n, float p, uint32_
 const float* head_input(const Dims& d, const Work& w, bool tangent, int64_t* zstride);
 void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* theta, int64_t tstride,
                     const ParamOff& po);
+// chunk / nch: the launch covers row tiles [chunk ntm / nch, (chunk + 1) ntm / nch) of every problem on the
+// big tiles whatever the size (the BPTT of a row touches only that row's slabs, so row chunks on separate
+// streams are independent -- as long as EVERY diagonal is chunked the same way)
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
-                          const ParamOff& po);
+                          const ParamOff& po, int chunk = 0, int nch = 1);
 // kernels_small.hip: the small-grid (batch-1) forward / BPTT diagonal as one launch with the K
 // reduction split over the waves of a workgroup (used where the split-K pair would run)
 bool small_kw_ok(const Dims& d, const Work& w);
@@ -552,13 +568,14 @@ void launch_adam_l2(hipStream_t s, float* p, const float* g, float* m, float* v,
 
 // ---- second-order launchers (kernels_dual.hip) ----
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
-                               const float* U, int64_t tstride, const ParamOff& po, double* flops);
+                               const float* U, int64_t tstride, const ParamOff& po, double* flops, int chunk = 0,
+                               int nch = 1);
 void launch_head_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
                       int64_t tstride, const ParamOff& po, const float* const* xtab, float dscale);
 void launch_head_dh_dual(hipStream_t s, const Dims& d, const Work& w, const float* theta, const float* U,
                          int64_t tstride, const ParamOff& po);
 void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
-                               const float* U, int64_t tstride, const ParamOff& po);
+                               const float* U, int64_t tstride, const ParamOff& po, int chunk = 0, int nch = 1);
 void launch_axpy(hipStream_t s, float* V, const float* X, int64_t n, float alpha);
 
 }  // namespace smaml

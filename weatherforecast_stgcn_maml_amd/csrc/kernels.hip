@@ -379,8 +379,10 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
   LstmFwdB<H> lb{th + lo.wih, th + lo.whh, cin};
   int tm, ug;
   constexpr int UPB = CfgGate::WAVES_N;  // 32-unit groups per workgroup
-  if (!gate_tile(bk.x - b0, (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+  if (!gate_tile(bk.x - b0, wv.ntm ? wv.ntm : (M + CfgGate::BM - 1) / CfgGate::BM, (H + 32 * UPB - 1) / (32 * UPB), tm,
+                 ug))
     return;
+  tm += wv.tm0;
   const int m0 = tm * CfgGate::BM, n0 = ug * CfgGate::BN;
   Acc<CfgGate> acc;
   int kbeg = 0;  // (XG: the K loop starts past the input segment)
@@ -771,7 +773,7 @@ bool fwd_wave_big(const Dims& d, const Work& w, const ParamOff& po, int diag) {
 }
 
 void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
-                          int64_t tstride, const ParamOff& po, double* flops) {
+                          int64_t tstride, const ParamOff& po, double* flops, int chunk, int nch) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   const int ntm = (w.M + CfgGate::BM - 1) / CfgGate::BM;
   const int ngrp = (d.H + 32 * CfgGate::WAVES_N - 1) / (32 * CfgGate::WAVES_N);
@@ -779,6 +781,13 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   const double fl = fwd_wave(d, w, po, diag, gate_blocks(ntm, ngrp), false, wv);
   if (flops) *flops = fl;
   if (wv.n == 0) return;
+  if (nch > 1) {  // this launch's row tiles only, always on the big tiles (see launch_lstm_bwd_wave)
+    const int lo = (int)((int64_t)ntm * chunk / nch), hi = (int)((int64_t)ntm * (chunk + 1) / nch);
+    if (hi <= lo) return;
+    fwd_wave(d, w, po, diag, gate_blocks(hi - lo, ngrp), false, wv);
+    wv.tm0 = lo;
+    wv.ntm = hi - lo;
+  }
   dim3 grid(wv.off[wv.n], 1, w.Z);
   if (w.drop.lstm()) {
     count_variant(w, V_FWD_DROP);
@@ -786,7 +795,7 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
                                                                                    tstride, wv, d.T, w.M, w.drop));
     return;
   }
-  {
+  if (nch <= 1) {
     // split-K over the small-grid tile (CfgGateP): its own block offsets per problem
     const int ntmP = (w.M + CfgGateP::BM - 1) / CfgGateP::BM;
     const int ngrpP = (d.H + 32 * CfgGateP::WAVES_N - 1) / (32 * CfgGateP::WAVES_N);
@@ -1375,6 +1384,7 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
   const Blk bk = xcd_block();
   int mb;
   const int p = bwd_block(wv, bk.x, mb);
+  mb += wv.tm0;
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
   const LayerOff lo = wave_sel(wv.lo, p);
   const int64_t wih_up = wave_sel(wv.wih_up, p);
@@ -1558,17 +1568,26 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell_q(const float* GsA
 #endif
 
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
-                          const ParamOff& po) {
+                          const ParamOff& po, int chunk, int nch) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   BwdWave wv{};
   const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
+  // row chunks (nch > 1) always run the big tiles: every diagonal of a chunk must touch only its rows,
+  // or a chunk's next diagonal would race with another stream's whole-row launch
+  const bool big = nch > 1 || (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min;
+  if (nch > 1) {  // this launch's row tiles only
+    const int lo = (int)((int64_t)ntm * chunk / nch), hi = (int)((int64_t)ntm * (chunk + 1) / nch);
+    if (hi <= lo) return;
+    bwd_wave(d, w, po, e, hi - lo, false, wv);
+    wv.tm0 = lo;
+  }
 #define SMAML_BWD_STEP(CFG, D_)                                                                               \
   SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
                             w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
   // threshold in 64-row tile units (the knob predates the 128-row tile)
-  if ((int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min) {
+  if (big) {
     count_variant(w, V_BWD_BIG);
     dim3 grid(wv.off[wv.n], ntn, w.Z);
     if (w.drop.lstm()) {

@@ -220,8 +220,10 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
   const int wh = hp ? H : 0;
   int tm, ug;
   constexpr int UPB = CfgGateD::WAVES_N;  // 32-unit groups per workgroup
-  if (!gate_tile(bk.x - b0, (M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB), tm, ug))
+  if (!gate_tile(bk.x - b0, wv.ntm ? wv.ntm : (M + CfgGateD::BM - 1) / CfgGateD::BM, (H + 32 * UPB - 1) / (32 * UPB),
+                 tm, ug))
     return;
+  tm += wv.tm0;
   const int m0 = tm * CfgGateD::BM, n0 = ug * CfgGateD::BN;
   XDrop xdr{};
   if (DROP && l > 0)
@@ -328,7 +330,7 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
 }
 
 void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int diag, const float* theta,
-                               const float* U, int64_t tstride, const ParamOff& po, double* flops) {
+                               const float* U, int64_t tstride, const ParamOff& po, double* flops, int chunk, int nch) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
   const int ntm = (w.M + CfgGateD::BM - 1) / CfgGateD::BM;
   const int ngrp = (d.H + 32 * CfgGateD::WAVES_N - 1) / (32 * CfgGateD::WAVES_N);
@@ -336,6 +338,13 @@ void launch_lstm_fwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   const double fl = fwd_wave(d, w, po, diag, gate_blocks(ntm, ngrp), true, wv);
   if (flops) *flops = fl;
   if (wv.n == 0) return;
+  if (nch > 1) {  // this launch's row tiles only (see launch_lstm_fwd_wave)
+    const int lo = (int)((int64_t)ntm * chunk / nch), hi = (int)((int64_t)ntm * (chunk + 1) / nch);
+    if (hi <= lo) return;
+    fwd_wave(d, w, po, diag, gate_blocks(hi - lo, ngrp), true, wv);
+    wv.tm0 = lo;
+    wv.ntm = hi - lo;
+  }
   dim3 grid(wv.off[wv.n], 1, w.Z);
   const bool kept = w.primal_kept != 0, drop = w.drop.lstm();
   count_variant(w, kept ? V_FWDD_KEPT : V_FWDD);
@@ -665,6 +674,7 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
     z = bk.z;
     ny = bk.y;
   }
+  mb += wv.tm0;
   const int Zt = rm.on ? rm.Z : (int)gridDim.z;
   const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
   const LayerOff lo = wave_sel(wv.lo, p);
@@ -827,13 +837,21 @@ static void bwd_dual_grid(hipStream_t s, const Dims& d, const Work& w, const Bwd
 }
 
 void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
-                               const float* U, int64_t tstride, const ParamOff& po) {
+                               const float* U, int64_t tstride, const ParamOff& po, int chunk, int nch) {
   BwdWave wv{};
   const int ntm = (w.M + CfgBwdD::BM - 1) / CfgBwdD::BM, ntn = (d.H + CfgBwdD::BN - 1) / CfgBwdD::BN;
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
   const bool kept = w.primal_kept != 0;
-  if ((int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min) {  // 64-row tile units
+  // (64-row tile units; row chunks always on the big tiles, see launch_lstm_bwd_wave)
+  const bool big = nch > 1 || (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min;
+  if (nch > 1) {  // this launch's row tiles only
+    const int lo = (int)((int64_t)ntm * chunk / nch), hi = (int)((int64_t)ntm * (chunk + 1) / nch);
+    if (hi <= lo) return;
+    bwd_wave(d, w, po, e, hi - lo, true, wv);
+    wv.tm0 = lo;
+  }
+  if (big) {
     count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
     if (kept)
       bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
