@@ -269,7 +269,10 @@ int smaml_timing(smaml_ctx* ctx, int32_t enable);
  * 7 wgrad (split-K GEMM), 8 wgrad_reduce, 9 misc, 10 xg_proj (layer 0's input projection formed before
  * the wavefront: k_xg_dedup once per distinct stream row of consecutive windows, or the batch-1
  * k_gemm_nt), 11 dg_rowsum (k_dg_rowsum: layer 0's dG summed per distinct stream row before its
- * input-weight gradient). */
+ * input-weight gradient), 12-15 lstm_fwd_step_wall, lstm_fwd_dual_wall, lstm_bwd_step_wall,
+ * lstm_bwd_dual_wall: the wall time of a forward / tangent-forward / BPTT / tangent-BPTT sweep whose
+ * diagonals ran as concurrent row chunks on side streams (options fwd_streams / bptt_streams; the
+ * per-category kernel times 1, 2, 5, 6 then sum the concurrent chunks' launches). */
 int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* count, int32_t cap);
 
 /* Launch counts per kernel variant (tile configuration) since the last reset, in the order of
@@ -331,7 +334,13 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "wgrad_dedup":                 the same steps form layer 0's input-weight gradient (and its tangent)
  *                                  over the distinct stream rows: dG0 summed per stream row
  *                                  (k_dg_rowsum) times the gathered F rows, (2B + T - 2) N rows
- *                                  instead of T B N (1, the default; equal to 0 up to summation order). */
+ *                                  instead of T B N (1, the default; equal to 0 up to summation order);
+ *   "bptt_streams", "fwd_streams": every BPTT / forward diagonal (primal and tangent) of a large
+ *                                  launch split into this many row chunks on side streams (1-4; rows are
+ *                                  independent through the whole recurrence, so a chunk's next diagonal
+ *                                  fills another's tail; bitwise equal to 1). Defaults: bptt_streams 2,
+ *                                  fwd_streams 0 = auto (2 when a problem's gate launch fills at most
+ *                                  two workgroups per CU, else 1). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -496,14 +496,16 @@ def _check_meta_step(res, ml, ref, d, names, n_tasks, K):
         assert rel(mg[k].cpu().numpy(), ref["meta_grad"][k].numpy()) < 1e-4, k
 
 
+@pytest.mark.parametrize("streams", [1, 2])
 @pytest.mark.parametrize("keep", [-1, 0, 1])
-def test_second_order_bench_tiles_b32(keep):
+def test_second_order_bench_tiles_b32(keep, streams):
     """1 task x B=32 x K=2 at config-2 shapes (M = 14,112 sequences): a diagonal with all 4
     layers holds 4 x 111 x 2 = 888 >= 768 64-row tile units, so the bench's 128x128
-    k_lstm_bwd_step and k_lstm_bwd_dual run (kept-primal and recomputed-primal forms by `keep`);
-    the short corner diagonals run the 64x64 tiles. Per-step losses, query MSE and the
-    second-order meta-gradient against the oracle (train_hybrid_maml_v5.py:110-184 + torch
-    autograd)."""
+    k_lstm_bwd_step and k_lstm_bwd_dual run (kept-primal and recomputed-primal forms by `keep`).
+    streams 1: the short corner diagonals run the 64x64 tiles; streams 2 (the default bptt_streams):
+    every diagonal in two row chunks on side streams, all on the 128x128 tiles. Per-step losses,
+    query MSE and the second-order meta-gradient against the oracle (train_hybrid_maml_v5.py:110-184
+    + torch autograd)."""
     d = CONFIG2
     cfg = MamlConfig(inner_steps=2, batch=32, order=2)
     P = synth.init_params(13, d, gcn_bias_scale=0.1)
@@ -513,10 +515,11 @@ def test_second_order_bench_tiles_b32(keep):
     ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=None)
     ml.set_tasks(feats)
     ml.ctx.set_option("keep", keep)
+    ml.ctx.set_option("bptt_streams", streams)
     ml.ctx.variant_counts(reset=True)
     res = ml.meta_step()
     vc = ml.ctx.variant_counts()
-    assert vc["bwd_big"] > 0 and vc["bwd_small"] > 0, vc
+    assert vc["bwd_big"] > 0 and (vc["bwd_small"] > 0) == (streams == 1), vc
     if keep == 0:
         assert vc["bwd_dual_big"] > 0 and vc["bwd_dual_big_kept"] == 0, vc
     elif keep == 1:

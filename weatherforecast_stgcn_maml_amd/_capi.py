@@ -35,7 +35,8 @@ VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kep
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",
-                     "lstm_bwd_dual", "wgrad", "wgrad_reduce", "misc", "xg_proj", "dg_rowsum")
+                     "lstm_bwd_dual", "wgrad", "wgrad_reduce", "misc", "xg_proj", "dg_rowsum",
+                     "lstm_fwd_step_wall", "lstm_fwd_dual_wall", "lstm_bwd_step_wall", "lstm_bwd_dual_wall")
 
 ERRORS = {1: "EINVAL", 2: "EHIP", 3: "ENOMEM", 4: "ESTATE", 5: "ENOTIMPL"}
 

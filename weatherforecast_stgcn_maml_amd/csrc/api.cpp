@@ -127,8 +127,10 @@ int build_ell(const int64_t* ei, int64_t E, int N, std::vector<int32_t>& cols, s
 }
 
 // one kernel per timing category (bench roofline = one kernel's launches)
+// (the *_WALL categories: the wall time of a sweep whose diagonals ran as concurrent row chunks on side
+// streams -- events on the caller's stream around the fork / join -- beside the per-chunk kernel times)
 enum Cat { C_GCN = 0, C_FWD, C_FWD_DUAL, C_HEAD, C_HEAD_DH, C_BWD, C_BWD_DUAL, C_WGRAD, C_WGRAD_RED, C_MISC, C_XG, C_DGSUM,
-           NCAT };
+           C_FWD_WALL, C_FWD_DUAL_WALL, C_BWD_WALL, C_BWD_DUAL_WALL, NCAT };
 
 // Live per-category kernel timing with HIP events on the launch stream (bench roofline).
 struct Timer {
@@ -233,6 +235,7 @@ struct smaml_ctx {
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
            SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT};
+  int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
   std::vector<const float*> feats;
@@ -640,6 +643,19 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
   return true;
 }
 
+// Row chunks of a forward sweep (knob fwd_streams; 0 = auto: two when one problem's big-tile gate launch
+// fills at most one round of the device's workgroup slots, e.g. config 5's one-task groups, where the
+// chunks fill each other's tails; at config 2 a diagonal is ~9 rounds and chunking measured slower).
+int fwd_chunks(const smaml_ctx* c) {
+  const Work& w = c->w;
+  // (only where the full diagonal runs the big tiles anyway; every chunked diagonal does)
+  if ((int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows || !fwd_wave_big(c->d, w, c->po, std::min(c->d.L, c->d.T) - 1))
+    return 1;
+  if (c->kn.fwd_streams > 0) return c->kn.fwd_streams;
+  const int64_t wgs = (int64_t)(w.M + 255) / 256 * ((c->d.H + 31) / 32) * w.Z;  // 256-row x 32-unit gate tiles
+  return wgs <= 2LL * c->n_cu ? 2 : 1;
+}
+
 // Side streams for row chunks of the BPTT (knob bptt_streams): each waits for the work already on s.
 int fork_streams(smaml_ctx* c, hipStream_t s, int n) {
   if (!c->fork_ev) HIP_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
@@ -651,6 +667,21 @@ int fork_streams(smaml_ctx* c, hipStream_t s, int n) {
   }
   return SMAML_OK;
 }
+// the workspace as chunk ci's launches see it: launch counters once per diagonal (chunk 0's)
+Work chunk_work(const Work& w, int ci) {
+  Work q = w;
+  if (ci > 0) q.vcount = nullptr;
+  return q;
+}
+
+// a timing record of category cat from event a (recorded on s before a fork) to now on s (after the join)
+void time_wall(smaml_ctx* c, hipStream_t s, hipEvent_t a, int cat, double fl) {
+  if (!a) return;
+  hipEvent_t b = c->tm.get();
+  (void)hipEventRecord(b, s);
+  c->tm.recs.push_back({cat, a, b, fl});
+}
+
 // s waits for everything issued on the side streams
 int join_streams(smaml_ctx* c, hipStream_t s, int n) {
   for (int i = 0; i < n; ++i) {
@@ -932,24 +963,31 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
       w.xg_src = theta;
     }
   }
-  // row chunks on side streams (knob fwd_streams; big sizes only, where every diagonal runs the big tiles)
-  const int nch = (int64_t)w.Z * w.M > c->kn.wgrad_group_max_rows && !w.xg ? c->kn.fwd_streams : 1;
+  // row chunks on side streams (fwd_chunks; big sizes only, where every diagonal runs the big tiles)
+  const int nch = w.xg ? 1 : fwd_chunks(c);
+  hipEvent_t wa = nullptr;
+  if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
+  double wfl = 0.0;
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, false, wv);
     if ((w.xg && fwd_wave_kw(d, w, c->po, diag)) || use_xgd)  // (the projection's flops are counted above)
       for (int q = 0; q < wv.n; ++q)
         if (wv.l[q] == 0) fl -= 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
+    wfl += fl;
     if (nch > 1) {
       for (int ci = 0; ci < nch; ++ci)
         TIMED(c, c->cs[ci], C_FWD, fl / nch,
-              launch_lstm_fwd_wave(c->cs[ci], d, w, diag, theta, tstride, c->po, nullptr, ci, nch));
+              launch_lstm_fwd_wave(c->cs[ci], d, chunk_work(w, ci), diag, theta, tstride, c->po, nullptr, ci, nch));
     } else {
       TIMED(c, s, C_FWD, fl, launch_lstm_fwd_wave(s, d, w, diag, theta, tstride, c->po, nullptr));
     }
   }
-  if (nch > 1) TRY(join_streams(c, s, nch));
+  if (nch > 1) {
+    TRY(join_streams(c, s, nch));
+    time_wall(c, s, wa, C_FWD_WALL, wfl);
+  }
   w.xg = nullptr;
   w.xg_src = nullptr;
   w.xgd = XgDedup{};
@@ -1034,14 +1072,19 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   };
   // row chunks on side streams (knob bptt_streams): every diagonal's big-tile launch split by rows, the
   // weight gradients after the sweep on the caller's stream
-  const int nch = grouped ? 1 : c->kn.bptt_streams;
+  // (chunked only where a full diagonal runs the big tiles anyway: tile-forcing knobs keep their meaning)
+  const int nch = grouped || !bwd_wave_big(d, w, po, std::min(d.L, d.T) - 1) ? 1 : c->kn.bptt_streams;
+  hipEvent_t wa = nullptr;
+  if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
+  double wfl = 0.0;
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
     const double fl = bwd_wave(d, w, po, e, 0, false, wv);
+    wfl += fl;
     if (nch > 1) {
       for (int ci = 0; ci < nch; ++ci)
-        TIMED(c, c->cs[ci], C_BWD, fl / nch, launch_lstm_bwd_wave(c->cs[ci], d, w, e, theta, tstride, po, ci, nch));
+        TIMED(c, c->cs[ci], C_BWD, fl / nch, launch_lstm_bwd_wave(c->cs[ci], d, chunk_work(w, ci), e, theta, tstride, po, ci, nch));
     } else {
       TIMED(c, s, C_BWD, fl, launch_lstm_bwd_wave(s, d, w, e, theta, tstride, po));
     }
@@ -1051,6 +1094,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   }
   if (nch > 1) {
     TRY(join_streams(c, s, nch));
+    time_wall(c, s, wa, C_BWD_WALL, wfl);
     for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
@@ -1068,8 +1112,11 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   TRY(prep_gate_images(c, s, theta, tstride, U));
   // layer 0's tangent projection F U_ih0^T (and, unless the primal is kept, F W_ih0^T) once per stream row
   const bool use_xgd = prep_xg_dedup(c, s, first_tab != nullptr, theta, U, tstride, !w.primal_kept);
-  const int nch = (int64_t)w.Z * w.M > c->kn.wgrad_group_max_rows ? c->kn.fwd_streams : 1;  // (row chunks)
+  const int nch = fwd_chunks(c);  // (row chunks on side streams)
+  hipEvent_t wa = nullptr;
+  if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
+  double wfl = 0.0;
   for (int diag = 0; diag < d.T + d.L - 1; ++diag) {
     FwdWave wv{};
     double fl = fwd_wave(d, w, c->po, diag, 0, true, wv);
@@ -1077,15 +1124,19 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
     if (use_xgd)  // (counted in C_XG)
       for (int q = 0; q < wv.n; ++q)
         if (wv.l[q] == 0) fl -= (w.primal_kept ? 1.0 : 2.0) * 2.0 * w.Z * w.M * 4 * d.H * wv.lo[q].cin;
+    wfl += fl;
     if (nch > 1) {
       for (int ci = 0; ci < nch; ++ci)
         TIMED(c, c->cs[ci], C_FWD_DUAL, fl / nch,
-              launch_lstm_fwd_dual_wave(c->cs[ci], d, w, diag, theta, U, tstride, c->po, nullptr, ci, nch));
+              launch_lstm_fwd_dual_wave(c->cs[ci], d, chunk_work(w, ci), diag, theta, U, tstride, c->po, nullptr, ci, nch));
     } else {
       TIMED(c, s, C_FWD_DUAL, fl, launch_lstm_fwd_dual_wave(s, d, w, diag, theta, U, tstride, c->po, nullptr));
     }
   }
-  if (nch > 1) TRY(join_streams(c, s, nch));
+  if (nch > 1) {
+    TRY(join_streams(c, s, nch));
+    time_wall(c, s, wa, C_FWD_DUAL_WALL, wfl);
+  }
   w.xgd = XgDedup{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -1138,15 +1189,21 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
                 TM * lo.cin, l > 0 ? lo.cin : 0, w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih,
                 lo.whh, lo.bih, lo.bhh, false, true, l - 1);
   };
-  const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows ? 1 : c->kn.bptt_streams;
+  const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows || !bwd_dual_wave_big(d, w, po, std::min(d.L, d.T) - 1)
+                      ? 1
+                      : c->kn.bptt_streams;
+  hipEvent_t wa = nullptr;
+  if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
+  double wfl = 0.0;
   for (int e = 0; e < d.T + d.L - 1; ++e) {
     BwdWave wv{};
     const double fl = bwd_wave(d, w, po, e, 0, true, wv) * (w.primal_kept ? 2.0 / 3.0 : 1.0);
+    wfl += fl;
     if (nch > 1) {
       for (int ci = 0; ci < nch; ++ci)
         TIMED(c, c->cs[ci], C_BWD_DUAL, fl / nch,
-              launch_lstm_bwd_dual_wave(c->cs[ci], d, w, e, theta, U, tstride, po, ci, nch));
+              launch_lstm_bwd_dual_wave(c->cs[ci], d, chunk_work(w, ci), e, theta, U, tstride, po, ci, nch));
     } else {
       TIMED(c, s, C_BWD_DUAL, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
     }
@@ -1156,6 +1213,7 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   }
   if (nch > 1) {
     TRY(join_streams(c, s, nch));
+    time_wall(c, s, wa, C_BWD_DUAL_WALL, wfl);
     for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   HIP_TRY(hipGetLastError());
@@ -1299,6 +1357,8 @@ int smaml_create(const smaml_dims* dims, int32_t device, smaml_ctx** out) {
     delete c;
     return fail(SMAML_EHIP, std::string("context init: ") + hipGetErrorString(e));
   }
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->n_cu = ncu;
   *out = c;
   return SMAML_OK;
 }
@@ -1900,7 +1960,7 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_dedup = (int)value;
   } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
     c->kn.bptt_streams = (int)value;
-  } else if (k == "fwd_streams" && value >= 1 && value <= 4) {
+  } else if (k == "fwd_streams" && value >= 0 && value <= 4) {
     c->kn.fwd_streams = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
     c->ad_gcn_batch = (int)value;

@@ -139,7 +139,7 @@ struct Knobs {
   int bptt_streams = 1;          // > 1: the big-tile BPTT diagonals (primal and tangent) split into this many row
                                  // chunks on side streams (a chunk's rows depend on nothing else), so one
                                  // chunk's next diagonal fills the other's tail; weight gradients after the sweep
-  int fwd_streams = 1;           // the same for the big-tile forward diagonals (primal and tangent)
+  int fwd_streams = 0;           // the same for the big-tile forward diagonals (primal and tangent); 0 = auto
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -163,10 +163,10 @@ struct Knobs {
 #define SMAML_WGRAD_DEDUP_DEFAULT 1
 #endif
 #ifndef SMAML_BPTT_STREAMS_DEFAULT
-#define SMAML_BPTT_STREAMS_DEFAULT 1
+#define SMAML_BPTT_STREAMS_DEFAULT 2  // A/B (profiles/r05_ab_streams*.log): config 2 1653 -> 1618 ms, config-5 share 4453 -> 4308 ms
 #endif
 #ifndef SMAML_FWD_STREAMS_DEFAULT
-#define SMAML_FWD_STREAMS_DEFAULT 1
+#define SMAML_FWD_STREAMS_DEFAULT 0  // auto (api.cpp fwd_chunks): config-5 share 4308 -> 4202 ms; config 2 (not chunked) +25 ms
 #endif
 #ifndef SMAML_WGRAD_PAIR
 #define SMAML_WGRAD_PAIR 1
@@ -463,6 +463,9 @@ void launch_head_dh(hipStream_t s, const Dims& d, const Work& w, const float* th
 // streams are independent -- as long as EVERY diagonal is chunked the same way)
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
                           const ParamOff& po, int chunk = 0, int nch = 1);
+// the unchunked launch of diagonal e would run the big tiles (primal / tangent BPTT)
+bool bwd_wave_big(const Dims& d, const Work& w, const ParamOff& po, int e);
+bool bwd_dual_wave_big(const Dims& d, const Work& w, const ParamOff& po, int e);
 // kernels_small.hip: the small-grid (batch-1) forward / BPTT diagonal as one launch with the K
 // reduction split over the waves of a workgroup (used where the split-K pair would run)
 bool small_kw_ok(const Dims& d, const Work& w);

@@ -1567,6 +1567,13 @@ __global__ __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_cell_q(const float* GsA
 #define SMAML_BWD_CELL_Q 1  // split-K BPTT step's cell kernel over 4x the threads (0: k_lstm_bwd_cell)
 #endif
 
+bool bwd_wave_big(const Dims& d, const Work& w, const ParamOff& po, int e) {
+  BwdWave wv{};
+  const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
+  bwd_wave(d, w, po, e, ntm, false, wv);
+  return (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min;
+}
+
 void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta, int64_t tstride,
                           const ParamOff& po, int chunk, int nch) {
   const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;

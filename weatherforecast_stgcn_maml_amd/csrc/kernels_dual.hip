@@ -836,6 +836,13 @@ static void bwd_dual_grid(hipStream_t s, const Dims& d, const Work& w, const Bwd
   }
 }
 
+bool bwd_dual_wave_big(const Dims& d, const Work& w, const ParamOff& po, int e) {
+  BwdWave wv{};
+  const int ntm = (w.M + CfgBwdD::BM - 1) / CfgBwdD::BM, ntn = (d.H + CfgBwdD::BN - 1) / CfgBwdD::BN;
+  bwd_wave(d, w, po, e, ntm, true, wv);
+  return (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min;
+}
+
 void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int e, const float* theta,
                                const float* U, int64_t tstride, const ParamOff& po, int chunk, int nch) {
   BwdWave wv{};

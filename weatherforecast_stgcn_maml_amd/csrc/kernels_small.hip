@@ -13,7 +13,8 @@
 // are summed in K-range order (deterministic), and the workgroup runs the cell epilogue. The
 // epilogue's own operands (bias sums, c_{t-1}; gates, carry, head dh in the BPTT) are loaded before
 // the K loop, so their latency hides under it. The problem of a diagonal is the grid row (blockIdx.y).
-// Config 4: 1.03 -> 0.68 ms per sample-step with these kernels.
+// Config 4: 1.03 -> 0.63 ms per later-epoch sample-step with these kernels and the round-4 launch trims
+// (DESIGN.md section 8).
 //
 // Products: bf16x6 (gemm_core.h mfma_x6, f32-accurate). Forward B operand: the pre-split gate
 // images (launch_split_gate) read straight into fragments, or the f32 weights split in registers.
