@@ -279,7 +279,7 @@ int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* cou
  * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
  * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
  * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw, gcn_dedup,
- * xg_dedup, wgrad_dedup.
+ * xg_dedup, wgrad_dedup, f_compact.
  * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
  * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
@@ -340,7 +340,13 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  independent through the whole recurrence, so a chunk's next diagonal
  *                                  fills another's tail; bitwise equal to 1). Defaults: bptt_streams 2,
  *                                  fwd_streams 0 = auto (2 when a problem's gate launch fills at most
- *                                  two workgroups per CU, else 1). */
+ *                                  two workgroups per CU, else 1);
+ *   "f_compact":                   where every reader of a step's GCN features goes through the distinct
+ *                                  stream rows (xg_dedup forwards on the big tiles, wgrad_dedup
+ *                                  backwards), the GCN stores each distinct row once instead of to every
+ *                                  (sample, step) holding it (1, the default; bitwise equal to 0);
+ *   "wgrad_overlap":               with row chunks, layer l's weight gradient on the caller's stream as
+ *                                  soon as its BPTT is done (1) or after the sweep (0, the default). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

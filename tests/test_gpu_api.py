@@ -494,42 +494,48 @@ def test_stgcn_autograd_matches_oracle(d, p):
     assert rel(xg.grad.cpu(), xt.grad) < 1e-4
 
 
-@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams"])
+@pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams",
+                                  "f_compact", "f_compact_layers"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
     stored to every sample holding them; gcn_dedup_layers: the same on the per-layer GCN path,
     gcn_fused 0, as one pseudo-sample of distinct stream rows per task expanded into F; bptt_streams /
     fwd_streams: every BPTT / forward diagonal in two row chunks on side streams, always on the big tiles,
-    the weight gradients after the sweep) leave every
+    the weight gradients after the sweep; f_compact: the features of those steps stored once per distinct
+    stream row, read only through the layer-0 projection tables and the gathered dW_ih0 -- fused and per-layer
+    GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles) leave every
     row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
     kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
-    cfg = MamlConfig(inner_steps=2, batch=4, order=2)
+    compact = knob.startswith("f_compact")
+    cfg = MamlConfig(inner_steps=2, batch=8 if compact else 4, order=2)
     P = synth.init_params(47, d, gcn_bias_scale=0.1)
     Ptr, Pg, _ = split(P)
     ei = grid_edges(d)
-    feats = [synth.make_features(4700 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(3)]
+    feats = [synth.make_features(4700 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2 if compact else 3)]
     out = []
     for on in (1, 0):
         ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
         ml.set_tasks(feats)
         ml.ctx.set_option("bwdd_big_min", 0)
-        if knob == "gcn_dedup_layers":
+        if knob.endswith("_layers"):
             ml.ctx.set_option("gcn_fused", 0)
         if knob.endswith("_streams"):
             ml.ctx.set_option("bwd_big_min", 0)  # (chunked diagonals always run the big tiles: both arms do)
             ml.ctx.set_option(knob, 2 if on else 1)
         else:
-            ml.ctx.set_option("gcn_dedup" if knob.startswith("gcn_dedup") else knob, on)
+            ml.ctx.set_option(knob.removesuffix("_layers"), on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()
         vc = ml.ctx.variant_counts()
         assert vc["bwd_dual_big_kept"] > 0, vc
         if knob.startswith("gcn_dedup"):
             assert (vc["gcn_dedup"] > 0) == bool(on), vc
+        if compact:  # every step: K inner steps + the query; the sweep reads them from so_F
+            assert vc["f_compact"] == (cfg.inner_steps + 1 if on else 0), vc
         out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
         del ml
     for a, b in zip(out[0], out[1]):

@@ -234,7 +234,8 @@ struct smaml_ctx {
   int64_t vcount[NVAR] = {};
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
-           SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT};
+           SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
+           SMAML_F_COMPACT_DEFAULT};
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
@@ -295,6 +296,7 @@ struct smaml_ctx {
   // side streams of the row-chunked BPTT (knob bptt_streams) and their fork / join events
   hipStream_t cs[4] = {};
   hipEvent_t fork_ev = nullptr, join_ev[4] = {};
+  hipEvent_t lay_ev[MAX_LAYERS][4] = {};  // wgrad_overlap: layer l's BPTT done on chunk stream i
   // RCCL communicator (smaml_comm_init), opaque; created non-blocking when the library allows it
   void* comm = nullptr;
   int comm_nb = 0;
@@ -586,6 +588,8 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.lblocks = head_lblocks(c->d, c->w.M);
   c->w.F = c->F_main;
   c->w.primal_kept = 0;
+  c->w.consec = 0;
+  c->w.fcompact = 0;
   c->w.drop = Drop{};  // dropout only inside smaml_meta_step / smaml_adapt_steps (set_step_drop)
   c->w.vcount = c->vcount;
   c->w.kn = c->kn;
@@ -682,6 +686,16 @@ void time_wall(smaml_ctx* c, hipStream_t s, hipEvent_t a, int cat, double fl) {
   c->tm.recs.push_back({cat, a, b, fl});
 }
 
+// s waits for what the side streams have issued so far (layer l's events; the streams go on)
+int wait_streams_layer(smaml_ctx* c, hipStream_t s, int n, int l) {
+  for (int i = 0; i < n; ++i) {
+    if (!c->lay_ev[l][i]) HIP_TRY(hipEventCreateWithFlags(&c->lay_ev[l][i], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->lay_ev[l][i], c->cs[i]));
+    HIP_TRY(hipStreamWaitEvent(s, c->lay_ev[l][i], 0));
+  }
+  return SMAML_OK;
+}
+
 // s waits for everything issued on the side streams
 int join_streams(smaml_ctx* c, hipStream_t s, int n) {
   for (int i = 0; i < n; ++i) {
@@ -728,13 +742,31 @@ bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float*
   plan_wgrad(w, S, rows * 4 * d.H, 4 * d.H, w.F, TM * lo.cin, lo.cin, nullptr, 0, 0, rows, 0, grad, c->po.P, lo.wih, -1,
              -1, -1, false, false, p);
   p.ws = false;
-  p.gather = WgGather{w.M, d.N, d.T, FastDiv((uint32_t)d.N)};
+  p.gather = WgGather{w.M, d.N, d.T, FastDiv((uint32_t)d.N), w.fcompact};
   count_variant(w, V_WGRAD);
   count_variant(w, V_WGRAD_DEDUP);
   if (p.wide) count_variant(w, V_WGRAD_WIDE);
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * rows * 4 * d.H * lo.cin, launch_wgrad_gemm(s, p));
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
   return true;
+}
+
+// Whether a consecutive-window step's features may be stored compact (Work::fcompact, the distinct rows
+// only, XgDedup order): every reader of F must then take those rows -- the forwards' layer-0 gates through
+// the k_xg_dedup tables (every layer-0 diagonal on the big tiles; the tangent forward always reads them),
+// the backwards' dW_ih0 through the gathered form (not the grouped small-grid launch) -- with the
+// scratch for both tables reserved here, so neither reader can miss it later. Deterministic in the
+// step's state: the tangent sweep re-derives the flag of a step whose features it reads from so_F.
+bool f_compact_ok(smaml_ctx* c, bool consec) {
+  const Dims& d = c->d;
+  const Work& w = c->w;
+  const Knobs& kn = c->kn;
+  if (!consec || !kn.f_compact || !kn.gcn_dedup || !kn.xg_dedup || !kn.wgrad_dedup || w.B <= 1 || w.drop.gcn() ||
+      w.drop.lstm() || (int64_t)w.Z * w.M <= kn.wgrad_group_max_rows)
+    return false;
+  for (int diag = 0; diag < d.T; ++diag)
+    if (!fwd_wave_big(d, w, c->po, diag)) return false;
+  return xgd_scratch(c, 2 * xg_dedup_rows(w.B, d.T, d.N) * 4 * d.H * w.Z) != nullptr;
 }
 
 // GCN x4 (no_grad, F2): sample windows -> w.F [Z][T][M][Hc]. With the fused kernel (Hc = 256): the
@@ -748,6 +780,8 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, const flo
   const bool consec = first_tab != nullptr;
   const Dims& d = c->d;
   Work& w = c->w;
+  w.fcompact = f_compact_ok(c, consec) ? 1 : 0;
+  if (w.fcompact) count_variant(w, V_F_COMPACT);
   const int rps = d.T * d.N;
   const int zb = w.Z * w.B;
   const float* src = nullptr;
@@ -765,7 +799,7 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, const flo
     if (dedup) count_variant(w, V_GCN_DEDUP);
     const double rows1 = dedup ? (double)w.Z * (w.B + d.T - 2) * d.N : (double)zb * (d.T - 1) * d.N;
     TIMED(c, s, C_GCN, 2.0 * rows1 * d.Hc * (d.Cin0 + 3.0 * d.Hc),
-          launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop, dedup));
+          launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop, dedup, w.fcompact));
     for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks, masks indexed as rows of T*N-row samples
       const bool last = k == 3;
       float* dst = last ? w.F : bufs[k & 1];
@@ -789,7 +823,7 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, const flo
                              rpsC, 0, nullptr));
       src = dst;
     }
-    TIMED(c, s, C_GCN, 0, launch_gcn_expand(s, d, w.Z, w.B, src, w.F));
+    TIMED(c, s, C_GCN, 0, launch_gcn_expand(s, d, w.Z, w.B, src, w.F, w.fcompact));
     src = nullptr;
     for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks with the ELL gather, as on the fused path
       const bool last = k == 3;
@@ -936,6 +970,7 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
   bool xgd_ok = consec;
   for (int diag = 0; xgd_ok && diag < d.T; ++diag) xgd_ok = fwd_wave_big(d, w, c->po, diag);
   const bool use_xgd = xgd_ok && prep_xg_dedup(c, s, true, theta, nullptr, tstride, true);
+  if (w.fcompact && !use_xgd) return fail(SMAML_ESTATE, "compact features without the layer-0 projection table");
   // Batch-1 sizes (the small-grid steps): layer 0's input projection F . W_ih0^T does not depend on the
   // recurrence, so it runs for all T steps as one throughput-bound GEMM before the wavefront and the
   // layer-0 steps' latency-bound K loops cover only the recurrent segment (kernels_small.hip).
@@ -1089,13 +1124,19 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       TIMED(c, s, C_BWD, fl, launch_lstm_bwd_wave(s, d, w, e, theta, tstride, po));
     }
     const int l = d.L - 1 - (e - (d.T - 1));
-    if (e < d.T - 1 || l < 0 || nch > 1) continue;
-    layer_wgrad(l);
+    if (e < d.T - 1 || l < 0) continue;
+    if (nch > 1 && c->kn.wgrad_overlap) {  // layer l's gradient on s beside the chunks' next diagonals
+      TRY(wait_streams_layer(c, s, nch, l));
+      layer_wgrad(l);
+    } else if (nch <= 1) {
+      layer_wgrad(l);
+    }
   }
   if (nch > 1) {
     TRY(join_streams(c, s, nch));
     time_wall(c, s, wa, C_BWD_WALL, wfl);
-    for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
+    if (!c->kn.wgrad_overlap)
+      for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
   HIP_TRY(hipGetLastError());
@@ -1108,10 +1149,12 @@ int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const floa
   const Dims& d = c->d;
   Work& w = c->w;
   if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, first_tab));
+  else w.fcompact = f_compact_ok(c, first_tab != nullptr) ? 1 : 0;  // (as when so_F's slot was written)
   w.consec = first_tab != nullptr;
   TRY(prep_gate_images(c, s, theta, tstride, U));
   // layer 0's tangent projection F U_ih0^T (and, unless the primal is kept, F W_ih0^T) once per stream row
   const bool use_xgd = prep_xg_dedup(c, s, first_tab != nullptr, theta, U, tstride, !w.primal_kept);
+  if (w.fcompact && !use_xgd) return fail(SMAML_ESTATE, "compact features without the layer-0 projection tables");
   const int nch = fwd_chunks(c);  // (row chunks on side streams)
   hipEvent_t wa = nullptr;
   if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
@@ -1208,13 +1251,19 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
       TIMED(c, s, C_BWD_DUAL, fl, launch_lstm_bwd_dual_wave(s, d, w, e, theta, U, tstride, po));
     }
     const int l = d.L - 1 - (e - (d.T - 1));
-    if (e < d.T - 1 || l < 0 || nch > 1) continue;
-    layer_wgrad(l);
+    if (e < d.T - 1 || l < 0) continue;
+    if (nch > 1 && c->kn.wgrad_overlap) {
+      TRY(wait_streams_layer(c, s, nch, l));
+      layer_wgrad(l);
+    } else if (nch <= 1) {
+      layer_wgrad(l);
+    }
   }
   if (nch > 1) {
     TRY(join_streams(c, s, nch));
     time_wall(c, s, wa, C_BWD_DUAL_WALL, wfl);
-    for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
+    if (!c->kn.wgrad_overlap)
+      for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
@@ -1394,6 +1443,9 @@ int smaml_destroy(smaml_ctx* c) {
     if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
   }
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  for (auto& row : c->lay_ev)
+    for (auto& e : row)
+      if (e) (void)hipEventDestroy(e);
   if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
@@ -1960,6 +2012,10 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_dedup = (int)value;
   } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
     c->kn.bptt_streams = (int)value;
+  } else if (k == "f_compact" && (value == 0 || value == 1)) {
+    c->kn.f_compact = (int)value;
+  } else if (k == "wgrad_overlap" && (value == 0 || value == 1)) {
+    c->kn.wgrad_overlap = (int)value;
   } else if (k == "fwd_streams" && value >= 0 && value <= 4) {
     c->kn.fwd_streams = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {

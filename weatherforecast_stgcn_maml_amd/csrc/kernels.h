@@ -101,6 +101,7 @@ enum Variant {
   V_GCN_DEDUP,       // k_gcn_mlp once per distinct stream row of consecutive windows
   V_XG_DEDUP,        // k_xg_dedup: layer 0's input projection once per distinct stream row (big-tile forward)
   V_WGRAD_DEDUP,     // layer 0's input-weight gradient over distinct stream rows (k_dg_rowsum + gathered k_wgrad)
+  V_F_COMPACT,       // GCN features stored once per distinct stream row (Work::fcompact)
   NVAR
 };
 
@@ -140,6 +141,10 @@ struct Knobs {
                                  // chunks on side streams (a chunk's rows depend on nothing else), so one
                                  // chunk's next diagonal fills the other's tail; weight gradients after the sweep
   int fwd_streams = 0;           // the same for the big-tile forward diagonals (primal and tangent); 0 = auto
+  int wgrad_overlap = 0;         // 1 (with row chunks): layer l's weight gradient on the caller's stream as soon as
+                                 // its BPTT is done, beside the chunks' remaining diagonals
+  int f_compact = 0;             // 1: where every reader of a step's features goes through the distinct stream rows
+                                 // (xg_dedup forwards, wgrad_dedup backwards), the GCN stores only those rows
 };
 #ifndef SMAML_GATE_IMG
 #define SMAML_GATE_IMG 1
@@ -164,6 +169,9 @@ struct Knobs {
 #endif
 #ifndef SMAML_BPTT_STREAMS_DEFAULT
 #define SMAML_BPTT_STREAMS_DEFAULT 2  // A/B (profiles/r05_ab_streams*.log): config 2 1653 -> 1618 ms, config-5 share 4453 -> 4308 ms
+#endif
+#ifndef SMAML_F_COMPACT_DEFAULT
+#define SMAML_F_COMPACT_DEFAULT 1
 #endif
 #ifndef SMAML_FWD_STREAMS_DEFAULT
 #define SMAML_FWD_STREAMS_DEFAULT 0  // auto (api.cpp fwd_chunks): config-5 share 4308 -> 4202 ms; config 2 (not chunked) +25 ms
@@ -230,6 +238,8 @@ struct Work {
   const float* xg_src = nullptr;   // the parameter vector xg was formed with
   XgDedup xgd{};                   // big-tile forward: layer 0's projection once per distinct stream row
   int consec = 0;                  // this step's tasks each read B consecutive windows (set by the forward)
+  int fcompact = 0;                // F holds only the distinct rows of those windows, in XgDedup's row order
+                                   // (rows [0, (2B + T - 2) N) of each task's slab): read through XgDedup only
   GateImgs gimg{};         // pre-split images of the weights the gate GEMMs read (launch_split_gate)
   const float* gimg_src = nullptr; // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src = nullptr;// ... and gimg.u (the sweep's tangent direction)
@@ -413,21 +423,25 @@ struct GcnMlpArgs {
   int64_t R1 = 0, M = 0;               // rows t >= 1 over all samples; B*N
   FastDiv rows_div{}, b_div{}, n_div{};
   int rows1 = 0, N = 0, T = 0, B = 0, cin0 = 0;
+  int compact = 0;                     // dedup: store each distinct row ONCE, at its compact row (XgDedup order)
   int dedup = 0;                       // 1: every task's B windows are consecutive; rows1 = (B + T - 2) * N distinct
                              // time steps per task, each row written to every (sample, t >= 1) holding it
   Drop dr{};
 };
 bool gcn_mlp_supported(const Dims& d);
-void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F);
+// compact: only the distinct rows, F[z][M + (s - 1) N + n] = C[z][s][n] for s >= 1 (XgDedup order)
+void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F, bool compact = false);
 int64_t gcn_wimg_bytes(const Dims& d);
 void launch_gcn_wsplit(hipStream_t s, const Dims& d, const float* gcn, const GcnWOff& wo, char* img);
 // dedup: the B windows of every task start at consecutive stream rows (xtab[z*B + b] = xtab[z*B] + b
 // time steps) and there is no GCN dropout -- see k_gcn_mlp
 void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
-                    const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup = false);
+                    const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup = false,
+                    bool compact = false);
 // out[z] = layer-0 input projection of every distinct stream row of task z's consecutive windows
 // (XgDedup layout) with the gate weights W_ih0 of `params` (theta or the tangent direction U); the
-// weights come from the pre-split images `img` when given (w.gimg.th / .u), else from `params`
+// weights come from the pre-split images `img` when given (w.gimg.th / .u), else from `params`; F is
+// read in XgDedup order when w.fcompact, else at each stream row's (window, step) slot
 void launch_xg_dedup(hipStream_t s, const Dims& d, const Work& w, const float* params, int64_t tstride,
                      const ParamOff& po, const char* img, int64_t img_tstride, int64_t img_off, float* out);
 // chunk / nch: row chunks as in launch_lstm_bwd_wave (nch > 1: every diagonal on the big tiles)
@@ -489,6 +503,7 @@ void launch_wgrad(hipStream_t s, const Dims& d, const Work& w, const float* A, i
 struct WgGather {
   int M = 0, N = 0, T = 0;
   FastDiv ndiv{};
+  int compact = 0;  // F is compact (Work::fcompact): row k is F's row k
 };
 // launch_wgrad split in its two launches (the GEMM into split-K partial slabs, then the
 // fixed-order reduce into the flat gradient), so each can be timed on its own.

@@ -472,10 +472,11 @@ struct XgRowsA {
   const float* F;  // [T][M][cin] (one task)
   int M, N, T, cin, rows;
   FastDiv ndiv;
+  int compact;     // F in XgDedup order (Work::fcompact): row r is F's row r
   __device__ __forceinline__ float4 operator()(int r, int k) const {
     r = min(r, rows - 1);
     int64_t row = r;
-    if (r >= M) {
+    if (r >= M && !compact) {
       const int rr = r - M;
       const int s1 = (int)ndiv.div((uint32_t)rr);
       const int s = s1 + 1, t = min(s, T - 1);
@@ -524,7 +525,7 @@ void launch_xg_dedup(hipStream_t s, const Dims& d, const Work& w, const float* p
   const int ngrp = (d.H + 32 * CfgGate::WAVES_N - 1) / (32 * CfgGate::WAVES_N);
   dim3 grid(gate_blocks(ntm, ngrp), 1, w.Z);
   const int cin = po.lay[0].cin;
-  const XgRowsA a{nullptr, w.M, d.N, d.T, cin, rows, FastDiv((uint32_t)d.N)};
+  const XgRowsA a{nullptr, w.M, d.N, d.T, cin, rows, FastDiv((uint32_t)d.N), w.fcompact};
   const int64_t fz = (int64_t)d.T * w.M * cin;
   count_variant(w, V_XG_DEDUP);
   if (img) {
@@ -1844,7 +1845,13 @@ __device__ __forceinline__ void wgrad_glds_loop(const float* A, int64_t K, const
 #ifndef SMAML_WGRAD_WIDE
 #define SMAML_WGRAD_WIDE 1
 #endif
-using CfgTW = GemmCfg<256, 256, 4, 2, false, false, SMAML_TN_BK, SMAML_X6_WGRAD, SMAML_TN_NST, false>;
+#ifndef SMAML_TW_BN
+#define SMAML_TW_BN 256  // (A/B arm: 128 with SMAML_TW_WN 1 = 256 x 128 tiles of 4 waves, two workgroups per CU)
+#endif
+#ifndef SMAML_TW_WN
+#define SMAML_TW_WN 2
+#endif
+using CfgTW = GemmCfg<256, SMAML_TW_BN, 4, SMAML_TW_WN, false, false, SMAML_TN_BK, SMAML_X6_WGRAD, SMAML_TN_NST, false>;
 template <class C>
 constexpr int wgrad_smem_floats() {
   return std::is_same<C, CfgTN>::value ? WG_SMEM : C::SMEM_FLOATS;
@@ -1878,10 +1885,11 @@ struct WgBGather {
   WgB b;
   int M, N, T;
   FastDiv ndiv;
+  int compact;
   __device__ __forceinline__ float4 operator()(int64_t k, int j) const {
     if (k >= b.K || j >= b.c1) return f4zero();
     int64_t row = k;
-    if (k >= M) {
+    if (k >= M && !compact) {
       const int rr = (int)(k - M);
       const int s1 = (int)ndiv.div((uint32_t)rr);
       const int s = s1 + 1, t = min(s, T - 1);
@@ -1923,7 +1931,7 @@ __device__ __forceinline__ void wgrad_block(int L, const float* __restrict__ A, 
   // k indices exceed int range only in the loaders (int64 there); the mainloop
   // passes kbeg + kt*BK as int, so K per task must stay below 2^31 (T*M*... ok).
   if constexpr (GATHER) {
-    const WgBGather bg{b, ga.M, ga.N, ga.T, ga.ndiv};
+    const WgBGather bg{b, ga.M, ga.N, ga.T, ga.ndiv, ga.compact};
     if (tn == 0 && with_bias) {
       wgrad_mainloop<C>(la, bg, m0, n0, (int)kbeg, (int)kend, acc, smem, hook);
     } else {
@@ -2334,13 +2342,13 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
                     Mrows % CfgTW::BM == 0;
   const int BMc = ws ? CfgWS::BM : wide ? CfgTW::BM : CfgTN::BM, BNc = ws ? CfgWS::BN : wide ? CfgTW::BN : CfgTN::BN;
 
-  static_assert(CfgTW::NTH == CfgTN::NTH && CfgTW::BK == CfgTN::BK, "one split-K plan for both tiles");
+  static_assert(CfgTW::BK == CfgTN::BK, "one split-K K-tile for both tiles");
   const int ntm = (Mrows + BMc - 1) / BMc;
   const int ntn = (ncols + BNc - 1) / BNc;
   const int64_t ktiles = (K + CfgTN::BK - 1) / CfgTN::BK;
-  // aim for ~2048 4-wave workgroups' worth of waves, at least 8 K-tiles per split, bounded by
-  // the slab buffer
-  int64_t nsplit = (SMAML_WGRAD_THREADS / CfgTN::NTH) / ((int64_t)ntm * ntn * w.Z);
+  // aim for SMAML_WGRAD_THREADS threads in all, at least 8 K-tiles per split, bounded by the slab buffer
+  const int nth = wide ? CfgTW::NTH : CfgTN::NTH;
+  int64_t nsplit = (SMAML_WGRAD_THREADS / nth) / ((int64_t)ntm * ntn * w.Z);
   if (nsplit < 1) nsplit = 1;
   if (nsplit > ktiles / 8) nsplit = ktiles / 8 > 0 ? ktiles / 8 : 1;
   const int64_t per_split = (int64_t)w.Z * Mrows * ldp;

@@ -114,6 +114,9 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
   const int t_lo = a.dedup ? max(1, t - (a.B - 1)) : t, t_hi = a.dedup ? min(a.T - 1, t) : t;
   const int boff = s + t;
   float* frow = a.F + (((int64_t)z * a.T) * a.M + n) * HC;
+  if (a.compact) {  // once, at compact row M + (t - 1) N + n (t = the stream row here): tt = t_lo only
+    frow = a.F + (((int64_t)z * a.T) * a.M + a.M + (int64_t)(t - 1) * a.N + n) * HC;
+  }
   uint64_t didx = 0;
   if (a.dr.gcn()) didx = (((uint64_t)a.dr.task_id[z] * a.B + s) * (uint64_t)(a.T * a.N) + (uint64_t)q) * HC;
 
@@ -212,8 +215,8 @@ __global__ __launch_bounds__(64 * GM_WAVES) void k_gcn_mlp(GcnMlpArgs a) {
     epilogue(layer);
   }
   if (valid) {
-    for (int tt = t_lo; tt <= t_hi; ++tt) {
-      float* fr = frow + ((int64_t)tt * a.M + (int64_t)(boff - tt) * a.N) * HC;
+    for (int tt = t_lo; tt <= (a.compact ? t_lo : t_hi); ++tt) {
+      float* fr = a.compact ? frow : frow + ((int64_t)tt * a.M + (int64_t)(boff - tt) * a.N) * HC;
 #pragma unroll
       for (int ci = 0; ci < NT; ++ci)
 #pragma unroll
@@ -244,8 +247,24 @@ __global__ void k_gcn_expand(const float* __restrict__ C, float* __restrict__ F,
     dst[i] = src[i];
 }
 
-void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F) {
+// compact: per task the distinct rows s >= 1 only, one contiguous block: F[z][M + (s - 1) N ..] = C[z][s N ..]
+__global__ void k_gcn_compact(const float* __restrict__ C, float* __restrict__ F, int B, int T, int64_t blk) {
+  const int z = blockIdx.y;
+  const int64_t n4 = (int64_t)(B + T - 2) * blk / 4;
+  const float4* src = reinterpret_cast<const float4*>(C + ((int64_t)z * (B + T - 1) + 1) * blk);
+  float4* dst = reinterpret_cast<float4*>(F + ((int64_t)z * T * B + B) * blk);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* C, float* F, bool compact) {
   const int64_t blk = (int64_t)d.N * d.Hc;  // floats per (task, t, window) block; Hc % 4 == 0
+  if (compact) {
+    const int64_t n4 = (int64_t)(B + d.T - 2) * blk / 4;
+    const unsigned gx = (unsigned)std::min<int64_t>((n4 + 255) / 256, 1024);
+    k_gcn_compact<<<dim3(gx, (unsigned)Z), 256, 0, s>>>(C, F, B, d.T, blk);
+    return;
+  }
   const unsigned gx = (unsigned)std::min<int64_t>((blk / 4 + 255) / 256, 64);
   k_gcn_expand<<<dim3(gx, (unsigned)(Z * B * (d.T - 1))), 256, 0, s>>>(C, F, B, d.T, blk);
 }
@@ -253,7 +272,7 @@ void launch_gcn_expand(hipStream_t s, const Dims& d, int Z, int B, const float* 
 bool gcn_mlp_supported(const Dims& d) { return d.Hc == 256 && d.Cin0 <= 32 && d.Cin0 % 4 == 0 && d.T > 1; }
 
 void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* const* xtab, const float* gcn,
-                    const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup) {
+                    const GcnWOff& wo, const char* img, float* F, const Drop* drop, bool dedup, bool compact) {
   GcnMlpArgs a{};
   a.xtab = xtab;
   a.gcn = gcn;
@@ -261,6 +280,7 @@ void launch_gcn_mlp(hipStream_t s, const Dims& d, int Zb, int B, const float* co
   a.wimg = img;
   a.F = F;
   a.dedup = dedup && B > 1 && !(drop && drop->gcn()) ? 1 : 0;
+  a.compact = a.dedup && compact ? 1 : 0;
   a.rows1 = (a.dedup ? B + d.T - 2 : d.T - 1) * d.N;
   a.R1 = (int64_t)(a.dedup ? Zb / B : Zb) * a.rows1;
   a.rows_div = FastDiv((uint32_t)a.rows1);
