@@ -279,7 +279,7 @@ int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* cou
  * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
  * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
  * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw, gcn_dedup,
- * xg_dedup, wgrad_dedup, f_compact.
+ * xg_dedup, wgrad_dedup, f_compact, bwd_push, bwd_dual_push.
  * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
  * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
@@ -345,6 +345,12 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  stream rows (xg_dedup forwards on the big tiles, wgrad_dedup
  *                                  backwards), the GCN stores each distinct row once instead of to every
  *                                  (sample, step) holding it (1, the default; bitwise equal to 0);
+ *   "bptt_push":                   big-tile BPTT sweeps without LSTM dropout (primal, and the tangent sweep
+ *                                  of a kept step) in the producer-side form: each step runs its cell
+ *                                  backward from the dh partial sums its producers left, then forms its
+ *                                  consumers' partial sums dG . W_hh and dG . W_ih, so every dG is read
+ *                                  once as a GEMM operand instead of twice (1; 0 = the consumer-side
+ *                                  form; equal up to f32 rounding: dh = Pup + Prec adds once more);
  *   "wgrad_overlap":               with row chunks, layer l's weight gradient on the caller's stream as
  *                                  soon as its BPTT is done (1) or after the sweep (0, the default). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);

@@ -235,7 +235,7 @@ struct smaml_ctx {
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
            SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
-           SMAML_F_COMPACT_DEFAULT};
+           SMAML_BPTT_PUSH_DEFAULT, SMAML_F_COMPACT_DEFAULT};
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
@@ -262,6 +262,8 @@ struct smaml_ctx {
   int64_t xg_cap = 0;
   float* xgd_buf = nullptr;   // big-tile forward: layer 0's projection per distinct stream row (prep_xg_dedup)
   int64_t xgd_cap = 0;
+  float* push_buf = nullptr;  // push BPTT partial sums: primal [3][L][Z][M][H], then tangent (push_partials)
+  int64_t push_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
   // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
   unsigned* bar = nullptr;
@@ -590,6 +592,7 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.primal_kept = 0;
   c->w.consec = 0;
   c->w.fcompact = 0;
+  c->w.push = 0;
   c->w.drop = Drop{};  // dropout only inside smaml_meta_step / smaml_adapt_steps (set_step_drop)
   c->w.vcount = c->vcount;
   c->w.kn = c->kn;
@@ -718,6 +721,34 @@ float* xgd_scratch(smaml_ctx* c, int64_t floats) {
     c->xgd_cap = floats;
   }
   return c->xgd_buf;
+}
+
+// Whether this BPTT sweep runs in the push form (knob bptt_push, kernels.hip k_lstm_bwd_push): every
+// diagonal on the big tiles (row chunks force them; else each diagonal's own size), no LSTM dropout,
+// the tangent sweep only for a kept step; points the Work at the partial-sum buffers (allocated here,
+// both sets at once so the tangent sweep never reallocates under the primal's; no room: pull form).
+bool push_sweep(smaml_ctx* c, bool dual, int nch) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  if (!c->kn.bptt_push || w.drop.lstm() || (dual && !w.primal_kept)) return false;
+  for (int e = 0; nch <= 1 && e < d.T + d.L - 1; ++e)
+    if (!(dual ? bwd_dual_wave_big(d, w, c->po, e) : bwd_wave_big(d, w, c->po, e))) return false;
+  const int64_t set = 3ll * d.L * w.Z * w.M * d.H;
+  if (2 * set > c->push_cap) {
+    if (c->push_buf) (void)hipFree(c->push_buf);
+    c->push_buf = nullptr;
+    c->push_cap = 0;
+    if (hipMalloc((void**)&c->push_buf, 2 * set * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    c->push_cap = 2 * set;
+  }
+  const int64_t lz = (int64_t)d.L * w.Z * w.M * d.H;
+  float* b = c->push_buf + (dual ? set : 0);
+  (dual ? w.RPrec : w.Prec) = b;
+  (dual ? w.RPup : w.Pup) = b + lz;
+  return true;
 }
 
 // Whether this step's layer-0 input-weight gradient runs over distinct stream rows (wgrad_dedup).
@@ -1109,6 +1140,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   // weight gradients after the sweep on the caller's stream
   // (chunked only where a full diagonal runs the big tiles anyway: tile-forcing knobs keep their meaning)
   const int nch = grouped || !bwd_wave_big(d, w, po, std::min(d.L, d.T) - 1) ? 1 : c->kn.bptt_streams;
+  w.push = push_sweep(c, false, nch) ? 1 : 0;
   hipEvent_t wa = nullptr;
   if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
@@ -1139,6 +1171,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
   if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
+  w.push = 0;
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1235,6 +1268,7 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows || !bwd_dual_wave_big(d, w, po, std::min(d.L, d.T) - 1)
                       ? 1
                       : c->kn.bptt_streams;
+  w.push = push_sweep(c, true, nch) ? 1 : 0;
   hipEvent_t wa = nullptr;
   if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
@@ -1265,6 +1299,7 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     if (!c->kn.wgrad_overlap)
       for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   }
+  w.push = 0;
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1437,6 +1472,7 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->bimg_buf) (void)hipFree(c->bimg_buf);
   if (c->xg_buf) (void)hipFree(c->xg_buf);
   if (c->xgd_buf) (void)hipFree(c->xgd_buf);
+  if (c->push_buf) (void)hipFree(c->push_buf);
   if (c->bar) (void)hipFree(c->bar);
   for (int i = 0; i < 4; ++i) {
     if (c->cs[i]) (void)hipStreamDestroy(c->cs[i]);
@@ -2012,6 +2048,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_dedup = (int)value;
   } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
     c->kn.bptt_streams = (int)value;
+  } else if (k == "bptt_push" && (value == 0 || value == 1)) {
+    c->kn.bptt_push = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
     c->kn.f_compact = (int)value;
   } else if (k == "wgrad_overlap" && (value == 0 || value == 1)) {

@@ -205,6 +205,22 @@ __device__ __forceinline__ int acc_col(int j) {
   return wn * (C::WTN * 32) + j * 32 + (lane & 31);
 }
 
+// acc -> P[m][j] (rows m0.., columns n0..; [M][H] rows)
+template <class C>
+__device__ __forceinline__ void store_acc_rows(const Acc<C>& acc, float* P, int m0, int n0, int M, int H) {
+#pragma unroll
+  for (int i = 0; i < C::WTM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < C::WTN; ++jj) {
+      const int j = n0 + acc_col<C>(jj);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + acc_row<C>(i, r);
+        if (m < M && j < H) P[(int64_t)m * H + j] = acc.v[i][jj][r];
+      }
+    }
+}
+
 // Optional hooks: operator() runs once per K-tile on the staged A tile; afrag(i, a) sees every
 // A fragment this lane feeds to the MFMAs (4 k-steps of tile row i), e.g. for column sums
 // of A (bias gradients) kept in registers instead of re-read from LDS.

@@ -102,6 +102,8 @@ enum Variant {
   V_XG_DEDUP,        // k_xg_dedup: layer 0's input projection once per distinct stream row (big-tile forward)
   V_WGRAD_DEDUP,     // layer 0's input-weight gradient over distinct stream rows (k_dg_rowsum + gathered k_wgrad)
   V_F_COMPACT,       // GCN features stored once per distinct stream row (Work::fcompact)
+  V_BWD_PUSH,        // k_lstm_bwd_push (push BPTT, big tiles)
+  V_BWDD_PUSH,       // k_lstm_bwd_dual_push (push tangent BPTT of a kept step, big tiles)
   NVAR
 };
 
@@ -143,6 +145,10 @@ struct Knobs {
   int fwd_streams = 0;           // the same for the big-tile forward diagonals (primal and tangent); 0 = auto
   int wgrad_overlap = 0;         // 1 (with row chunks): layer l's weight gradient on the caller's stream as soon as
                                  // its BPTT is done, beside the chunks' remaining diagonals
+  int bptt_push = 0;             // 1: big-tile BPTT sweeps (primal, and the tangent of kept steps) as producer-side
+                                 // steps: cell backward first, from the dh partial sums its producers left, then
+                                 // dG . W_hh and dG . W_ih for the two consumers (each dG read once as a GEMM
+                                 // operand instead of twice)
   int f_compact = 0;             // 1: where every reader of a step's features goes through the distinct stream rows
                                  // (xg_dedup forwards, wgrad_dedup backwards), the GCN stores only those rows
 };
@@ -169,6 +175,9 @@ struct Knobs {
 #endif
 #ifndef SMAML_BPTT_STREAMS_DEFAULT
 #define SMAML_BPTT_STREAMS_DEFAULT 2  // A/B (profiles/r05_ab_streams*.log): config 2 1653 -> 1618 ms, config-5 share 4453 -> 4308 ms
+#endif
+#ifndef SMAML_BPTT_PUSH_DEFAULT
+#define SMAML_BPTT_PUSH_DEFAULT 0
 #endif
 #ifndef SMAML_F_COMPACT_DEFAULT
 #define SMAML_F_COMPACT_DEFAULT 1
@@ -267,6 +276,12 @@ struct Work {
   // dropout (zero thresholds: off) and the masked head inputs drop(h_T), drop(R h_T) [Z][M][H]
   Drop drop{};
   float *hTd = nullptr, *RhTd = nullptr;
+  // push BPTT (knob bptt_push, BptPush below): this sweep's steps leave dh partial sums for their
+  // consumers instead of having them re-read dG; set per sweep by the caller
+  int push = 0;
+  float *Prec = nullptr, *Pup = nullptr;     // [L][Z][M][H] dG_t . W_hh(l) for (l, t-1); [2][L][Z][M][H]
+                                             // dG_t . W_ih(l) for (l-1, t), by the parity of t
+  float *RPrec = nullptr, *RPup = nullptr;   // the tangent sweep's R(dh) partial sums, same layouts
 };
 
 inline void count_variant(const Work& w, Variant v) {

@@ -1432,6 +1432,120 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
     bwd_cell<H, CfgNN, false>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
 }
 
+// ---- push BPTT (knob bptt_push) ---------------------------------------------------------------
+// The pull step above reads dG(l+1, t) and dG(l, t+1) as GEMM operands, so every dG is read twice
+// from HBM (once by each consumer) besides the weight gradient's read. The push step inverts it: step
+// (l, t) first runs its cell backward from the dh partial sums its two producers left,
+//   dh(l, t) = Pup(l, t) + Prec(l, t) [+ dh_T of the head at the top layer's last step],
+// writes dG(l, t), and then forms its consumers' partial sums from that dG tile (re-read from the
+// L2 it was just written through):
+//   Prec(l, t-1) = dG(l, t) . W_hh(l),   Pup(l-1, t) = dG(l, t) . W_ih(l)   ([M][H] each).
+// Same products, same diagonal order; the sum dh = Pup + Prec rounds once more than the fused K loop
+// (not bitwise equal to the pull step). Buffers (Work::Prec / Pup): Prec[l] is read and then written
+// by the same workgroup (the row tile of layer l's one problem per diagonal); Pup by the parity of t, so
+// a diagonal's writers (l + 1, t - 1) and readers (l, t) of layer l's slot never share one.
+#ifndef SMAML_BWD_PUSH_WPE
+#define SMAML_BWD_PUSH_WPE 3  // 3 workgroups of 4 waves per CU (<= 168 registers; 2 without the bound)
+#endif
+template <int H, class C, bool CHECK>
+__device__ __forceinline__ void bwd_cell_push_(const float* Gz, float* dGz, float* __restrict__ dhz,
+                                               const float* __restrict__ Cz, const float* __restrict__ hd,
+                                               const float* __restrict__ pu, const float* __restrict__ pr,
+                                               float* __restrict__ dcz, int m0, int n0, int t, int T, int M) {
+  constexpr int G4 = 4 * H;
+  constexpr int GPR = C::BN / 4;
+  constexpr int NIT = C::BM * GPR / C::NTH;
+  static_assert(NIT * C::NTH == C::BM * GPR, "epilogue items");
+  const bool first = (t == T - 1), past = t > 0;
+  const int64_t pM = past ? (int64_t)M * H : 0;
+  const int64_t tM = (int64_t)t * M;
+#pragma unroll 1
+  for (int k = 0; k < NIT; ++k) {
+    const int item = (int)threadIdx.x + C::NTH * k;
+    const int r = item / GPR;
+    int m = m0 + r, j = n0 + 4 * (item % GPR);
+    const bool ok = !CHECK || (m < M && j < H);
+    if (CHECK) {  // out-of-range items read a valid element (their results are not stored)
+      m = min(m, M - 1);
+      j = min(j, H - 4);
+    }
+    const int64_t row = tM + m, oc = (int64_t)m * H + j;
+    const float* gp = Gz + row * G4 + j;
+    float4 g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = ld4(gp + q * H);
+    const float4 cp = sel4(past, ld4(Cz + row * H - pM + j)), dc = sel4(!first, ld4(dcz + oc));
+    float4 dh = f4zero();
+    if (pu) dh = ld4(pu + oc);
+    if (pr) dh = add4(dh, ld4(pr + oc));
+    if (hd) dh = add4(dh, ld4(hd + oc));
+    if (!ok) continue;
+    float4 o[4], odc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gi = f4get(g[0], e), gf = f4get(g[1], e), gg = f4get(g[2], e), go = f4get(g[3], e);
+      const float d = f4get(dh, e);
+      const float tc = tanhf_(lstm_cell_c(gi, gf, gg, f4get(cp, e)));
+      const float dct = f4get(dc, e) + d * go * (1.f - tc * tc);
+      f4set(o[0], e, dct * gg * gi * (1.f - gi));
+      f4set(o[1], e, dct * f4get(cp, e) * gf * (1.f - gf));
+      f4set(o[2], e, dct * gi * (1.f - gg * gg));
+      f4set(o[3], e, d * tc * go * (1.f - go));
+      f4set(odc, e, dct * gf);
+    }
+    float* dp = dGz + row * G4 + j;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st4(dp + q * H, o[q]);
+    st4(dcz + oc, odc);
+    if (dhz) st4(dhz + row * H + j, dh);
+  }
+}
+
+template <int H, class C>
+__global__ __attribute__((amdgpu_waves_per_eu(SMAML_BWD_PUSH_WPE))) __launch_bounds__(C::NTH) void k_lstm_bwd_push(
+    const float* GsAll, float* dGAll, float* __restrict__ dhAll, const float* __restrict__ CsAll,
+    const float* __restrict__ dHhead, float* __restrict__ dcAll, float* Prec, float* Pup, int64_t lsz,
+    const float* __restrict__ theta, int64_t tstride, BwdWave wv, int L, int T, int M) {
+  __shared__ float smem[epi_smem_floats<C>()];
+  constexpr int G4 = 4 * H;
+  const Blk bk = xcd_block();
+  int mb;
+  const int p = bwd_block(wv, bk.x, mb);
+  mb += wv.tm0;
+  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
+  const LayerOff lo = wave_sel(wv.lo, p);
+  const int z = bk.z, Z = (int)gridDim.z;
+  const int m0 = mb * C::BM, n0 = bk.y * C::BN;
+  const int64_t slab = (int64_t)z * T * M, MH = (int64_t)M * H;
+  const float* th = theta + (int64_t)z * tstride;
+  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;
+  float* dhz = dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr;
+  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
+  float* dcz = dcAll + ((int64_t)l * Z + z) * MH;
+  float* prec = Prec + ((int64_t)l * Z + z) * MH;
+  const float* pu = l + 1 < L ? Pup + ((int64_t)((t & 1) * L + l) * Z + z) * MH : nullptr;
+  const float* pr = t + 1 < T ? prec : nullptr;
+  const float* hd = (l == L - 1 && t == T - 1) ? dHhead + (int64_t)z * MH : nullptr;
+  if (m0 + C::BM <= M && n0 + C::BN <= H)
+    bwd_cell_push_<H, C, false>(Gz, dGz, dhz, Cz, hd, pu, pr, dcz, m0, n0, t, T, M);
+  else
+    bwd_cell_push_<H, C, true>(Gz, dGz, dhz, Cz, hd, pu, pr, dcz, m0, n0, t, T, M);
+  __syncthreads();  // this tile's dG rows (every column) are written: the consumers' GEMMs read them
+  const SegKCt<1> la{{dGz + (int64_t)t * M * G4}, {G4}, M};
+  Acc<C> acc;
+  if (t > 0) {
+    acc.zero();
+    gemm_mainloop<C>(la, SegMCt<1>{{th + lo.whh}, {G4}, H}, m0, n0, 0, G4, acc, smem);
+    store_acc_rows<C>(acc, prec, m0, n0, M, H);
+  }
+  if (l > 0) {
+    acc.zero();
+    gemm_mainloop<C>(la, SegMCt<1>{{th + lo.wih}, {G4}, lo.cin}, m0, n0, 0, G4, acc, smem);
+    store_acc_rows<C>(acc, Pup + ((int64_t)((t & 1) * L + l - 1) * Z + z) * MH, m0, n0, M, lo.cin);
+  }
+}
+
 // Split-K BPTT step for small grids (see k_lstm_fwd_part): partial dh over a K-tile range of the
 // fused [above | next] GEMM, then k_lstm_bwd_cell sums the partials in order and runs bwd_cell.
 template <int H, class CfgNN>
@@ -1590,6 +1704,14 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
     if (hi <= lo) return;
     bwd_wave(d, w, po, e, hi - lo, false, wv);
     wv.tm0 = lo;
+  }
+  if (w.push) {  // (the caller chose the push form for the whole sweep: big tiles, no dropout)
+    count_variant(w, V_BWD_PUSH);
+    dim3 grid(wv.off[wv.n], ntn, w.Z);
+    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_push<HT, CfgBwd><<<grid, CfgBwd::NTH, 0, s>>>(
+                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, w.Prec, w.Pup, lsz, theta, tstride, wv, d.L, d.T,
+                              w.M)));
+    return;
   }
 #define SMAML_BWD_STEP(CFG, D_)                                                                               \
   SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \

@@ -602,6 +602,9 @@ struct HalfRows {  // the epilogue's view of one row half of C's tile
 };
 
 __device__ __forceinline__ float4 sel4(bool c, float4 a) { return c ? a : f4zero(); }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 __device__ __forceinline__ void f4set(float4& v, int e, float x) {
   if (e == 0) v.x = x;
   if (e == 1) v.y = x;
