@@ -317,7 +317,7 @@ TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
 # timing category -> the kernel symbol its HIP-event brackets enclose
 KERNEL_SYMBOL = {"gcn_layer": "k_gcn_layer|k_gcn_mlp", "lstm_fwd_step": "k_lstm_fwd_step", "lstm_fwd_dual": "k_lstm_fwd_dual",
                  "head_loss": "k_head_loss|k_head_dual", "head_dh": "k_gemm_nn|k_gemm_nn_dual",
-                 "lstm_bwd_step": "k_lstm_bwd_step", "lstm_bwd_dual": "k_lstm_bwd_dual", "wgrad": "k_wgrad",
+                 "lstm_bwd_step": "k_lstm_bwd_step|k_lstm_bwd_push", "lstm_bwd_dual": "k_lstm_bwd_dual", "wgrad": "k_wgrad",
                  "wgrad_reduce": "k_wgrad_reduce", "xg_proj": "k_xg_dedup|k_gemm_nt",
                  "dg_rowsum": "k_dg_rowsum"}
 

@@ -65,7 +65,7 @@ for s in "$@"; do
         > "$D/prof_kt.log" 2>&1
       ok $? prof_kt
       PB="$W --steps 1 --warmup 0 --cpu-sample-steps 0 --adapt-epochs 0 --cfg5-share-tasks 0 --no-timing"
-      RX="${PMC_REGEX:-k_lstm_fwd|k_lstm_bwd|k_wgrad|k_gcn_layer|k_gcn_mlp|k_gcn_expand|k_gemm_nn|k_gemm_nt|k_xg}"
+      RX="${PMC_REGEX:-k_lstm_fwd|k_lstm_bwd|k_wgrad|k_gcn_layer|k_gcn_mlp|k_gcn_expand|k_gcn_compact|k_gemm_nn|k_gemm_nt|k_xg|k_dg_rowsum}"
       for C in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 600 rocprofv3 --pmc $C --kernel-include-regex "$RX" -f csv -d "$D/prof_pmc_$C" -o run -- \
           python bench.py $PB > "$D/prof_pmc_$C.log" 2>&1

@@ -20,10 +20,10 @@ import sys
 
 # bench.py timing categories (api.cpp TIMED(...)) -> the kernels each category launches
 CATEGORIES = {
-    "gcn_layer": r"k_gcn_layer|k_gcn_mlp",
+    "gcn_layer": r"k_gcn_layer|k_gcn_mlp|k_gcn_expand|k_gcn_compact",
     "lstm_fwd_step": r"k_lstm_fwd_step",
     "lstm_fwd_dual": r"k_lstm_fwd_dual",
-    "lstm_bwd_step": r"k_lstm_bwd_step",
+    "lstm_bwd_step": r"k_lstm_bwd_step|k_lstm_bwd_push",
     "lstm_bwd_dual": r"k_lstm_bwd_dual",
     "wgrad": r"k_wgrad$|k_wgrad\b(?!_)",
     "wgrad_reduce": r"k_wgrad_reduce",

@@ -730,7 +730,7 @@ float* xgd_scratch(smaml_ctx* c, int64_t floats) {
 bool push_sweep(smaml_ctx* c, bool dual, int nch) {
   const Dims& d = c->d;
   Work& w = c->w;
-  if (!c->kn.bptt_push || w.drop.lstm() || (dual && !w.primal_kept)) return false;
+  if (!c->kn.bptt_push || (!dual && c->kn.bptt_push == 2) || w.drop.lstm() || (dual && !w.primal_kept)) return false;
   for (int e = 0; nch <= 1 && e < d.T + d.L - 1; ++e)
     if (!(dual ? bwd_dual_wave_big(d, w, c->po, e) : bwd_wave_big(d, w, c->po, e))) return false;
   const int64_t set = 3ll * d.L * w.Z * w.M * d.H;
@@ -2048,7 +2048,7 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_dedup = (int)value;
   } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
     c->kn.bptt_streams = (int)value;
-  } else if (k == "bptt_push" && (value == 0 || value == 1)) {
+  } else if (k == "bptt_push" && value >= 0 && value <= 2) {
     c->kn.bptt_push = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
     c->kn.f_compact = (int)value;

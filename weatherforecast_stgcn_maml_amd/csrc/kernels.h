@@ -145,7 +145,7 @@ struct Knobs {
   int fwd_streams = 0;           // the same for the big-tile forward diagonals (primal and tangent); 0 = auto
   int wgrad_overlap = 0;         // 1 (with row chunks): layer l's weight gradient on the caller's stream as soon as
                                  // its BPTT is done, beside the chunks' remaining diagonals
-  int bptt_push = 0;             // 1: big-tile BPTT sweeps (primal, and the tangent of kept steps) as producer-side
+  int bptt_push = 0;             // 1 (2: the tangent sweep only): big-tile BPTT sweeps (primal, and the tangent of kept steps) as producer-side
                                  // steps: cell backward first, from the dh partial sums its producers left, then
                                  // dG . W_hh and dG . W_ih for the two consumers (each dG read once as a GEMM
                                  // operand instead of twice)
