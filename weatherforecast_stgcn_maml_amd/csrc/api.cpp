@@ -235,7 +235,7 @@ struct smaml_ctx {
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
            SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
-           SMAML_BPTT_PUSH_DEFAULT, SMAML_F_COMPACT_DEFAULT};
+           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_F_COMPACT_DEFAULT};
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
@@ -2050,6 +2050,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bptt_streams = (int)value;
   } else if (k == "bptt_push" && value >= 0 && value <= 2) {
     c->kn.bptt_push = (int)value;
+  } else if (k == "wgrad_min_kt" && value >= 1 && value <= 4096) {
+    c->kn.wgrad_min_kt = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
     c->kn.f_compact = (int)value;
   } else if (k == "wgrad_overlap" && (value == 0 || value == 1)) {

@@ -149,6 +149,7 @@ struct Knobs {
                                  // steps: cell backward first, from the dh partial sums its producers left, then
                                  // dG . W_hh and dG . W_ih for the two consumers (each dG read once as a GEMM
                                  // operand instead of twice)
+  int wgrad_min_kt = 8;          // split-K weight gradients: at least this many K-tiles per split
   int f_compact = 0;             // 1: where every reader of a step's features goes through the distinct stream rows
                                  // (xg_dedup forwards, wgrad_dedup backwards), the GCN stores only those rows
 };
@@ -178,6 +179,9 @@ struct Knobs {
 #endif
 #ifndef SMAML_BPTT_PUSH_DEFAULT
 #define SMAML_BPTT_PUSH_DEFAULT 0
+#endif
+#ifndef SMAML_WGRAD_MIN_KT
+#define SMAML_WGRAD_MIN_KT 8  // K-tiles per split-K slice at least (knob wgrad_min_kt)
 #endif
 #ifndef SMAML_F_COMPACT_DEFAULT
 #define SMAML_F_COMPACT_DEFAULT 1

@@ -2472,7 +2472,8 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   const int nth = wide ? CfgTW::NTH : CfgTN::NTH;
   int64_t nsplit = (SMAML_WGRAD_THREADS / nth) / ((int64_t)ntm * ntn * w.Z);
   if (nsplit < 1) nsplit = 1;
-  if (nsplit > ktiles / 8) nsplit = ktiles / 8 > 0 ? ktiles / 8 : 1;
+  const int64_t min_kt = std::max(1, w.kn.wgrad_min_kt);
+  if (nsplit > ktiles / min_kt) nsplit = ktiles / min_kt > 0 ? ktiles / min_kt : 1;
   const int64_t per_split = (int64_t)w.Z * Mrows * ldp;
   if (nsplit * per_split > w.wpart_floats) nsplit = w.wpart_floats / per_split;
   if (nsplit < 1) nsplit = 1;
