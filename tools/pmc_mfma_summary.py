@@ -1,4 +1,4 @@
-"""Per-kernel MFMA utilisation / effective clock from tools/gpu_pmc_mfma.sh output.
+"""Per-kernel MFMA utilisation / effective clock from a rocprofv3 --pmc MFMA-busy pass (the round-1..3 sessions; `tools/gpu.sh pmc_sq` now).
 
 busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), kernel cycles =
 GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs); clock = kernel cycles / wall time."""

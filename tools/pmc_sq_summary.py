@@ -1,4 +1,4 @@
-"""Per-kernel SQ instruction mix from a rocprofv3 --pmc pass (tools/gpu_x6_pmc.sh pmc_sq):
+"""Per-kernel SQ instruction mix from a rocprofv3 --pmc pass (`tools/gpu.sh pmc_sq`):
 instructions per MFMA and the wait / active fractions of wave time."""
 import collections
 import csv
