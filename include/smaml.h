@@ -351,6 +351,11 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  consumers' partial sums dG . W_hh and dG . W_ih, so every dG is read
  *                                  once as a GEMM operand instead of twice (1; 0 = the consumer-side
  *                                  form; equal up to f32 rounding: dh = Pup + Prec adds once more);
+ *   "rowsum_side":                 after a chunked BPTT sweep, layer 0's dG row sums (wgrad_dedup) on a
+ *                                  side stream beside the weight gradients of layers L-1 .. 1 (1, the
+ *                                  default; bitwise equal to 0);
+ *   "wgrad_min_kt":                split-K weight gradients: at least this many 16-k tiles per slice
+ *                                  (default 8: the thread target decides);
  *   "wgrad_overlap":               with row chunks, layer l's weight gradient on the caller's stream as
  *                                  soon as its BPTT is done (1) or after the sweep (0, the default). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);

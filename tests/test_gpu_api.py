@@ -495,7 +495,7 @@ def test_stgcn_autograd_matches_oracle(d, p):
 
 
 @pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams",
-                                  "f_compact", "f_compact_layers"])
+                                  "f_compact", "f_compact_layers", "rowsum_side"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
@@ -504,13 +504,14 @@ def test_order_only_knobs_bitwise(knob):
     fwd_streams: every BPTT / forward diagonal in two row chunks on side streams, always on the big tiles,
     the weight gradients after the sweep; f_compact: the features of those steps stored once per distinct
     stream row, read only through the layer-0 projection tables and the gathered dW_ih0 -- fused and per-layer
-    GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles) leave every
+    GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles; rowsum_side: after a chunked
+    sweep, layer 0's dG row sums on a side stream beside the upper layers' weight gradients) leave every
     row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
     kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
-    compact = knob.startswith("f_compact")
+    compact = knob.startswith("f_compact") or knob == "rowsum_side"
     cfg = MamlConfig(inner_steps=2, batch=8 if compact else 4, order=2)
     P = synth.init_params(47, d, gcn_bias_scale=0.1)
     Ptr, Pg, _ = split(P)
@@ -523,6 +524,8 @@ def test_order_only_knobs_bitwise(knob):
         ml.ctx.set_option("bwdd_big_min", 0)
         if knob.endswith("_layers"):
             ml.ctx.set_option("gcn_fused", 0)
+        if knob == "rowsum_side":
+            ml.ctx.set_option("bwd_big_min", 0)  # (every sweep chunked: the row sums follow the joined sweep)
         if knob.endswith("_streams"):
             ml.ctx.set_option("bwd_big_min", 0)  # (chunked diagonals always run the big tiles: both arms do)
             ml.ctx.set_option(knob, 2 if on else 1)
@@ -534,7 +537,7 @@ def test_order_only_knobs_bitwise(knob):
         assert vc["bwd_dual_big_kept"] > 0, vc
         if knob.startswith("gcn_dedup"):
             assert (vc["gcn_dedup"] > 0) == bool(on), vc
-        if compact:  # every step: K inner steps + the query; the sweep reads them from so_F
+        if knob.startswith("f_compact"):  # every step: K inner steps + the query; the sweep reads them from so_F
             assert vc["f_compact"] == (cfg.inner_steps + 1 if on else 0), vc
         out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
         del ml

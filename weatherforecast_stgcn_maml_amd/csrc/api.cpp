@@ -235,7 +235,8 @@ struct smaml_ctx {
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
            SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
-           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_F_COMPACT_DEFAULT};
+           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_ROWSUM_SIDE_DEFAULT,
+           SMAML_F_COMPACT_DEFAULT};
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
@@ -761,14 +762,15 @@ bool wgrad_dedup_ok(const smaml_ctx* c) {
 // S = row sums of dGl (layer 0's dG or R(dG), k_dg_rowsum, in the scratch), then ONE gathered split-K
 // GEMM into grad's W_ih0 block (no bias; written, not accumulated). False: no scratch (the caller runs
 // the full-row form).
-bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float* grad) {
+// summed: the row sums are already in the scratch (rowsum_side, launched by the caller).
+bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float* grad, bool summed = false) {
   const Dims& d = c->d;
   Work& w = c->w;
   const int64_t rows = xg_dedup_rows(w.B, d.T, d.N), TM = (int64_t)d.T * w.M;
-  float* S = xgd_scratch(c, rows * 4 * d.H * w.Z);
+  float* S = summed ? c->xgd_buf : xgd_scratch(c, rows * 4 * d.H * w.Z);
   if (!S) return false;
   const LayerOff& lo = c->po.lay[0];
-  TIMED(c, s, C_DGSUM, 0, launch_dg_rowsum(s, d, w, dGl, TM * 4 * d.H, S));
+  if (!summed) TIMED(c, s, C_DGSUM, 0, launch_dg_rowsum(s, d, w, dGl, TM * 4 * d.H, S));
   WgradPlan p;
   plan_wgrad(w, S, rows * 4 * d.H, 4 * d.H, w.F, TM * lo.cin, lo.cin, nullptr, 0, 0, rows, 0, grad, c->po.P, lo.wih, -1,
              -1, -1, false, false, p);
@@ -780,6 +782,20 @@ bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float*
   TIMED(c, s, C_WGRAD, 2.0 * w.Z * rows * 4 * d.H * lo.cin, launch_wgrad_gemm(s, p));
   TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
   return true;
+}
+
+// rowsum_side: layer 0's dG row sums on side stream cs[0], forked from s now (the sweep is joined), so
+// they run beside the weight gradients of layers L-1 .. 1; s waits for join_ev[0] before layer 0's
+// gathered weight gradient. False: not applicable (the caller sums on s as usual).
+bool rowsum_side(smaml_ctx* c, hipStream_t s, const float* dGl) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  if (!c->kn.rowsum_side || !wgrad_dedup_ok(c)) return false;
+  const int64_t rows = xg_dedup_rows(w.B, d.T, d.N), TM = (int64_t)d.T * w.M;
+  float* S = xgd_scratch(c, rows * 4 * d.H * w.Z);
+  if (!S || fork_streams(c, s, 1) != SMAML_OK) return false;
+  TIMED(c, c->cs[0], C_DGSUM, 0, launch_dg_rowsum(c->cs[0], d, w, dGl, TM * 4 * d.H, S));
+  return hipEventRecord(c->join_ev[0], c->cs[0]) == hipSuccess;
 }
 
 // Whether a consecutive-window step's features may be stored compact (Work::fcompact, the distinct rows
@@ -1113,6 +1129,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   TRY(prep_bwd_images(c, s, theta, tstride));
   WgradPlan plans[MAX_LAYERS];
   double gfl = 0.0;
+  bool summed = false;  // (rowsum_side: layer 0's row sums already on their way)
   auto layer_wgrad = [&](int l) {
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
@@ -1126,7 +1143,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       gfl += 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H);
       return;
     }
-    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, w.dG, grad)) {
+    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, w.dG, grad, summed)) {
       // W_hh0 and the bias over every row (h_{t-1} differs per window): [0 | h_{t-1}], no input columns
       timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * d.H, w.dG, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.Hs, TM * d.H,
                   d.H, TM, w.M, grad, po.P, -1, lo.whh, lo.bih, lo.bhh, true, false, -1);
@@ -1135,6 +1152,15 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H), w.dG + (int64_t)l * lsz * 4, TM * 4 * d.H, 4 * d.H, X,
                 TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh,
                 lo.bih, lo.bhh, true, false, l - 1);
+  };
+  // after a chunked sweep: layers L-1 .. 1, with layer 0's row sums beside them (rowsum_side), then layer 0
+  auto after_sweep_wgrads = [&](const float* dG0) -> int {
+    summed = rowsum_side(c, s, dG0);
+    for (int l = d.L - 1; l >= 1; --l) layer_wgrad(l);
+    if (summed) HIP_TRY(hipStreamWaitEvent(s, c->join_ev[0], 0));
+    layer_wgrad(0);
+    summed = false;
+    return SMAML_OK;
   };
   // row chunks on side streams (knob bptt_streams): every diagonal's big-tile launch split by rows, the
   // weight gradients after the sweep on the caller's stream
@@ -1168,7 +1194,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     TRY(join_streams(c, s, nch));
     time_wall(c, s, wa, C_BWD_WALL, wfl);
     if (!c->kn.wgrad_overlap)
-      for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
+      TRY(after_sweep_wgrads(w.dG));
   }
   if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
   w.push = 0;
@@ -1233,13 +1259,14 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false);
   timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, RhT, hz, d.H, nullptr, 0, 0,
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true);
+  bool summed = false;  // (rowsum_side: layer 0's row sums already on their way)
   auto layer_wgrad = [&](int l) {
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
     const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
-    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, RdGl, HU)) {
+    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, RdGl, HU, summed)) {
       // R(dW_ih0) = R(dG0)^T F (R x = 0 at layer 0) over distinct stream rows above; R(dW_hh0) =
       // R(dG0)^T h + dG0^T R h and R(db) as one paired launch over every row
       const double flp = 2.0 * 2.0 * w.Z * TM * 4 * d.H * d.H;
@@ -1264,6 +1291,15 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * ((l > 0 ? lo.cin : 0) + d.H), dGl, TM * 4 * d.H, 4 * d.H, RX,
                 TM * lo.cin, l > 0 ? lo.cin : 0, w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih,
                 lo.whh, lo.bih, lo.bhh, false, true, l - 1);
+  };
+  // after a chunked sweep: layers L-1 .. 1, with layer 0's row sums beside them (rowsum_side), then layer 0
+  auto after_sweep_wgrads = [&](const float* dG0) -> int {
+    summed = rowsum_side(c, s, dG0);
+    for (int l = d.L - 1; l >= 1; --l) layer_wgrad(l);
+    if (summed) HIP_TRY(hipStreamWaitEvent(s, c->join_ev[0], 0));
+    layer_wgrad(0);
+    summed = false;
+    return SMAML_OK;
   };
   const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows || !bwd_dual_wave_big(d, w, po, std::min(d.L, d.T) - 1)
                       ? 1
@@ -1297,7 +1333,7 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     TRY(join_streams(c, s, nch));
     time_wall(c, s, wa, C_BWD_DUAL_WALL, wfl);
     if (!c->kn.wgrad_overlap)
-      for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
+      TRY(after_sweep_wgrads(w.RGs));
   }
   w.push = 0;
   HIP_TRY(hipGetLastError());
@@ -2052,6 +2088,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bptt_push = (int)value;
   } else if (k == "wgrad_min_kt" && value >= 1 && value <= 4096) {
     c->kn.wgrad_min_kt = (int)value;
+  } else if (k == "rowsum_side" && (value == 0 || value == 1)) {
+    c->kn.rowsum_side = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
     c->kn.f_compact = (int)value;
   } else if (k == "wgrad_overlap" && (value == 0 || value == 1)) {
