@@ -495,7 +495,7 @@ def test_stgcn_autograd_matches_oracle(d, p):
 
 
 @pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams",
-                                  "f_compact", "f_compact_layers", "rowsum_side"])
+                                  "f_compact", "f_compact_layers", "rowsum_side", "gcn_side"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
@@ -505,7 +505,8 @@ def test_order_only_knobs_bitwise(knob):
     the weight gradients after the sweep; f_compact: the features of those steps stored once per distinct
     stream row, read only through the layer-0 projection tables and the gathered dW_ih0 -- fused and per-layer
     GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles; rowsum_side: after a chunked
-    sweep, layer 0's dG row sums on a side stream beside the upper layers' weight gradients) leave every
+    sweep, layer 0's dG row sums on a side stream beside the upper layers' weight gradients; gcn_side: the
+    fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp) leave every
     row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
     kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for

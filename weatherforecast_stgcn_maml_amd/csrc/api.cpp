@@ -235,7 +235,7 @@ struct smaml_ctx {
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
            SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
-           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_ROWSUM_SIDE_DEFAULT,
+           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_GCN_SIDE_DEFAULT, SMAML_ROWSUM_SIDE_DEFAULT,
            SMAML_F_COMPACT_DEFAULT};
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
@@ -845,17 +845,21 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, const flo
     const bool dedup = consec && c->kn.gcn_dedup && w.B > 1 && !w.drop.gcn();
     if (dedup) count_variant(w, V_GCN_DEDUP);
     const double rows1 = dedup ? (double)w.Z * (w.B + d.T - 2) * d.N : (double)zb * (d.T - 1) * d.N;
+    // the t = 0 rows' ELL chain touches rows the fused kernel does not: on a side stream beside it (gcn_side)
+    const bool side = c->kn.gcn_side && fork_streams(c, s, 1) == SMAML_OK;
+    hipStream_t s0 = side ? c->cs[0] : s;
     TIMED(c, s, C_GCN, 2.0 * rows1 * d.Hc * (d.Cin0 + 3.0 * d.Hc),
           launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop, dedup, w.fcompact));
     for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks, masks indexed as rows of T*N-row samples
       const bool last = k == 3;
       float* dst = last ? w.F : bufs[k & 1];
-      TIMED(c, s, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
-            launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
+      TIMED(c, s0, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
+            launch_gcn_layer(s0, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
                              c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
                              d.N, d.N, &w.drop, rps));
       src = dst;
     }
+    if (side) TRY(join_streams(c, s, 1));
     HIP_TRY(hipGetLastError());
     return SMAML_OK;
   }
@@ -2088,6 +2092,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bptt_push = (int)value;
   } else if (k == "wgrad_min_kt" && value >= 1 && value <= 4096) {
     c->kn.wgrad_min_kt = (int)value;
+  } else if (k == "gcn_side" && (value == 0 || value == 1)) {
+    c->kn.gcn_side = (int)value;
   } else if (k == "rowsum_side" && (value == 0 || value == 1)) {
     c->kn.rowsum_side = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
