@@ -354,6 +354,9 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "rowsum_side":                 after a chunked BPTT sweep, layer 0's dG row sums (wgrad_dedup) on a
  *                                  side stream beside the weight gradients of layers L-1 .. 1 (1, the
  *                                  default; bitwise equal to 0);
+ *   "gcn_side", "reduce_side":     the fused GCN's t = 0 ELL chain beside k_gcn_mlp / each weight gradient's
+ *                                  split-K reduce beside the next GEMM, on side streams (0, the default;
+ *                                  bitwise equal to 1);
  *   "wgrad_min_kt":                split-K weight gradients: at least this many 16-k tiles per slice
  *                                  (default 8: the thread target decides);
  *   "wgrad_overlap":               with row chunks, layer l's weight gradient on the caller's stream as

@@ -495,7 +495,8 @@ def test_stgcn_autograd_matches_oracle(d, p):
 
 
 @pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams",
-                                  "f_compact", "f_compact_layers", "rowsum_side", "gcn_side"])
+                                  "f_compact", "f_compact_layers", "rowsum_side", "gcn_side",
+                                  "reduce_side"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
@@ -506,13 +507,14 @@ def test_order_only_knobs_bitwise(knob):
     stream row, read only through the layer-0 projection tables and the gathered dW_ih0 -- fused and per-layer
     GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles; rowsum_side: after a chunked
     sweep, layer 0's dG row sums on a side stream beside the upper layers' weight gradients; gcn_side: the
-    fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp) leave every
+    fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp; reduce_side: each weight gradient's
+    split-K reduce on a side stream beside the next GEMM, two partial slabs) leave every
     row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
     kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
-    compact = knob.startswith("f_compact") or knob == "rowsum_side"
+    compact = knob.startswith("f_compact") or knob in ("rowsum_side", "reduce_side")
     cfg = MamlConfig(inner_steps=2, batch=8 if compact else 4, order=2)
     P = synth.init_params(47, d, gcn_bias_scale=0.1)
     Ptr, Pg, _ = split(P)
@@ -525,7 +527,7 @@ def test_order_only_knobs_bitwise(knob):
         ml.ctx.set_option("bwdd_big_min", 0)
         if knob.endswith("_layers"):
             ml.ctx.set_option("gcn_fused", 0)
-        if knob == "rowsum_side":
+        if knob in ("rowsum_side", "reduce_side"):
             ml.ctx.set_option("bwd_big_min", 0)  # (every sweep chunked: the row sums follow the joined sweep)
         if knob.endswith("_streams"):
             ml.ctx.set_option("bwd_big_min", 0)  # (chunked diagonals always run the big tiles: both arms do)

@@ -235,7 +235,8 @@ struct smaml_ctx {
   Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
            SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
            SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
-           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_GCN_SIDE_DEFAULT, SMAML_ROWSUM_SIDE_DEFAULT,
+           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_GCN_SIDE_DEFAULT, SMAML_REDUCE_SIDE_DEFAULT,
+           SMAML_ROWSUM_SIDE_DEFAULT,
            SMAML_F_COMPACT_DEFAULT};
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
@@ -263,6 +264,15 @@ struct smaml_ctx {
   int64_t xg_cap = 0;
   float* xgd_buf = nullptr;   // big-tile forward: layer 0's projection per distinct stream row (prep_xg_dedup)
   int64_t xgd_cap = 0;
+  // reduce_side: a second partial slab and the events that order the two slabs' GEMMs and reduces
+  struct {
+    bool on = false;
+    int next = 0;
+    bool pending[2] = {false, false};
+    hipEvent_t gemm[2] = {}, done[2] = {};
+  } red;
+  float* wpart2 = nullptr;
+  int64_t wpart2_cap = 0;
   float* push_buf = nullptr;  // push BPTT partial sums: primal [3][L][Z][M][H], then tangent (push_partials)
   int64_t push_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
@@ -614,6 +624,62 @@ void set_work(smaml_ctx* c, int Z, int B) {
   } while (0)
 
 // Weight gradient = split-K GEMM (C_WGRAD) + fixed-order reduce (C_WGRAD_RED).
+int fork_streams(smaml_ctx* c, hipStream_t s, int n);
+
+// One weight gradient's split-K GEMM + reduce. With reduce_side on (after a chunked sweep) the reduce
+// runs on side stream cs[1] behind an event, the GEMMs alternate between the two partial slabs, and a
+// GEMM waits for the reduce that last read its slab; reduce_side_end makes s wait for them all.
+void wgrad_run(smaml_ctx* c, hipStream_t s, double fl, WgradPlan& p) {
+  if (!c->red.on) {
+    TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
+    TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+    return;
+  }
+  const int b = c->red.next;
+  c->red.next ^= 1;
+  if (b) p.part = c->wpart2;
+  if (c->red.pending[b]) (void)hipStreamWaitEvent(s, c->red.done[b], 0);
+  TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
+  (void)hipEventRecord(c->red.gemm[b], s);
+  (void)hipStreamWaitEvent(c->cs[1], c->red.gemm[b], 0);
+  TIMED(c, c->cs[1], C_WGRAD_RED, 0, launch_wgrad_reduce(c->cs[1], p));
+  (void)hipEventRecord(c->red.done[b], c->cs[1]);
+  c->red.pending[b] = true;
+}
+
+bool reduce_side_begin(smaml_ctx* c, hipStream_t s) {
+  c->red.on = false;
+  if (!c->kn.reduce_side) return false;
+  const int64_t need = c->w.wpart_floats;
+  if (need > c->wpart2_cap) {
+    if (c->wpart2) (void)hipFree(c->wpart2);
+    c->wpart2 = nullptr;
+    c->wpart2_cap = 0;
+    if (hipMalloc((void**)&c->wpart2, need * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    c->wpart2_cap = need;
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (!c->red.gemm[i] && hipEventCreateWithFlags(&c->red.gemm[i], hipEventDisableTiming) != hipSuccess) return false;
+    if (!c->red.done[i] && hipEventCreateWithFlags(&c->red.done[i], hipEventDisableTiming) != hipSuccess) return false;
+  }
+  if (fork_streams(c, s, 2) != SMAML_OK) return false;  // (creates cs[1]; it starts behind s's work so far)
+  c->red.on = true;
+  c->red.next = 0;
+  c->red.pending[0] = c->red.pending[1] = false;
+  return true;
+}
+
+int reduce_side_end(smaml_ctx* c, hipStream_t s) {
+  if (!c->red.on) return SMAML_OK;
+  c->red.on = false;
+  for (int i = 0; i < 2; ++i)
+    if (c->red.pending[i]) HIP_TRY(hipStreamWaitEvent(s, c->red.done[i], 0));
+  return SMAML_OK;
+}
+
 void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t a_zstride, int Mrows,
                  const float* B1, int64_t b1_zstride, int c1, const float* B2, int64_t b2_zstride, int c2, int64_t K,
                  int Mshift, float* grad, int64_t P, int64_t off_w1, int64_t off_w2, int64_t off_b1, int64_t off_b2,
@@ -626,8 +692,7 @@ void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t
   count_variant(c->w, V_WGRAD);
   if (p.wide) count_variant(c->w, V_WGRAD_WIDE);
   if (p.ws) count_variant(c->w, V_WGRAD_WS);
-  TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
-  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+  wgrad_run(c, s, fl, p);
 }
 
 // Tangent weight gradient of one LSTM layer as ONE split-K launch + ONE reduce:
@@ -646,8 +711,7 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
   if (p.wide) count_variant(c->w, V_WGRAD_WIDE);
   if (p.ws) count_variant(c->w, V_WGRAD_WS);
   count_variant(c->w, V_WGRAD_PAIR);
-  TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
-  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+  wgrad_run(c, s, fl, p);
   return true;
 }
 
@@ -779,8 +843,7 @@ bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float*
   count_variant(w, V_WGRAD);
   count_variant(w, V_WGRAD_DEDUP);
   if (p.wide) count_variant(w, V_WGRAD_WIDE);
-  TIMED(c, s, C_WGRAD, 2.0 * w.Z * rows * 4 * d.H * lo.cin, launch_wgrad_gemm(s, p));
-  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
+  wgrad_run(c, s, 2.0 * w.Z * rows * 4 * d.H * lo.cin, p);
   return true;
 }
 
@@ -1160,11 +1223,12 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   // after a chunked sweep: layers L-1 .. 1, with layer 0's row sums beside them (rowsum_side), then layer 0
   auto after_sweep_wgrads = [&](const float* dG0) -> int {
     summed = rowsum_side(c, s, dG0);
+    reduce_side_begin(c, s);
     for (int l = d.L - 1; l >= 1; --l) layer_wgrad(l);
     if (summed) HIP_TRY(hipStreamWaitEvent(s, c->join_ev[0], 0));
     layer_wgrad(0);
     summed = false;
-    return SMAML_OK;
+    return reduce_side_end(c, s);
   };
   // row chunks on side streams (knob bptt_streams): every diagonal's big-tile launch split by rows, the
   // weight gradients after the sweep on the caller's stream
@@ -1299,11 +1363,12 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
   // after a chunked sweep: layers L-1 .. 1, with layer 0's row sums beside them (rowsum_side), then layer 0
   auto after_sweep_wgrads = [&](const float* dG0) -> int {
     summed = rowsum_side(c, s, dG0);
+    reduce_side_begin(c, s);
     for (int l = d.L - 1; l >= 1; --l) layer_wgrad(l);
     if (summed) HIP_TRY(hipStreamWaitEvent(s, c->join_ev[0], 0));
     layer_wgrad(0);
     summed = false;
-    return SMAML_OK;
+    return reduce_side_end(c, s);
   };
   const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows || !bwd_dual_wave_big(d, w, po, std::min(d.L, d.T) - 1)
                       ? 1
@@ -1513,6 +1578,11 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->xg_buf) (void)hipFree(c->xg_buf);
   if (c->xgd_buf) (void)hipFree(c->xgd_buf);
   if (c->push_buf) (void)hipFree(c->push_buf);
+  if (c->wpart2) (void)hipFree(c->wpart2);
+  for (int i = 0; i < 2; ++i) {
+    if (c->red.gemm[i]) (void)hipEventDestroy(c->red.gemm[i]);
+    if (c->red.done[i]) (void)hipEventDestroy(c->red.done[i]);
+  }
   if (c->bar) (void)hipFree(c->bar);
   for (int i = 0; i < 4; ++i) {
     if (c->cs[i]) (void)hipStreamDestroy(c->cs[i]);
@@ -2094,6 +2164,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_min_kt = (int)value;
   } else if (k == "gcn_side" && (value == 0 || value == 1)) {
     c->kn.gcn_side = (int)value;
+  } else if (k == "reduce_side" && (value == 0 || value == 1)) {
+    c->kn.reduce_side = (int)value;
   } else if (k == "rowsum_side" && (value == 0 || value == 1)) {
     c->kn.rowsum_side = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {

@@ -151,6 +151,8 @@ struct Knobs {
                                  // operand instead of twice)
   int wgrad_min_kt = 8;          // split-K weight gradients: at least this many K-tiles per split
   int gcn_side = 0;              // 1: the fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp (disjoint rows)
+  int reduce_side = 0;           // 1: after a chunked sweep, each weight gradient's split-K reduce on a side stream
+                                 // beside the next layer's GEMM (two partial slabs, alternating)
   int rowsum_side = 0;           // 1: after a chunked sweep, layer 0's dG row sums (k_dg_rowsum) on a side stream
                                  // beside the weight gradients of layers L-1 .. 1
   int f_compact = 0;             // 1: where every reader of a step's features goes through the distinct stream rows
@@ -188,6 +190,9 @@ struct Knobs {
 #endif
 #ifndef SMAML_GCN_SIDE_DEFAULT
 #define SMAML_GCN_SIDE_DEFAULT 0
+#endif
+#ifndef SMAML_REDUCE_SIDE_DEFAULT
+#define SMAML_REDUCE_SIDE_DEFAULT 0
 #endif
 #ifndef SMAML_ROWSUM_SIDE_DEFAULT
 #define SMAML_ROWSUM_SIDE_DEFAULT 1  // A/B (profiles/r05_ab_rowsum_side.log): config 2 -5 ms, config-5 share -14 ms
