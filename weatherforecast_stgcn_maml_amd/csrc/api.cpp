@@ -201,6 +201,37 @@ struct Staging {
 
 }  // namespace
 
+// The build-time defaults of the run-time knobs, by name (kernels.h Knobs; smaml_set_option changes them).
+static Knobs default_knobs() {
+  Knobs k;
+  k.bwd_big_min = SMAML_BWD_BIG_MIN;
+  k.bwdd_big_min = SMAML_BWDD_BIG_MIN;
+  k.split_max = SMAML_SPLIT_MAX;
+  k.wgrad_group_max_rows = SMAML_WGRAD_GROUP_ROWS;
+  k.wgrad_group_wgs = SMAML_WGRAD_GROUP_WGS;
+  k.gcn_fused = SMAML_GCN_FUSED;
+  k.gate_img = SMAML_GATE_IMG;
+  k.wgrad_wide = 1;
+  k.wgrad_pair = SMAML_WGRAD_PAIR;
+  k.wgrad_ws = SMAML_WGRAD_WS_DEFAULT;
+  k.bwdd_remap = SMAML_BWDD_REMAP_DEFAULT;
+  k.small_kw = SMAML_SMALL_KW;
+  k.gcn_dedup = 1;
+  k.xg_dedup = SMAML_XG_DEDUP_DEFAULT;
+  k.wgrad_dedup = SMAML_WGRAD_DEDUP_DEFAULT;
+  k.bptt_streams = SMAML_BPTT_STREAMS_DEFAULT;
+  k.fwd_streams = SMAML_FWD_STREAMS_DEFAULT;
+  k.wgrad_overlap = 0;
+  k.bptt_push = SMAML_BPTT_PUSH_DEFAULT;
+  k.wgrad_min_kt = SMAML_WGRAD_MIN_KT;
+  k.wgrad_threads = 0;
+  k.gcn_side = SMAML_GCN_SIDE_DEFAULT;
+  k.reduce_side = SMAML_REDUCE_SIDE_DEFAULT;
+  k.rowsum_side = SMAML_ROWSUM_SIDE_DEFAULT;
+  k.f_compact = SMAML_F_COMPACT_DEFAULT;
+  return k;
+}
+
 struct smaml_ctx {
   smaml_dims dims{};
   Dims d{};
@@ -232,12 +263,7 @@ struct smaml_ctx {
   Staging stage;
   // kernel-variant launch counters and run-time tile knobs (smaml_variant_counts / smaml_set_option)
   int64_t vcount[NVAR] = {};
-  Knobs kn{SMAML_BWD_BIG_MIN, SMAML_BWDD_BIG_MIN, SMAML_SPLIT_MAX, SMAML_WGRAD_GROUP_ROWS, SMAML_WGRAD_GROUP_WGS,
-           SMAML_GCN_FUSED, SMAML_GATE_IMG, 1, SMAML_WGRAD_PAIR, SMAML_WGRAD_WS_DEFAULT, SMAML_BWDD_REMAP_DEFAULT, SMAML_SMALL_KW, 1,
-           SMAML_XG_DEDUP_DEFAULT, SMAML_WGRAD_DEDUP_DEFAULT, SMAML_BPTT_STREAMS_DEFAULT, SMAML_FWD_STREAMS_DEFAULT, 0,
-           SMAML_BPTT_PUSH_DEFAULT, SMAML_WGRAD_MIN_KT, SMAML_GCN_SIDE_DEFAULT, SMAML_REDUCE_SIDE_DEFAULT,
-           SMAML_ROWSUM_SIDE_DEFAULT,
-           SMAML_F_COMPACT_DEFAULT};
+  Knobs kn = default_knobs();
   int n_cu = 256;  // compute units of the device (smaml_create)
   int keep_max = -1;  // cap on kept second-order steps (-1: SMAML_KEEP env or all that fit)
   // tasks
@@ -2160,6 +2186,8 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.bptt_streams = (int)value;
   } else if (k == "bptt_push" && value >= 0 && value <= 2) {
     c->kn.bptt_push = (int)value;
+  } else if (k == "wgrad_threads" && value >= 0 && value <= (1 << 24)) {
+    c->kn.wgrad_threads = (int)value;
   } else if (k == "wgrad_min_kt" && value >= 1 && value <= 4096) {
     c->kn.wgrad_min_kt = (int)value;
   } else if (k == "gcn_side" && (value == 0 || value == 1)) {

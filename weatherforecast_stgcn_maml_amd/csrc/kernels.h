@@ -150,6 +150,7 @@ struct Knobs {
                                  // dG . W_hh and dG . W_ih for the two consumers (each dG read once as a GEMM
                                  // operand instead of twice)
   int wgrad_min_kt = 8;          // split-K weight gradients: at least this many K-tiles per split
+  int wgrad_threads = 0;         // split-K weight gradients: thread target of one launch (0 = SMAML_WGRAD_THREADS)
   int gcn_side = 0;              // 1: the fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp (disjoint rows)
   int reduce_side = 0;           // 1: after a chunked sweep, each weight gradient's split-K reduce on a side stream
                                  // beside the next layer's GEMM (two partial slabs, alternating)

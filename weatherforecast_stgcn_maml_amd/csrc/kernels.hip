@@ -2470,7 +2470,8 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   const int64_t ktiles = (K + CfgTN::BK - 1) / CfgTN::BK;
   // aim for SMAML_WGRAD_THREADS threads in all, at least 8 K-tiles per split, bounded by the slab buffer
   const int nth = wide ? CfgTW::NTH : CfgTN::NTH;
-  int64_t nsplit = (SMAML_WGRAD_THREADS / nth) / ((int64_t)ntm * ntn * w.Z);
+  const int64_t target = w.kn.wgrad_threads > 0 ? w.kn.wgrad_threads : SMAML_WGRAD_THREADS;
+  int64_t nsplit = (target / nth) / ((int64_t)ntm * ntn * w.Z);
   if (nsplit < 1) nsplit = 1;
   const int64_t min_kt = std::max(1, w.kn.wgrad_min_kt);
   if (nsplit > ktiles / min_kt) nsplit = ktiles / min_kt > 0 ? ktiles / min_kt : 1;
