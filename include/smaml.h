@@ -352,8 +352,8 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  once as a GEMM operand instead of twice (1; 0 = the consumer-side
  *                                  form; equal up to f32 rounding: dh = Pup + Prec adds once more);
  *   "rowsum_side":                 after a chunked BPTT sweep, layer 0's dG row sums (wgrad_dedup) on a
- *                                  side stream beside the weight gradients of layers L-1 .. 1 (1, the
- *                                  default; bitwise equal to 0);
+ *                                  side stream beside the weight gradients of layers L-1 .. 1 (0, the
+ *                                  default; bitwise equal to 1);
  *   "gcn_side", "reduce_side":     the fused GCN's t = 0 ELL chain beside k_gcn_mlp / each weight gradient's
  *                                  split-K reduce beside the next GEMM, on side streams (0, the default;
  *                                  bitwise equal to 1);

@@ -196,7 +196,8 @@ struct Knobs {
 #define SMAML_REDUCE_SIDE_DEFAULT 0
 #endif
 #ifndef SMAML_ROWSUM_SIDE_DEFAULT
-#define SMAML_ROWSUM_SIDE_DEFAULT 1  // A/B (profiles/r05_ab_rowsum_side.log): config 2 -5 ms, config-5 share -14 ms
+#define SMAML_ROWSUM_SIDE_DEFAULT 0  // A/B (profiles/r05_ab_rowsum_side.log): config 2 -5 ms, config-5 share -14 ms, but the
+                                     // weight gradients then share the chip with it (their measured rate -4 %): off
 #endif
 #ifndef SMAML_F_COMPACT_DEFAULT
 #define SMAML_F_COMPACT_DEFAULT 1
