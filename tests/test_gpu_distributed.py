@@ -23,14 +23,14 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, tasks, out_q):
+def _rank_main(rank, world, port, tasks, out_q, config="cfg1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     import torch
     import torch.distributed as dist
 
     from weatherforecast_stgcn_maml_amd import synth
-    from weatherforecast_stgcn_maml_amd.config import CONFIG1, MamlConfig
+    from weatherforecast_stgcn_maml_amd.config import CONFIG1, CONFIG2, MamlConfig
     from weatherforecast_stgcn_maml_amd.distributed import init_from_env, shard_tasks
     from weatherforecast_stgcn_maml_amd.graph import build_spatial_graph
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
@@ -38,29 +38,34 @@ def _rank_main(rank, world, port, tasks, out_q):
     torch.cuda.set_device(0)
     if world > 1:
         init_from_env("gloo")
-    d = CONFIG1
-    cfg = MamlConfig(inner_steps=2, batch=2, order=2)
+    d = CONFIG1 if config == "cfg1" else CONFIG2
+    cfg = MamlConfig(inner_steps=2, batch=2 if config == "cfg1" else 4, order=2)
     P = synth.init_params(31, d, gcn_bias_scale=0.1)
     names = [k for k in P if k.startswith(("lstm.", "output_layer."))]
-    lats, lons = synth.region_grid(n_lat=5, n_lon=5)
+    side = int(round(d.num_nodes ** 0.5))
+    lats, lons = synth.region_grid(n_lat=side, n_lon=side)
     ei = build_spatial_graph(lats, lons, 4)[0]
     mine = shard_tasks(tasks, rank, world)
     feats = [synth.make_features(synth.task_seed(j), d.num_nodes, stream_len_for(cfg, d)) for j in mine]
     ml = MetaLearner(d, cfg, {k: v for k, v in P.items() if k not in names}, {k: P[k] for k in names}, ei,
                      device="cuda:0")
     ml.set_tasks(feats, task_ids=mine)
-    meta_losses = [ml.meta_step().meta_loss for _ in range(STEPS)]
-    out_q.put((rank, mine, ml.theta.cpu().numpy(), meta_losses))
+    meta_losses, mg1 = [], None
+    for i in range(STEPS):
+        meta_losses.append(ml.meta_step().meta_loss)
+        if i == 0:  # the first step's all-reduced meta-gradient (both sides at the same theta)
+            mg1 = ml.meta_grad.cpu().numpy().copy()
+    out_q.put((rank, mine, ml.theta.cpu().numpy(), meta_losses, mg1))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _run(world, tasks):
+def _run(world, tasks, config="cfg1"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, tasks, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, tasks, q, config)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
@@ -132,3 +137,18 @@ def test_two_rank_meta_learner_matches_one_rank(tasks):
         assert np.array_equal(two[0][2], one[2])
     assert not np.array_equal(one[2], np.zeros_like(one[2]))
     np.testing.assert_allclose(two[0][3], one[3], rtol=1e-6)
+
+
+def test_two_rank_meta_learner_cfg2_shapes():
+    """The same sharding at BASELINE config-2 shapes (N=441, Hc=256, LSTM 4x128; B=4, K=2, second order,
+    3 tasks: rank 0 holds two, rank 1 one): the all-reduced meta-gradient equals the one-rank one up to
+    the summation order of the task terms (<= 1e-6 rel-L2), and the replicated AdamW leaves theta and the
+    meta-loss bitwise identical on both ranks (train_hybrid_maml_v5.py:144-184)."""
+    one = _run(1, 3, "cfg2")[0]
+    two = _run(2, 3, "cfg2")
+    assert sorted(two[0][1] + two[1][1]) == [0, 1, 2] and len(two[0][1]) == 2
+    assert np.array_equal(two[0][2], two[1][2]) and two[0][3] == two[1][3]
+    assert np.array_equal(two[0][4], two[1][4])
+    err = np.linalg.norm(two[0][4] - one[4]) / np.linalg.norm(one[4])
+    assert err <= 1e-6, err
+    np.testing.assert_allclose(two[0][3][0], one[3][0], rtol=1e-6)  # (step 1: same theta on both sides)
