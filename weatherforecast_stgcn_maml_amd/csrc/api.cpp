@@ -295,6 +295,7 @@ struct smaml_ctx {
     bool on = false;
     int next = 0;
     bool pending[2] = {false, false};
+    bool failed = false;  // an event call failed: the rest ran on s, reduce_side_end reports it
     hipEvent_t gemm[2] = {}, done[2] = {};
   } red;
   float* wpart2 = nullptr;
@@ -664,13 +665,25 @@ void wgrad_run(smaml_ctx* c, hipStream_t s, double fl, WgradPlan& p) {
   const int b = c->red.next;
   c->red.next ^= 1;
   if (b) p.part = c->wpart2;
-  if (c->red.pending[b]) (void)hipStreamWaitEvent(s, c->red.done[b], 0);
+  if (c->red.pending[b] && hipStreamWaitEvent(s, c->red.done[b], 0) != hipSuccess) {
+    // the slab's last reader cannot be ordered by an event: drain the side stream, then carry on on s
+    (void)hipStreamSynchronize(c->cs[1]);
+    c->red.failed = true;
+  }
   TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
-  (void)hipEventRecord(c->red.gemm[b], s);
-  (void)hipStreamWaitEvent(c->cs[1], c->red.gemm[b], 0);
+  if (c->red.failed || hipEventRecord(c->red.gemm[b], s) != hipSuccess ||
+      hipStreamWaitEvent(c->cs[1], c->red.gemm[b], 0) != hipSuccess) {
+    c->red.failed = true;
+    TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));  // (in order on s)
+    c->red.pending[b] = false;
+    return;
+  }
   TIMED(c, c->cs[1], C_WGRAD_RED, 0, launch_wgrad_reduce(c->cs[1], p));
-  (void)hipEventRecord(c->red.done[b], c->cs[1]);
-  c->red.pending[b] = true;
+  c->red.pending[b] = hipEventRecord(c->red.done[b], c->cs[1]) == hipSuccess;
+  if (!c->red.pending[b]) {
+    (void)hipStreamSynchronize(c->cs[1]);
+    c->red.failed = true;
+  }
 }
 
 bool reduce_side_begin(smaml_ctx* c, hipStream_t s) {
@@ -694,6 +707,7 @@ bool reduce_side_begin(smaml_ctx* c, hipStream_t s) {
   if (fork_streams(c, s, 2) != SMAML_OK) return false;  // (creates cs[1]; it starts behind s's work so far)
   c->red.on = true;
   c->red.next = 0;
+  c->red.failed = false;
   c->red.pending[0] = c->red.pending[1] = false;
   return true;
 }
@@ -703,6 +717,7 @@ int reduce_side_end(smaml_ctx* c, hipStream_t s) {
   c->red.on = false;
   for (int i = 0; i < 2; ++i)
     if (c->red.pending[i]) HIP_TRY(hipStreamWaitEvent(s, c->red.done[i], 0));
+  if (c->red.failed) return fail(SMAML_EHIP, "reduce_side: an event call failed (the reduces ran in order on s)");
   return SMAML_OK;
 }
 
