@@ -899,7 +899,9 @@ bool rowsum_side(smaml_ctx* c, hipStream_t s, const float* dGl) {
   float* S = xgd_scratch(c, rows * 4 * d.H * w.Z);
   if (!S || fork_streams(c, s, 1) != SMAML_OK) return false;
   TIMED(c, c->cs[0], C_DGSUM, 0, launch_dg_rowsum(c->cs[0], d, w, dGl, TM * 4 * d.H, S));
-  return hipEventRecord(c->join_ev[0], c->cs[0]) == hipSuccess;
+  if (hipEventRecord(c->join_ev[0], c->cs[0]) == hipSuccess) return true;
+  (void)hipStreamSynchronize(c->cs[0]);  // (no event to order by: the caller sums again on s, after this one)
+  return false;
 }
 
 // Whether a consecutive-window step's features may be stored compact (Work::fcompact, the distinct rows
