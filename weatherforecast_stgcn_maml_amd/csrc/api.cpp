@@ -515,7 +515,9 @@ int ensure_keep(smaml_ctx* c, int K, int Z, int B) {
   const int64_t rowsL = (int64_t)Z * B * d.T * d.N * d.L;
   c->keep_want = want;
   if (want <= c->keep_n && rowsL <= c->keep_rows) return SMAML_OK;
-  if (want == c->keep_tried_K && rowsL == c->keep_tried_rows) return SMAML_OK;  // already as many as fit
+  // already as many as fit for a group at least this large: keep those slots (unequal task groups, e.g.
+  // 8 + 7, would otherwise free and re-allocate every slot at every group change, seconds per meta-step)
+  if (rowsL <= c->keep_rows && want <= c->keep_tried_K && rowsL <= c->keep_tried_rows) return SMAML_OK;
   TRY(free_keep(c));
   c->keep_tried_K = want;
   c->keep_tried_rows = rowsL;
