@@ -632,6 +632,17 @@ __device__ __forceinline__ void sto(float* base, uint32_t byteoff, const float4&
 // Per pass a lane has 2 items: ld(ml, u) issues both items' loads before st(ml, u, pre, v) stores
 // either (ml = tile row, u = tile unit, pre[g] = gate g of units u .. u+3). Starts with a barrier
 // (the mainloop's last LDS reads), leaves the LDS in use until the caller's next barrier.
+#ifndef SMAML_EPI_WAVE_SYNC
+#define SMAML_EPI_WAVE_SYNC 0  // 1: the exchange below syncs each wave alone (its LDS region is its own, and every
+#endif                         // mainloop ends with a workgroup barrier), not the whole workgroup
+// Orders one wave's LDS writes before its own later LDS reads (and vice versa): the DS unit runs a
+// wave's instructions in order, so only the compiler must not move them across.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <class C, class LD, class ST>
 __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (&badd)[4], float* smem, LD&& ld,
                                                 ST&& st) {
@@ -641,7 +652,8 @@ __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (
   float* ws = smem + wave * 2048;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    __syncthreads();  // p = 0: the mainloop's LDS reads are done; p = 1: pass 0's reads are done
+    // p = 0: the mainloop's LDS reads are done; p = 1: pass 0's reads are done
+    if constexpr (SMAML_EPI_WAVE_SYNC) wave_lds_sync(); else __syncthreads();
 #pragma unroll
     for (int r = 8 * p; r < 8 * p + 8; ++r) {
       const int rl = racc(r) + 4 * h - 16 * p;
@@ -649,7 +661,7 @@ __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (
 #pragma unroll
       for (int g = 0; g < 4; ++g) ws[rl * 128 + (g ^ sw) * 32 + jj] = acc.v[0][g][r] + badd[g];
     }
-    __syncthreads();
+    if constexpr (SMAML_EPI_WAVE_SYNC) wave_lds_sync(); else __syncthreads();
     decltype(ld(0, 0)) v[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
