@@ -352,6 +352,9 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
       });
 }
 
+#ifndef SMAML_DIAG_FWD
+#define SMAML_DIAG_FWD 0  // timing diagnostics only (wrong results): 1 = forward step without its epilogue,
+#endif                    // 2 = without its GEMM
 // XG (xg != null): layer 0's input projection of this step's windows comes from the XgDedup table
 // (launch_xg_dedup): the accumulators start from it and the K loop covers the recurrent segment only.
 template <int H, bool DROP, bool IMG = false>
@@ -387,6 +390,10 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
   Acc<CfgGate> acc;
   int kbeg = 0;  // (XG: the K loop starts past the input segment)
   acc.zero();
+  if (SMAML_DIAG_FWD == 2) {  // timing diagnostic: cell epilogue only (no K loop)
+    fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, nullptr);
+    return;
+  }
   // (the table is added in the epilogue: loading it into the accumulators before the K loop keeps 64 more
   // registers live through the loop's prologue and spills)
   const float* xgt = !DROP && xg && l == 0 ? xg + (int64_t)z * xg_zstride + xg_dedup_row0(t, M, xg_N) * (4 * H) : nullptr;
@@ -416,6 +423,15 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     }
   }
 
+  if (SMAML_DIAG_FWD == 1) {  // timing diagnostic: GEMM phase only (every accumulator kept live)
+    float sum = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sum += acc.v[0][g][r];
+    if (sum == 12345.678f) Gz[threadIdx.x] = sum;  // (never true in practice; the MFMAs stay)
+    return;
+  }
   if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1) {
     fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
   } else {
