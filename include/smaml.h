@@ -359,6 +359,8 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  bitwise equal to 1);
  *   "wgrad_min_kt":                split-K weight gradients: at least this many 16-k tiles per slice
  *                                  (default 8: the thread target decides);
+ *   "wgrad_threads":               split-K weight gradients: the thread target of one launch (0, the
+ *                                  default = 3072 x 256);
  *   "wgrad_overlap":               with row chunks, layer l's weight gradient on the caller's stream as
  *                                  soon as its BPTT is done (1) or after the sweep (0, the default). */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
