@@ -35,7 +35,7 @@ PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS  # dense BF16 MFMA = 16x the 
 PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
 # timing category -> GEMM family of smaml_build_info (product form of its contraction)
-CAT_FAMILY = {"gcn_layer": "gcn", "lstm_fwd_step": "gate", "lstm_fwd_dual": "gate_dual", "lstm_bwd_step": "bptt",
+CAT_FAMILY = {"gcn_layer": "gcn", "xg_proj": "gate", "lstm_fwd_step": "gate", "lstm_fwd_dual": "gate_dual", "lstm_bwd_step": "bptt",
               "lstm_bwd_dual": "bptt_dual", "wgrad": "wgrad", "head_dh": "bptt", "head_loss": "bptt"}
 
 
@@ -166,7 +166,9 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
     """BASELINE config 4 (regional adaptation, adapt_hybrid_v5.py:186-208): epochs of shuffled batch-1
     train steps (fwd + bwd + clip + Adam(L2)) of the pretrained init on one N=441 region, each epoch
     one smaml_adapt_steps call on a fresh context (cold per-window GCN feature cache: epoch 1 also
-    computes every window's GCN features, later epochs reuse them, F2). Returns the per-epoch times
+    computes every window's GCN features, later epochs reuse them, F2). The context's workspace and
+    cache are allocated before the first epoch (smaml_adapt_prepare, reported as setup_ms), as
+    adapt.adapt does; each epoch's phases (reserve / cache alloc / cache fill / steps) are reported. Returns the per-epoch times
     and a per-category kernel breakdown of ``breakdown_steps`` warm steps timed with HIP events in a
     separate pass (the events add launch overhead, so those steps are not the timed value)."""
     import torch
@@ -188,6 +190,8 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
 
     def run(n_epochs, steps=None, timing=False):
         ctx = _capi.Context(d, dev.index or 0)
+        ts = time.perf_counter()
+        phases = []
         ctx.set_graph(ei)
         gflat = params.pack(gcn, d, which=1, device=dev)
         ctx.set_gcn_params(gflat)
@@ -197,8 +201,15 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
         m, v = torch.zeros_like(th), torch.zeros_like(th)
         losses = torch.empty(n_train, device=dev)
         lr_dev = torch.full((n_train,), lr, device=dev, dtype=torch.float32)
-        per_epoch, step, kern = [], 0, None
+        # set-up (as adapt.adapt does before its epochs): workspace + per-window feature cache allocated
+        # and touched here, so a driver-side clear of released VRAM cannot land in the first epoch
+        ctx.adapt_prepare(stream, 1)
+        prep = ctx.adapt_phases()  # (its reserve / cache-allocation phases)
+        ctx.set_option("adapt_phase_sync", 1)  # phase times below include GPU time (2 syncs per epoch)
         torch.cuda.synchronize()
+        setup_ms = (time.perf_counter() - ts) * 1e3
+        phases.append({"prepare_" + k: v for k, v in prep.items() if k in ("reserve_ms", "cache_alloc_ms")})
+        per_epoch, step, kern = [], 0, None
         for e in range(n_epochs):
             order = rng.permutation(n_train).astype(np.int32)[:steps or n_train]
             if timing and e == n_epochs - 1:
@@ -209,19 +220,20 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
                             adapt.MAX_GRAD_NORM, losses)
             torch.cuda.synchronize()
             per_epoch.append(time.perf_counter() - t0)
+            phases.append(ctx.adapt_phases())
             step += len(order)
         if timing:
             ctx.timing(False)
             kern = ctx.timing_collect()
         loss = float(losses[:len(order)].double().mean().item())
         ctx.close()
-        return per_epoch, loss, kern
+        return per_epoch, loss, kern, setup_ms, phases
 
     if warmup:
         run(1, steps=64)  # module load, first touch of a workspace
-    per_epoch, loss, _ = run(epochs)
+    per_epoch, loss, _, setup_ms, phases = run(epochs)
     assert np.isfinite(loss), loss
-    _, _, kern = run(2, steps=breakdown_steps, timing=True)  # epoch 1 fills the cache for the timed steps
+    _, _, kern, _, _ = run(2, steps=breakdown_steps, timing=True)  # epoch 1 fills the cache for the timed steps
     later = per_epoch[1:] or per_epoch
     out = {
         "metric": "regional adaptation ms per later-epoch sample-step (batch-1 fwd+bwd+clip+Adam, N=441, T=24)",
@@ -230,6 +242,14 @@ def adaptation_bench(d, P, ei, epochs=2, max_samples=1200, region="Amazon", brea
         "higher_is_better": False,
         "first_epoch_ms": per_epoch[0] * 1e3,
         "later_epoch_ms": float(np.mean(later)) * 1e3,
+        "setup_ms": setup_ms,
+        "setup_phases_ms": {k: round(v, 3) for k, v in phases[0].items()},
+        "epoch_phases_ms": [{k: round(v, 3) for k, v in ph.items()} for ph in phases[1:]],
+        "phases_note": "host-timed phases of each smaml_adapt_steps call (smaml_adapt_phases, option "
+                       "adapt_phase_sync: fill and steps end with a stream sync); setup_ms = context set-up "
+                       "incl. smaml_adapt_prepare (workspace reserve + feature-cache allocation, each touched "
+                       "and synced: setup_phases_ms), outside the epochs. Round 5's ~6 s first-epoch stall on "
+                       "some boxes was this allocation after the headline run released its ~250 GB",
         "sample_steps_per_s": n_train / float(np.mean(later)),
         "train_loss": loss,
         "config": {"workload": f"BASELINE config 4: {epochs}-epoch adaptation (adapt_hybrid_v5), epochs of {n_train} "
@@ -317,7 +337,7 @@ TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
 # timing category -> the kernel symbol its HIP-event brackets enclose
 KERNEL_SYMBOL = {"gcn_layer": "k_gcn_layer|k_gcn_mlp", "lstm_fwd_step": "k_lstm_fwd_step", "lstm_fwd_dual": "k_lstm_fwd_dual",
                  "head_loss": "k_head_loss|k_head_dual", "head_dh": "k_gemm_nn|k_gemm_nn_dual",
-                 "lstm_bwd_step": "k_lstm_bwd_step|k_lstm_bwd_push", "lstm_bwd_dual": "k_lstm_bwd_dual", "wgrad": "k_wgrad",
+                 "lstm_bwd_step": "k_lstm_bwd_step", "lstm_bwd_dual": "k_lstm_bwd_dual", "wgrad": "k_wgrad",
                  "wgrad_reduce": "k_wgrad_reduce", "xg_proj": "k_xg_dedup|k_gemm_nt",
                  "dg_rowsum": "k_dg_rowsum"}
 
@@ -392,6 +412,32 @@ def kernel_report(kern, steps, elapsed, rank_key):
                           "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] > 0 else 0.0,
                           "launches_per_step": v["launches"] / steps}
                       for k, v in kern.items() if v["launches"] > 0}
+    # every major category against both roofs: its f32-work rate over the product form's MFMA peak and its
+    # HBM bytes (committed PMC passes of this workload, per launch x launches) over 8 TB/s; categories whose
+    # sweeps ran as concurrent row chunks are timed by their sweeps' wall (<cat>_wall), not the summed chunks
+    rl = {}
+    for k, v in kern.items():
+        if k.endswith("_wall") or k == "misc" or v["launches"] == 0:
+            continue
+        wall = kern.get(k + "_wall", {})
+        t_ms = wall["ms"] if wall.get("launches") else v["ms"]
+        if t_ms <= 0:
+            continue
+        fam = CAT_FAMILY.get(k)
+        pk = (PEAK_X6_TFLOPS if forms.get(fam, 0) > 0 else PEAK_FP32_MFMA_TFLOPS) if fam else None
+        tf = v["flops"] / (t_ms * 1e-3) / 1e12
+        e = {"ms_per_step": t_ms / steps, "timed_by": "sweep wall" if wall.get("launches") else "kernel events",
+             "tflops": tf, "mfma_frac": (tf / pk) if (pk and v["flops"] > 0) else None}
+        tr = measured_traffic(k, rank_key)
+        if tr:
+            gbs = tr["bytes_per_launch"] * v["launches"] / (t_ms * 1e-3) / 1e9
+            e.update({"hbm_bytes_per_launch": tr["bytes_per_launch"], "hbm_tbs": gbs / 1e3, "hbm_frac": gbs / PEAK_HBM_GBS})
+        rl[k] = e
+    out["rooflines"] = rl
+    out["whole_step_executed_frac"] = out["achieved_tflops_executed"] / PEAK_X6_TFLOPS
+    out["rooflines_note"] = ("per category: mfma_frac = f32-work TFLOP/s / the product form's MFMA peak (419.5 for "
+                             "bf16x6); hbm_frac = PMC bytes per launch (profiles/traffic.json, this workload) x "
+                             "launches / time / 8 TB/s; whole_step_executed_frac = executed TFLOP/s / 419.5")
     if any(k.endswith("_wall") for k in out["kernels"]):
         out["kernels_note"] = ("LSTM sweeps whose diagonals ran as concurrent row chunks on side streams (options "
                                "bptt_streams / fwd_streams): their category's ms sums the chunks' kernel times, which "
@@ -583,7 +629,7 @@ def main():
             del ml
             torch.cuda.empty_cache()
         progress("config 5 rank share")
-        out["config5_rank_share"] = config5_share_bench(args.cfg5_share_tasks)
+        out["config5_rank_share"] = config5_share_bench(args.cfg5_share_tasks, timing=not args.no_timing)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

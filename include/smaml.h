@@ -184,6 +184,20 @@ int smaml_adapt_steps(smaml_ctx* ctx, void* stream, float* theta, float* m, floa
                       float beta1, float beta2, float eps, float weight_decay, float max_norm,
                       float* losses);
 
+/* Set-up half of smaml_adapt_steps, for callers that keep allocation out of their timed epochs
+ * (adaptModel builds its model and optimiser before the epoch loop, adapt_hybrid_v5.py:152-181):
+ * sizes the workspace for `batch`-sample steps and allocates the per-window GCN feature cache
+ * (batch 1), touching both once and synchronising `stream`. smaml_adapt_steps does the same on its
+ * first call when this was not called. No compute; the cache stays cold. */
+int smaml_adapt_prepare(smaml_ctx* ctx, void* stream, int32_t batch);
+
+/* Host-timed phases of the last smaml_adapt_steps call, in ms: [0] workspace reserve, [1] feature-
+ * cache allocation, [2] the batched feature-cache fill, [3] the step loop ([2] and [3] are enqueue
+ * times unless smaml_set_option("adapt_phase_sync", 1), which ends each with a stream sync).
+ * Writes min(cap, count) entries; *count = number of phases; *filled = windows whose features a
+ * step computed itself (outside the batched fill). Measurement only; no reference counterpart. */
+int smaml_adapt_phases(const smaml_ctx* ctx, double* ms, int32_t cap, int32_t* count, int64_t* filled);
+
 /* ---- finer-grained operators (the module pieces callers compose) -------- */
 
 /* Backward of the most recent smaml_forward (same theta): dpred [nsamples][N*Hf][C]
@@ -278,8 +292,8 @@ int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* cou
 /* Launch counts per kernel variant (tile configuration) since the last reset, in the order of
  * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
  * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
- * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, wgrad_ws, fwd_kw, bwd_kw, gcn_dedup,
- * xg_dedup, wgrad_dedup, f_compact, bwd_push, bwd_dual_push.
+ * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, fwd_kw, bwd_kw, gcn_dedup,
+ * xg_dedup, wgrad_dedup, f_compact, fwd_himg.
  * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
  * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
@@ -310,8 +324,6 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "barrier_oversize":            debug: > 0 launches the grid-barrier kernels with that many
  *                                  times the resident capacity (+1 block), which can never be
  *                                  co-resident, to exercise the bounded wait;
- *   "wgrad_ws":                    warp-specialised weight-gradient kernel where the shapes allow
- *                                  (1) or the staged one (0);
  *   "bwdd_remap":                  tangent BPTT tiles dealt in pair-segment order per XCD (1) or in
  *                                  hardware order (0; bitwise equal);
  *   "small_kw":                    small-grid (batch-1) LSTM forward / BPTT diagonals as one launch
@@ -322,6 +334,9 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  runs of up to this many consecutive missing windows per GCN pass
  *                                  (default 32; 0 or 1 = one window per step as it is first read;
  *                                  bitwise equal);
+ *   "adapt_phase_sync":            smaml_adapt_steps synchronises its stream after the feature-cache fill
+ *                                  and after the step loop so smaml_adapt_phases reports GPU time (0,
+ *                                  the default; measurement only);
  *   "gcn_dedup":                   smaml_meta_step steps whose every task reads B consecutive windows
  *                                  run the fused GCN rows t >= 1 once per distinct stream row and
  *                                  store each to every (sample, step) holding it (1, the default;
@@ -345,24 +360,14 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *                                  stream rows (xg_dedup forwards on the big tiles, wgrad_dedup
  *                                  backwards), the GCN stores each distinct row once instead of to every
  *                                  (sample, step) holding it (1, the default; bitwise equal to 0);
- *   "bptt_push":                   big-tile BPTT sweeps without LSTM dropout (primal, and the tangent sweep
- *                                  of a kept step) in the producer-side form: each step runs its cell
- *                                  backward from the dh partial sums its producers left, then forms its
- *                                  consumers' partial sums dG . W_hh and dG . W_ih, so every dG is read
- *                                  once as a GEMM operand instead of twice (1; 0 = the consumer-side
- *                                  form; equal up to f32 rounding: dh = Pup + Prec adds once more);
- *   "rowsum_side":                 after a chunked BPTT sweep, layer 0's dG row sums (wgrad_dedup) on a
- *                                  side stream beside the weight gradients of layers L-1 .. 1 (0, the
- *                                  default; bitwise equal to 1);
- *   "gcn_side", "reduce_side":     the fused GCN's t = 0 ELL chain beside k_gcn_mlp / each weight gradient's
- *                                  split-K reduce beside the next GEMM, on side streams (0, the default;
- *                                  bitwise equal to 1);
- *   "wgrad_min_kt":                split-K weight gradients: at least this many 16-k tiles per slice
- *                                  (default 8: the thread target decides);
- *   "wgrad_threads":               split-K weight gradients: the thread target of one launch (0, the
- *                                  default = 3072 x 256);
- *   "wgrad_overlap":               with row chunks, layer l's weight gradient on the caller's stream as
- *                                  soon as its BPTT is done (1) or after the sweep (0, the default). */
+ *   "h_img":                       a big-tile primal forward sweep with layer 0's XG table and the gate weight
+ *                                  images also writes each h(l, t) as the bf16-piece image of the gate GEMM's
+ *                                  A tiles, which the next diagonal copies into LDS with direct-to-LDS loads
+ *                                  instead of splitting f32 h in every workgroup (0, the default: measured
+ *                                  slower, the image writes cost the forward more than the split they
+ *                                  save; bitwise equal to 1).
+ *   (Round 6 removed the options of arms that measured slower -- bptt_push, wgrad_ws, rowsum_side,
+ *   gcn_side, reduce_side, wgrad_overlap, wgrad_min_kt, wgrad_threads; DESIGN.md keeps their A/B record.) */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

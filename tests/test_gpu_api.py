@@ -416,11 +416,9 @@ def test_gate_images_bitwise():
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("knob", ["wgrad_wide", "wgrad_pair", "wgrad_ws"])
+@pytest.mark.parametrize("knob", ["wgrad_wide", "wgrad_pair"])
 def test_wgrad_variants_match(knob):
-    """wgrad_ws: the warp-specialised weight gradients (k_wgrad_ws: 4 MFMA waves + 4 producer waves,
-    256 x 128 tiles), the default where the shapes allow, against the staged 256 x 256 / 512 x 128
-    tiles (different split-K slices: summation order only). wgrad_wide (with wgrad_ws off): weight
+    """wgrad_wide: weight
     gradients with 256-column problems (LSTM layers >= 1 and their tangent passes) on 256 x 256 tiles
     (kernels.hip CfgTW); the 512 x 128 tiles give the same weight sums (same split-K slices, same
     per-element MFMA order) and the bias column sums up to summation order. wgrad_pair: the tangent
@@ -439,8 +437,6 @@ def test_wgrad_variants_match(knob):
     for on in (1, 0):
         ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=None)
         ml.set_tasks(feats)
-        if knob == "wgrad_wide":
-            ml.ctx.set_option("wgrad_ws", 0)
         ml.ctx.set_option(knob, on)
         ml.ctx.variant_counts(reset=True)
         res = ml.meta_step()
@@ -495,8 +491,7 @@ def test_stgcn_autograd_matches_oracle(d, p):
 
 
 @pytest.mark.parametrize("knob", ["bwdd_remap", "gcn_dedup", "gcn_dedup_layers", "bptt_streams", "fwd_streams",
-                                  "f_compact", "f_compact_layers", "rowsum_side", "gcn_side",
-                                  "reduce_side"])
+                                  "f_compact", "f_compact_layers", "h_img"])
 def test_order_only_knobs_bitwise(knob):
     """Knobs that only reorder or deduplicate work (bwdd_remap: the tangent BPTT's pair-segment tile
     order per XCD; gcn_dedup: the fused GCN rows of consecutive windows once per distinct stream row,
@@ -505,16 +500,15 @@ def test_order_only_knobs_bitwise(knob):
     fwd_streams: every BPTT / forward diagonal in two row chunks on side streams, always on the big tiles,
     the weight gradients after the sweep; f_compact: the features of those steps stored once per distinct
     stream row, read only through the layer-0 projection tables and the gathered dW_ih0 -- fused and per-layer
-    GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles; rowsum_side: after a chunked
-    sweep, layer 0's dG row sums on a side stream beside the upper layers' weight gradients; gcn_side: the
-    fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp; reduce_side: each weight gradient's
-    split-K reduce on a side stream beside the next GEMM, two partial slabs) leave every
+    GCN paths, 2 tasks x B = 8 so every layer-0 diagonal runs the big tiles; h_img: the primal forward hands
+    h to the next diagonal as pre-split bf16 images copied into LDS, the same pieces the gate kernel's own
+    split forms) leave every
     row's arithmetic unchanged: a second-order meta-step (big tangent BPTT tiles forced, every primal
     kept) is bitwise equal with the knob on and off."""
     from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
 
     d = CONFIG2
-    compact = knob.startswith("f_compact") or knob in ("rowsum_side", "reduce_side")
+    compact = knob.startswith("f_compact")
     cfg = MamlConfig(inner_steps=2, batch=8 if compact else 4, order=2)
     P = synth.init_params(47, d, gcn_bias_scale=0.1)
     Ptr, Pg, _ = split(P)
@@ -527,8 +521,6 @@ def test_order_only_knobs_bitwise(knob):
         ml.ctx.set_option("bwdd_big_min", 0)
         if knob.endswith("_layers"):
             ml.ctx.set_option("gcn_fused", 0)
-        if knob in ("rowsum_side", "reduce_side"):
-            ml.ctx.set_option("bwd_big_min", 0)  # (every sweep chunked: the row sums follow the joined sweep)
         if knob.endswith("_streams"):
             ml.ctx.set_option("bwd_big_min", 0)  # (chunked diagonals always run the big tiles: both arms do)
             ml.ctx.set_option(knob, 2 if on else 1)
@@ -542,7 +534,59 @@ def test_order_only_knobs_bitwise(knob):
             assert (vc["gcn_dedup"] > 0) == bool(on), vc
         if knob.startswith("f_compact"):  # every step: K inner steps + the query; the sweep reads them from so_F
             assert vc["f_compact"] == (cfg.inner_steps + 1 if on else 0), vc
+        if knob == "h_img":  # every diagonal of the K inner steps' and the query's primal forwards
+            assert vc["fwd_himg"] == ((cfg.inner_steps + 1) * (d.window_size + d.lstm_num_layers - 1) if on else 0), vc
         out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
         del ml
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
+def test_row_chunks_bitwise_cfg5_corner_diagonals():
+    """The configuration that raced in round 5 (DESIGN.md "row chunks on side streams"): BASELINE config-5
+    shapes (N = 1024, Hc = 512), ONE task, B = 12, so the 4-problem BPTT diagonals are big by the default
+    tile threshold while the 1-problem corner diagonals are not -- with row chunks every chunked diagonal
+    must still run the row-restricted big tiles, or a whole-row launch on one stream would race the other
+    stream's chunk. Forward and BPTT chunks on (fwd_streams = bptt_streams = 2, default thresholds) against
+    one stream with the big tiles forced everywhere: the K = 2 second-order meta-step is bitwise equal,
+    and the launch counters show every diagonal, the corners included, on the big tiles
+    (hybrid_model.py:93-102 / train_hybrid_maml_v5.py:134 through the wavefront)."""
+    from weatherforecast_stgcn_maml_amd.config import CONFIG5
+    from weatherforecast_stgcn_maml_amd.maml import MetaLearner, stream_len_for
+
+    d = CONFIG5
+    cfg = MamlConfig(inner_steps=2, batch=12, order=2)
+    K, diags = cfg.inner_steps, d.window_size + d.lstm_num_layers - 1
+    P = synth.init_params(61, d, gcn_bias_scale=0.1)
+    Ptr, Pg, _ = split(P)
+    ei = grid_edges(d)
+    feats = [synth.make_features(6100, d.num_nodes, stream_len_for(cfg, d))]
+    out = []
+    for chunks in (2, 1):
+        ml = MetaLearner(d, cfg, Pg, Ptr, ei, device=DEV, task_group=1)
+        ml.set_tasks(feats)
+        ml.ctx.set_option("fwd_streams", chunks)
+        ml.ctx.set_option("bptt_streams", chunks)
+        if chunks == 1:  # (the one-stream arm on the big tiles everywhere, as every chunked diagonal runs)
+            ml.ctx.set_option("bwd_big_min", 0)
+            ml.ctx.set_option("bwdd_big_min", 0)
+        ml.ctx.variant_counts(reset=True)
+        ml.ctx.timing_collect()
+        ml.ctx.timing(True)
+        res = ml.meta_step()
+        kern = ml.ctx.timing_collect()
+        ml.ctx.timing(False)
+        vc = ml.ctx.variant_counts()
+        assert vc["bwd_big"] == (K + 1) * diags and vc["bwd_small"] == 0 and vc["bwd_split"] == 0, vc
+        assert vc["bwd_dual_big_kept"] == K * diags and vc["bwd_dual_small_kept"] == 0, vc
+        assert vc["fwd"] == (K + 1) * diags and vc["fwd_split"] == 0 and vc["fwd_kw"] == 0, vc
+        walls = {k for k, v in kern.items() if k.endswith("_wall") and v["launches"] > 0}
+        if chunks == 2:  # every sweep ran chunked: primal forward / BPTT, tangent forward / BPTT
+            assert walls == {"lstm_fwd_step_wall", "lstm_bwd_step_wall", "lstm_fwd_dual_wall", "lstm_bwd_dual_wall"}, kern
+        else:
+            assert not walls, kern
+        out.append((res.losses.cpu(), res.norms.cpu(), ml.meta_grad.cpu().clone()))
+        del ml
+        torch.cuda.empty_cache()
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)

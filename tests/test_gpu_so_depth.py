@@ -105,46 +105,6 @@ def test_second_order_k5_cfg2_bench_tiles(keep):
     check(res, ml, ref, d, names, 2, K)
 
 
-@pytest.mark.parametrize("keep", [-1, 3])
-def test_bptt_push_k5_cfg2_against_oracle_and_pull(keep):
-    """Push BPTT (option bptt_push; kernels.hip k_lstm_bwd_push, kernels_dual.hip k_lstm_bwd_dual_push):
-    each step's cell backward runs from the dh partial sums its producers left (Pup from the layer above,
-    Prec from the next step), then its own dG . W_hh and dG . W_ih become its consumers' partial sums
-    (and, in the tangent sweep of a kept step, R(dG) . W + dG . U) -- train_hybrid_maml_v5.py:134's
-    loss.backward through the LSTM, regrouped. The K = 5 configuration above with the bench tiles on every
-    diagonal: every primal sweep (K inner steps + the query) and every kept tangent sweep runs the push
-    form, the recomputed-primal steps (keep 3) the pull form; against the oracle at the parity tolerances
-    and against bptt_push 0 to f32 rounding."""
-    d, cfg = CONFIG2, K5_CFG
-    P = synth.init_params(23, d, gcn_bias_scale=0.1)
-    theta, gcn, names = split(P)
-    ei = grid_edges(d)
-    feats = [synth.make_features(2300 + j, d.num_nodes, stream_len_for(cfg, d)) for j in range(2)]
-    out = {}
-    for push in (1, 0):
-        ml = MetaLearner(d, cfg, gcn, theta, ei, device=DEV, task_group=1)
-        ml.set_tasks(feats)
-        ml.ctx.set_option("bwd_big_min", 0)
-        ml.ctx.set_option("bwdd_big_min", 0)
-        ml.ctx.set_option("keep", keep)
-        ml.ctx.set_option("bptt_push", push)
-        ml.ctx.variant_counts(reset=True)
-        res = ml.meta_step()
-        vc = ml.ctx.variant_counts()
-        K, G = cfg.inner_steps, len(ml._groups)
-        kept = K if keep < 0 else keep
-        if push:
-            assert vc["bwd_push"] == G * (K + 1) * DIAGS and vc["bwd_big"] == 0, vc
-            assert vc["bwd_dual_push"] == G * kept * DIAGS and vc["bwd_dual_big"] == G * (K - kept) * DIAGS, vc
-            ref = oracle("k5", d, P, names, feats, ei, cfg, list(ml.default_windows()[-1, 0]))
-            check(res, ml, ref, d, names, 2, K)
-        else:
-            assert vc["bwd_push"] == vc["bwd_dual_push"] == 0, vc
-        out[push] = (res.losses.cpu().numpy(), res.norms.cpu().numpy(), ml.meta_grad.cpu().numpy().copy())
-    for a, b in zip(out[1], out[0]):
-        assert rel(a, b) < 1e-5
-
-
 # ----------------------------------------------------------------------------- (b) config 5, K = 10
 def test_second_order_k10_cfg5():
     """BASELINE config-5 shapes (N=1024, Hc=512, LSTM 4x128), 1 task x B=1 x K=10, every inner

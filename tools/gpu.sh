@@ -13,7 +13,8 @@
 #                   (TASKS, default 15; CONFIG 2 or 5; tools/prof_summary.py reads the directory)
 #   pmc_sq          SQ instruction-mix / MFMA-busy counters of the same workload (one --pmc pass)
 #   shares          one-GPU timings of rank 0's share at N = 2 / 4 / 8 (8 / 4 / 2 tasks)
-#   ab              A/B: AB_VARIANTS (words "lib:<file in the package dir>" or "opt:<k=v[,k=v]>", "base" =
+#   ab              A/B: AB_VARIANTS (words "lib:<file in the package dir>", "opt:<k=v[,k=v]>" or both as
+#                   "lib:<file>+opt:<k=v>", "base" =
 #                   the default library) each in its own process, AB_ROUNDS interleaved rounds of
 #                   bench.py $AB_ARGS                      -> gpurun_out/$TAG/ab.log
 # TAG names the output directory (default "session").
@@ -91,6 +92,7 @@ for s in "$@"; do
       for round in $(seq 1 "${AB_ROUNDS:-2}"); do
         for v in ${AB_VARIANTS:-base}; do
           case $v in
+            lib:*+opt:*) l=${v#lib:}; envs=(SMAML_LIB=$PKG/${l%%+opt:*} SMAML_OPTIONS=${l#*+opt:}) ;;
             lib:*) envs=(SMAML_LIB=$PKG/${v#lib:}) ;;
             opt:*) envs=(SMAML_OPTIONS=${v#opt:}) ;;
             *) envs=() ;;

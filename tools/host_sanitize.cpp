@@ -174,7 +174,7 @@ static void check_barrier_grid() {
 }
 
 int main() {
-  CHECK(smaml_abi_version() == 6);
+  CHECK(smaml_abi_version() == 7);
   check_waves();
   check_wgrad_plans();
   check_barrier_grid();

@@ -23,7 +23,7 @@ CATEGORIES = {
     "gcn_layer": r"k_gcn_layer|k_gcn_mlp|k_gcn_expand|k_gcn_compact",
     "lstm_fwd_step": r"k_lstm_fwd_step",
     "lstm_fwd_dual": r"k_lstm_fwd_dual",
-    "lstm_bwd_step": r"k_lstm_bwd_step|k_lstm_bwd_push",
+    "lstm_bwd_step": r"k_lstm_bwd_step",
     "lstm_bwd_dual": r"k_lstm_bwd_dual",
     "wgrad": r"k_wgrad$|k_wgrad\b(?!_)",
     "wgrad_reduce": r"k_wgrad_reduce",

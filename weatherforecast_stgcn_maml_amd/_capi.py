@@ -24,15 +24,15 @@ EXPORTS = (
     "smaml_clip_sgd", "smaml_inner_loop", "smaml_alloc", "smaml_free", "smaml_comm_unique_id",
     "smaml_comm_init", "smaml_comm_allreduce", "smaml_comm_destroy", "smaml_variant_counts", "smaml_set_option",
     "smaml_dropout", "smaml_sync", "smaml_gcn_conv_ex", "smaml_gcn_conv_backward", "smaml_relu_mask",
+    "smaml_adapt_prepare", "smaml_adapt_phases",
 )
-ABI_VERSION = 6
+ABI_VERSION = 7
 GCN_RELU, GCN_PLAIN = 1, 2  # smaml_gcn_conv_ex / _backward flags
 
 # kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
 VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kept", "fwd_dual_img", "bwd_big", "bwd_small", "bwd_split",
             "bwd_dual_big", "bwd_dual_big_kept", "bwd_dual_small", "bwd_dual_small_kept", "wgrad", "wgrad_wide", "wgrad_pair",
-            "wgrad_ws", "fwd_kw", "bwd_kw", "gcn_dedup", "xg_dedup", "wgrad_dedup",
-            "f_compact", "bwd_push", "bwd_dual_push")
+            "fwd_kw", "bwd_kw", "gcn_dedup", "xg_dedup", "wgrad_dedup", "f_compact", "fwd_himg")
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",
@@ -115,7 +115,11 @@ _SIGS = {
     "smaml_gcn_conv_ex": ([P, P, P, I32, I32, P, P, I32, I32, P], I32),
     "smaml_gcn_conv_backward": ([P, P, P, I32, I32, P, I32, P, I32, P, P], I32),
     "smaml_relu_mask": ([P, P, P, P, I64], I32),
+    "smaml_adapt_prepare": ([P, P, I32], I32),
+    "smaml_adapt_phases": ([P, ctypes.POINTER(ctypes.c_double), I32, PI32, PI64], I32),
 }
+# smaml_adapt_phases order (api.cpp AdPhases)
+ADAPT_PHASES = ("reserve_ms", "cache_alloc_ms", "cache_fill_ms", "steps_ms")
 
 
 def lib():
@@ -297,6 +301,19 @@ class Context:
         check(self._L.smaml_adapt_steps(self._h, stream, ptr(theta), ptr(m), ptr(v), int(step0), w.shape[0],
                                         w.shape[1], w.ctypes.data_as(PI32), ptr(lr_dev), float(betas[0]),
                                         float(betas[1]), float(eps), float(wd), float(max_norm), ptr(losses)))
+
+    def adapt_prepare(self, stream, batch=1):
+        """Workspace + per-window feature cache for adapt_steps, allocated and touched now (no compute)."""
+        check(self._L.smaml_adapt_prepare(self._h, stream, int(batch)))
+
+    def adapt_phases(self):
+        """{phase: ms} of the last adapt_steps call (+ 'windows_filled_per_step')."""
+        ms = (ctypes.c_double * len(ADAPT_PHASES))()
+        n, filled = ctypes.c_int32(), ctypes.c_int64()
+        check(self._L.smaml_adapt_phases(self._h, ms, len(ADAPT_PHASES), ctypes.byref(n), ctypes.byref(filled)))
+        out = {k: ms[i] for i, k in enumerate(ADAPT_PHASES[:n.value])}
+        out["windows_filled_per_step"] = filled.value
+        return out
 
     def backward(self, stream, theta, dpred, grad):
         check(self._L.smaml_backward(self._h, stream, ptr(theta), ptr(dpred), ptr(grad)))

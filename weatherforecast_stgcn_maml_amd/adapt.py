@@ -124,6 +124,8 @@ def adapt(dims: ModelDims, features, edge_index, gcn: dict, theta: dict, region_
     step = 0
     losses = torch.empty(max(n_train, 1), device=dev)
     ctx.set_task_ids([0])
+    ctx.set_dropout(dropout[0], dropout[1], dropout_seed)
+    ctx.adapt_prepare(stream, 1)  # workspace + feature cache before the first epoch (setup, no compute)
     for _ in range(epochs):
         ctx.set_dropout(dropout[0], dropout[1], dropout_seed)  # masks keyed by the global step index
         ep = len(res.epoch_losses)

@@ -213,7 +213,6 @@ static Knobs default_knobs() {
   k.gate_img = SMAML_GATE_IMG;
   k.wgrad_wide = 1;
   k.wgrad_pair = SMAML_WGRAD_PAIR;
-  k.wgrad_ws = SMAML_WGRAD_WS_DEFAULT;
   k.bwdd_remap = SMAML_BWDD_REMAP_DEFAULT;
   k.small_kw = SMAML_SMALL_KW;
   k.gcn_dedup = 1;
@@ -221,16 +220,19 @@ static Knobs default_knobs() {
   k.wgrad_dedup = SMAML_WGRAD_DEDUP_DEFAULT;
   k.bptt_streams = SMAML_BPTT_STREAMS_DEFAULT;
   k.fwd_streams = SMAML_FWD_STREAMS_DEFAULT;
-  k.wgrad_overlap = 0;
-  k.bptt_push = SMAML_BPTT_PUSH_DEFAULT;
-  k.wgrad_min_kt = SMAML_WGRAD_MIN_KT;
-  k.wgrad_threads = 0;
-  k.gcn_side = SMAML_GCN_SIDE_DEFAULT;
-  k.reduce_side = SMAML_REDUCE_SIDE_DEFAULT;
-  k.rowsum_side = SMAML_ROWSUM_SIDE_DEFAULT;
   k.f_compact = SMAML_F_COMPACT_DEFAULT;
+  k.h_img = SMAML_H_IMG_DEFAULT;
   return k;
 }
+
+// Host-timed phases of one smaml_adapt_steps call (smaml_adapt_phases): workspace reserve, feature-cache
+// allocation, the batched cache fill, the step loop. The last two are enqueue times unless the option
+// adapt_phase_sync is on (then each ends with a stream sync and includes the GPU time).
+enum { AD_RESERVE = 0, AD_ALLOC, AD_FILL, AD_STEPS, AD_NPH };
+struct AdPhases {
+  double ms[AD_NPH] = {};
+  int64_t filled = 0;  // windows computed by a per-step GCN pass (not the batched fill)
+};
 
 struct smaml_ctx {
   smaml_dims dims{};
@@ -277,6 +279,7 @@ struct smaml_ctx {
   int64_t so_store_cap = 0, so_nc_cap = 0;
   float* so_F = nullptr;  // [K][Z][T][M][Hc] GCN features of every inner step (null: recompute)
   int64_t so_F_cap = 0;
+  std::vector<int8_t> so_fc;  // per inner step: whether run_gcn wrote its so_F slot compact (Work::fcompact)
   float* F_main = nullptr;  // the workspace's own F buffer
   // batch-1 adaptation: GCN features per window of task 0 (the frozen GCN stack without dropout
   // is a pure function of the window, F2), filled on first use and reused by later epochs.
@@ -290,18 +293,8 @@ struct smaml_ctx {
   int64_t xg_cap = 0;
   float* xgd_buf = nullptr;   // big-tile forward: layer 0's projection per distinct stream row (prep_xg_dedup)
   int64_t xgd_cap = 0;
-  // reduce_side: a second partial slab and the events that order the two slabs' GEMMs and reduces
-  struct {
-    bool on = false;
-    int next = 0;
-    bool pending[2] = {false, false};
-    bool failed = false;  // an event call failed: the rest ran on s, reduce_side_end reports it
-    hipEvent_t gemm[2] = {}, done[2] = {};
-  } red;
-  float* wpart2 = nullptr;
-  int64_t wpart2_cap = 0;
-  float* push_buf = nullptr;  // push BPTT partial sums: primal [3][L][Z][M][H], then tangent (push_partials)
-  int64_t push_cap = 0;
+  char* himg_buf = nullptr;   // big-tile forward: pre-split h images, a ring of two steps per layer (prep_h_img)
+  int64_t himg_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
   // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
   unsigned* bar = nullptr;
@@ -315,6 +308,8 @@ struct smaml_ctx {
   int64_t ad_cap = 0;              // windows the cache holds
   std::vector<uint8_t> ad_valid;   // per window start
   int ad_gcn_batch = 32;           // windows per GCN pass when filling the cache (<= 1: one per step)
+  int ad_phase_sync = 0;           // smaml_set_option("adapt_phase_sync"): sync at the phase boundaries
+  AdPhases ad_ph;                  // host-timed phases of the last smaml_adapt_steps (smaml_adapt_phases)
   float *Hs_main = nullptr, *Cs_main = nullptr, *Gs_main = nullptr;  // the workspace's own activations
   // primal of the last inner steps kept for the second-order sweep (ensure_keep): slot 0 adds
   // dG + dh to the workspace's Hs/Cs/Gs, slot i >= 1 holds Hs/Cs/Gs/dG/dh of its own
@@ -336,7 +331,6 @@ struct smaml_ctx {
   // side streams of the row-chunked BPTT (knob bptt_streams) and their fork / join events
   hipStream_t cs[4] = {};
   hipEvent_t fork_ev = nullptr, join_ev[4] = {};
-  hipEvent_t lay_ev[MAX_LAYERS][4] = {};  // wgrad_overlap: layer l's BPTT done on chunk stream i
   // RCCL communicator (smaml_comm_init), opaque; created non-blocking when the library allows it
   void* comm = nullptr;
   int comm_nb = 0;
@@ -632,7 +626,6 @@ void set_work(smaml_ctx* c, int Z, int B) {
   c->w.primal_kept = 0;
   c->w.consec = 0;
   c->w.fcompact = 0;
-  c->w.push = 0;
   c->w.drop = Drop{};  // dropout only inside smaml_meta_step / smaml_adapt_steps (set_step_drop)
   c->w.vcount = c->vcount;
   c->w.kn = c->kn;
@@ -655,72 +648,10 @@ void set_work(smaml_ctx* c, int Z, int B) {
 // Weight gradient = split-K GEMM (C_WGRAD) + fixed-order reduce (C_WGRAD_RED).
 int fork_streams(smaml_ctx* c, hipStream_t s, int n);
 
-// One weight gradient's split-K GEMM + reduce. With reduce_side on (after a chunked sweep) the reduce
-// runs on side stream cs[1] behind an event, the GEMMs alternate between the two partial slabs, and a
-// GEMM waits for the reduce that last read its slab; reduce_side_end makes s wait for them all.
+// One weight gradient's split-K GEMM + reduce, in order on s.
 void wgrad_run(smaml_ctx* c, hipStream_t s, double fl, WgradPlan& p) {
-  if (!c->red.on) {
-    TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
-    TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
-    return;
-  }
-  const int b = c->red.next;
-  c->red.next ^= 1;
-  if (b) p.part = c->wpart2;
-  if (c->red.pending[b] && hipStreamWaitEvent(s, c->red.done[b], 0) != hipSuccess) {
-    // the slab's last reader cannot be ordered by an event: drain the side stream, then carry on on s
-    (void)hipStreamSynchronize(c->cs[1]);
-    c->red.failed = true;
-  }
   TIMED(c, s, C_WGRAD, fl, launch_wgrad_gemm(s, p));
-  if (c->red.failed || hipEventRecord(c->red.gemm[b], s) != hipSuccess ||
-      hipStreamWaitEvent(c->cs[1], c->red.gemm[b], 0) != hipSuccess) {
-    c->red.failed = true;
-    TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));  // (in order on s)
-    c->red.pending[b] = false;
-    return;
-  }
-  TIMED(c, c->cs[1], C_WGRAD_RED, 0, launch_wgrad_reduce(c->cs[1], p));
-  c->red.pending[b] = hipEventRecord(c->red.done[b], c->cs[1]) == hipSuccess;
-  if (!c->red.pending[b]) {
-    (void)hipStreamSynchronize(c->cs[1]);
-    c->red.failed = true;
-  }
-}
-
-bool reduce_side_begin(smaml_ctx* c, hipStream_t s) {
-  c->red.on = false;
-  if (!c->kn.reduce_side) return false;
-  const int64_t need = c->w.wpart_floats;
-  if (need > c->wpart2_cap) {
-    if (c->wpart2) (void)hipFree(c->wpart2);
-    c->wpart2 = nullptr;
-    c->wpart2_cap = 0;
-    if (hipMalloc((void**)&c->wpart2, need * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    c->wpart2_cap = need;
-  }
-  for (int i = 0; i < 2; ++i) {
-    if (!c->red.gemm[i] && hipEventCreateWithFlags(&c->red.gemm[i], hipEventDisableTiming) != hipSuccess) return false;
-    if (!c->red.done[i] && hipEventCreateWithFlags(&c->red.done[i], hipEventDisableTiming) != hipSuccess) return false;
-  }
-  if (fork_streams(c, s, 2) != SMAML_OK) return false;  // (creates cs[1]; it starts behind s's work so far)
-  c->red.on = true;
-  c->red.next = 0;
-  c->red.failed = false;
-  c->red.pending[0] = c->red.pending[1] = false;
-  return true;
-}
-
-int reduce_side_end(smaml_ctx* c, hipStream_t s) {
-  if (!c->red.on) return SMAML_OK;
-  c->red.on = false;
-  for (int i = 0; i < 2; ++i)
-    if (c->red.pending[i]) HIP_TRY(hipStreamWaitEvent(s, c->red.done[i], 0));
-  if (c->red.failed) return fail(SMAML_EHIP, "reduce_side: an event call failed (the reduces ran in order on s)");
-  return SMAML_OK;
+  TIMED(c, s, C_WGRAD_RED, 0, launch_wgrad_reduce(s, p));
 }
 
 void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t a_zstride, int Mrows,
@@ -734,7 +665,6 @@ void timed_wgrad(smaml_ctx* c, hipStream_t s, double fl, const float* A, int64_t
   p.drop_layer = drop_layer;
   count_variant(c->w, V_WGRAD);
   if (p.wide) count_variant(c->w, V_WGRAD_WIDE);
-  if (p.ws) count_variant(c->w, V_WGRAD_WS);
   wgrad_run(c, s, fl, p);
 }
 
@@ -752,7 +682,6 @@ bool timed_wgrad_pair(smaml_ctx* c, hipStream_t s, double fl, const float* RdG, 
   p.drop_layer = drop_layer;
   count_variant(c->w, V_WGRAD);
   if (p.wide) count_variant(c->w, V_WGRAD_WIDE);
-  if (p.ws) count_variant(c->w, V_WGRAD_WS);
   count_variant(c->w, V_WGRAD_PAIR);
   wgrad_run(c, s, fl, p);
   return true;
@@ -797,16 +726,6 @@ void time_wall(smaml_ctx* c, hipStream_t s, hipEvent_t a, int cat, double fl) {
   c->tm.recs.push_back({cat, a, b, fl});
 }
 
-// s waits for what the side streams have issued so far (layer l's events; the streams go on)
-int wait_streams_layer(smaml_ctx* c, hipStream_t s, int n, int l) {
-  for (int i = 0; i < n; ++i) {
-    if (!c->lay_ev[l][i]) HIP_TRY(hipEventCreateWithFlags(&c->lay_ev[l][i], hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(c->lay_ev[l][i], c->cs[i]));
-    HIP_TRY(hipStreamWaitEvent(s, c->lay_ev[l][i], 0));
-  }
-  return SMAML_OK;
-}
-
 // s waits for everything issued on the side streams
 int join_streams(smaml_ctx* c, hipStream_t s, int n) {
   for (int i = 0; i < n; ++i) {
@@ -831,34 +750,6 @@ float* xgd_scratch(smaml_ctx* c, int64_t floats) {
   return c->xgd_buf;
 }
 
-// Whether this BPTT sweep runs in the push form (knob bptt_push, kernels.hip k_lstm_bwd_push): every
-// diagonal on the big tiles (row chunks force them; else each diagonal's own size), no LSTM dropout,
-// the tangent sweep only for a kept step; points the Work at the partial-sum buffers (allocated here,
-// both sets at once so the tangent sweep never reallocates under the primal's; no room: pull form).
-bool push_sweep(smaml_ctx* c, bool dual, int nch) {
-  const Dims& d = c->d;
-  Work& w = c->w;
-  if (!c->kn.bptt_push || (!dual && c->kn.bptt_push == 2) || w.drop.lstm() || (dual && !w.primal_kept)) return false;
-  for (int e = 0; nch <= 1 && e < d.T + d.L - 1; ++e)
-    if (!(dual ? bwd_dual_wave_big(d, w, c->po, e) : bwd_wave_big(d, w, c->po, e))) return false;
-  const int64_t set = 3ll * d.L * w.Z * w.M * d.H;
-  if (2 * set > c->push_cap) {
-    if (c->push_buf) (void)hipFree(c->push_buf);
-    c->push_buf = nullptr;
-    c->push_cap = 0;
-    if (hipMalloc((void**)&c->push_buf, 2 * set * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    c->push_cap = 2 * set;
-  }
-  const int64_t lz = (int64_t)d.L * w.Z * w.M * d.H;
-  float* b = c->push_buf + (dual ? set : 0);
-  (dual ? w.RPrec : w.Prec) = b;
-  (dual ? w.RPup : w.Pup) = b + lz;
-  return true;
-}
-
 // Whether this step's layer-0 input-weight gradient runs over distinct stream rows (wgrad_dedup).
 bool wgrad_dedup_ok(const smaml_ctx* c) {
   const Work& w = c->w;
@@ -869,19 +760,17 @@ bool wgrad_dedup_ok(const smaml_ctx* c) {
 // S = row sums of dGl (layer 0's dG or R(dG), k_dg_rowsum, in the scratch), then ONE gathered split-K
 // GEMM into grad's W_ih0 block (no bias; written, not accumulated). False: no scratch (the caller runs
 // the full-row form).
-// summed: the row sums are already in the scratch (rowsum_side, launched by the caller).
-bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float* grad, bool summed = false) {
+bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float* grad) {
   const Dims& d = c->d;
   Work& w = c->w;
   const int64_t rows = xg_dedup_rows(w.B, d.T, d.N), TM = (int64_t)d.T * w.M;
-  float* S = summed ? c->xgd_buf : xgd_scratch(c, rows * 4 * d.H * w.Z);
+  float* S = xgd_scratch(c, rows * 4 * d.H * w.Z);
   if (!S) return false;
   const LayerOff& lo = c->po.lay[0];
-  if (!summed) TIMED(c, s, C_DGSUM, 0, launch_dg_rowsum(s, d, w, dGl, TM * 4 * d.H, S));
+  TIMED(c, s, C_DGSUM, 0, launch_dg_rowsum(s, d, w, dGl, TM * 4 * d.H, S));
   WgradPlan p;
   plan_wgrad(w, S, rows * 4 * d.H, 4 * d.H, w.F, TM * lo.cin, lo.cin, nullptr, 0, 0, rows, 0, grad, c->po.P, lo.wih, -1,
              -1, -1, false, false, p);
-  p.ws = false;
   p.gather = WgGather{w.M, d.N, d.T, FastDiv((uint32_t)d.N), w.fcompact};
   count_variant(w, V_WGRAD);
   count_variant(w, V_WGRAD_DEDUP);
@@ -890,28 +779,12 @@ bool timed_wgrad_ih0_dedup(smaml_ctx* c, hipStream_t s, const float* dGl, float*
   return true;
 }
 
-// rowsum_side: layer 0's dG row sums on side stream cs[0], forked from s now (the sweep is joined), so
-// they run beside the weight gradients of layers L-1 .. 1; s waits for join_ev[0] before layer 0's
-// gathered weight gradient. False: not applicable (the caller sums on s as usual).
-bool rowsum_side(smaml_ctx* c, hipStream_t s, const float* dGl) {
-  const Dims& d = c->d;
-  Work& w = c->w;
-  if (!c->kn.rowsum_side || !wgrad_dedup_ok(c)) return false;
-  const int64_t rows = xg_dedup_rows(w.B, d.T, d.N), TM = (int64_t)d.T * w.M;
-  float* S = xgd_scratch(c, rows * 4 * d.H * w.Z);
-  if (!S || fork_streams(c, s, 1) != SMAML_OK) return false;
-  TIMED(c, c->cs[0], C_DGSUM, 0, launch_dg_rowsum(c->cs[0], d, w, dGl, TM * 4 * d.H, S));
-  if (hipEventRecord(c->join_ev[0], c->cs[0]) == hipSuccess) return true;
-  (void)hipStreamSynchronize(c->cs[0]);  // (no event to order by: the caller sums again on s, after this one)
-  return false;
-}
-
 // Whether a consecutive-window step's features may be stored compact (Work::fcompact, the distinct rows
 // only, XgDedup order): every reader of F must then take those rows -- the forwards' layer-0 gates through
 // the k_xg_dedup tables (every layer-0 diagonal on the big tiles; the tangent forward always reads them),
 // the backwards' dW_ih0 through the gathered form (not the grouped small-grid launch) -- with the
 // scratch for both tables reserved here, so neither reader can miss it later. Deterministic in the
-// step's state: the tangent sweep re-derives the flag of a step whose features it reads from so_F.
+// step's state; the tangent sweep reuses the flag recorded when a step's so_F slot was written (so_fc).
 bool f_compact_ok(smaml_ctx* c, bool consec) {
   const Dims& d = c->d;
   const Work& w = c->w;
@@ -953,21 +826,17 @@ int run_gcn(smaml_ctx* c, hipStream_t s, const float* const* xtab_dev, const flo
     const bool dedup = consec && c->kn.gcn_dedup && w.B > 1 && !w.drop.gcn();
     if (dedup) count_variant(w, V_GCN_DEDUP);
     const double rows1 = dedup ? (double)w.Z * (w.B + d.T - 2) * d.N : (double)zb * (d.T - 1) * d.N;
-    // the t = 0 rows' ELL chain touches rows the fused kernel does not: on a side stream beside it (gcn_side)
-    const bool side = c->kn.gcn_side && fork_streams(c, s, 1) == SMAML_OK;
-    hipStream_t s0 = side ? c->cs[0] : s;
     TIMED(c, s, C_GCN, 2.0 * rows1 * d.Hc * (d.Cin0 + 3.0 * d.Hc),
           launch_gcn_mlp(s, d, zb, w.B, xtab_dev, c->gcn, wo, c->gcn_wimg, w.F, &w.drop, dedup, w.fcompact));
     for (int k = 0; k < 4; ++k) {  // t = 0 rows: N-row blocks, masks indexed as rows of T*N-row samples
       const bool last = k == 3;
       float* dst = last ? w.F : bufs[k & 1];
-      TIMED(c, s0, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
-            launch_gcn_layer(s0, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
+      TIMED(c, s, C_GCN, 2.0 * zb * d.N * c->go.cin[k] * d.Hc,
+            launch_gcn_layer(s, d, k, zb, w.B, k == 0 ? xtab_dev : nullptr, src, dst, last, true,
                              c->gcn + c->go.w[k], c->gcn + c->go.b[k], c->go.cin[k], d.Hc, c->ell_c, c->ell_v,
                              d.N, d.N, &w.drop, rps));
       src = dst;
     }
-    if (side) TRY(join_streams(c, s, 1));
     HIP_TRY(hipGetLastError());
     return SMAML_OK;
   }
@@ -1119,6 +988,35 @@ bool prep_xg_dedup(smaml_ctx* c, hipStream_t s, bool consec, const float* theta,
   return true;
 }
 
+// Pre-split h images for this forward sweep (kernels.h HImgs, option h_img): only when EVERY diagonal runs
+// the big-tile gate kernel with the gate weight images and layer 0's XG table (so the input segment of
+// layer 0 never reads the images and every image's readers run after its writer). No room: off.
+bool prep_h_img(smaml_ctx* c, hipStream_t s, const float* theta, bool use_xgd) {
+  const Dims& d = c->d;
+  Work& w = c->w;
+  w.himg = HImgs{};
+  if (!c->kn.h_img || !use_xgd || w.drop.lstm() || !(w.gimg.th && w.gimg_src == theta) || d.H % 16) return false;
+  for (int diag = 0; diag < d.T + d.L - 1; ++diag)
+    if (!fwd_wave_big(d, w, c->po, diag)) return false;
+  const int64_t need = h_img_bytes(d.L, w.Z, w.M, d.H);
+  if (need > c->himg_cap) {
+    if (c->himg_buf) HIP_TRY(hipFree(c->himg_buf));
+    c->himg_buf = nullptr;
+    c->himg_cap = 0;
+    if (hipMalloc((void**)&c->himg_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    c->himg_cap = need;
+    // (rows of a partial last tile are never written: zeros, so their unused products stay finite)
+    HIP_TRY(hipMemsetAsync(c->himg_buf, 0, need, s));
+  }
+  w.himg.p = c->himg_buf;
+  w.himg.ntm = (w.M + 255) / 256;
+  w.himg.Z = w.Z;
+  return true;
+}
+
 // LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront). consec: every task
 // of this step reads B consecutive windows (layer 0's projection may then run once per stream row).
 int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, bool consec = false) {
@@ -1130,6 +1028,7 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
   for (int diag = 0; xgd_ok && diag < d.T; ++diag) xgd_ok = fwd_wave_big(d, w, c->po, diag);
   const bool use_xgd = xgd_ok && prep_xg_dedup(c, s, true, theta, nullptr, tstride, true);
   if (w.fcompact && !use_xgd) return fail(SMAML_ESTATE, "compact features without the layer-0 projection table");
+  prep_h_img(c, s, theta, use_xgd);
   // Batch-1 sizes (the small-grid steps): layer 0's input projection F . W_ih0^T does not depend on the
   // recurrence, so it runs for all T steps as one throughput-bound GEMM before the wavefront and the
   // layer-0 steps' latency-bound K loops cover only the recurrent segment (kernels_small.hip).
@@ -1185,6 +1084,7 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
   w.xg = nullptr;
   w.xg_src = nullptr;
   w.xgd = XgDedup{};
+  w.himg = HImgs{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1195,6 +1095,10 @@ static void ad_cache_drop(smaml_ctx* c) {
   c->ad_cap = 0;
   c->ad_valid.clear();
 }
+
+// New graph / GCN parameters / tasks: every cached window is stale, but the slots stay allocated (a
+// re-allocation can cost seconds when the driver has to clear released VRAM, see ad_prepare).
+static void ad_cache_invalidate(smaml_ctx* c) { std::fill(c->ad_valid.begin(), c->ad_valid.end(), (uint8_t)0); }
 
 int run_forward(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, const float* const* xtab_dev,
                 const float* const* first_tab = nullptr) {
@@ -1241,7 +1145,6 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
   TRY(prep_bwd_images(c, s, theta, tstride));
   WgradPlan plans[MAX_LAYERS];
   double gfl = 0.0;
-  bool summed = false;  // (rowsum_side: layer 0's row sums already on their way)
   auto layer_wgrad = [&](int l) {
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
@@ -1255,7 +1158,7 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
       gfl += 2.0 * w.Z * TM * 4 * d.H * (lo.cin + d.H);
       return;
     }
-    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, w.dG, grad, summed)) {
+    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, w.dG, grad)) {
       // W_hh0 and the bias over every row (h_{t-1} differs per window): [0 | h_{t-1}], no input columns
       timed_wgrad(c, s, 2.0 * w.Z * TM * 4 * d.H * d.H, w.dG, TM * 4 * d.H, 4 * d.H, nullptr, 0, 0, w.Hs, TM * d.H,
                   d.H, TM, w.M, grad, po.P, -1, lo.whh, lo.bih, lo.bhh, true, false, -1);
@@ -1265,21 +1168,14 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
                 TM * lo.cin, lo.cin, w.Hs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, grad, po.P, lo.wih, lo.whh,
                 lo.bih, lo.bhh, true, false, l - 1);
   };
-  // after a chunked sweep: layers L-1 .. 1, with layer 0's row sums beside them (rowsum_side), then layer 0
-  auto after_sweep_wgrads = [&](const float* dG0) -> int {
-    summed = rowsum_side(c, s, dG0);
-    reduce_side_begin(c, s);
-    for (int l = d.L - 1; l >= 1; --l) layer_wgrad(l);
-    if (summed) HIP_TRY(hipStreamWaitEvent(s, c->join_ev[0], 0));
-    layer_wgrad(0);
-    summed = false;
-    return reduce_side_end(c, s);
+  // after a chunked sweep: layers L-1 .. 0 on the caller's stream
+  auto after_sweep_wgrads = [&]() {
+    for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   };
   // row chunks on side streams (knob bptt_streams): every diagonal's big-tile launch split by rows, the
   // weight gradients after the sweep on the caller's stream
   // (chunked only where a full diagonal runs the big tiles anyway: tile-forcing knobs keep their meaning)
   const int nch = grouped || !bwd_wave_big(d, w, po, std::min(d.L, d.T) - 1) ? 1 : c->kn.bptt_streams;
-  w.push = push_sweep(c, false, nch) ? 1 : 0;
   hipEvent_t wa = nullptr;
   if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
@@ -1296,32 +1192,27 @@ int run_bptt(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, f
     }
     const int l = d.L - 1 - (e - (d.T - 1));
     if (e < d.T - 1 || l < 0) continue;
-    if (nch > 1 && c->kn.wgrad_overlap) {  // layer l's gradient on s beside the chunks' next diagonals
-      TRY(wait_streams_layer(c, s, nch, l));
-      layer_wgrad(l);
-    } else if (nch <= 1) {
-      layer_wgrad(l);
-    }
+    if (nch <= 1) layer_wgrad(l);
   }
   if (nch > 1) {
     TRY(join_streams(c, s, nch));
     time_wall(c, s, wa, C_BWD_WALL, wfl);
-    if (!c->kn.wgrad_overlap)
-      TRY(after_sweep_wgrads(w.dG));
+    after_sweep_wgrads();
   }
   if (grouped) TIMED(c, s, C_WGRAD, gfl, launch_wgrad_multi(s, w, plans, d.L, c->kn.wgrad_group_wgs));
-  w.push = 0;
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
 
 // Primal recompute + tangent along U (second-order sweep), GCN features recomputed.
+// gcn_cached: w.F is the step's so_F slot, written by the inner loop's GCN in the layout fcompact_rec
+// recorded then (not re-derived: f_compact_ok allocates, so a later call could decide differently).
 int run_forward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const float* U, int64_t tstride,
-                     const float* const* xtab_dev, bool gcn_cached, const float* const* first_tab) {
+                     const float* const* xtab_dev, bool gcn_cached, const float* const* first_tab, int fcompact_rec) {
   const Dims& d = c->d;
   Work& w = c->w;
   if (!gcn_cached) TRY(run_gcn(c, s, xtab_dev, first_tab));
-  else w.fcompact = f_compact_ok(c, first_tab != nullptr) ? 1 : 0;  // (as when so_F's slot was written)
+  else w.fcompact = fcompact_rec;
   w.consec = first_tab != nullptr;
   TRY(prep_gate_images(c, s, theta, tstride, U));
   // layer 0's tangent projection F U_ih0^T (and, unless the primal is kept, F W_ih0^T) once per stream row
@@ -1372,14 +1263,13 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, true, false);
   timed_wgrad(c, s, 2.0 * w.Z * w.M * d.HfC * d.H, w.dpred, (int64_t)w.M * d.HfC, d.HfC, RhT, hz, d.H, nullptr, 0, 0,
                      w.M, 0, HU, po.P, po.wo, -1, po.bo, -1, false, true);
-  bool summed = false;  // (rowsum_side: layer 0's row sums already on their way)
   auto layer_wgrad = [&](int l) {
     const LayerOff& lo = po.lay[l];
     const float* X = l == 0 ? w.F : w.Hs + (int64_t)(l - 1) * lsz;
     const float* RX = l == 0 ? nullptr : w.RHs + (int64_t)(l - 1) * lsz;
     const float* dGl = w.dG + (int64_t)l * lsz * 4;
     const float* RdGl = w.RGs + (int64_t)l * lsz * 4;
-    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, RdGl, HU, summed)) {
+    if (l == 0 && wgrad_dedup_ok(c) && timed_wgrad_ih0_dedup(c, s, RdGl, HU)) {
       // R(dW_ih0) = R(dG0)^T F (R x = 0 at layer 0) over distinct stream rows above; R(dW_hh0) =
       // R(dG0)^T h + dG0^T R h and R(db) as one paired launch over every row
       const double flp = 2.0 * 2.0 * w.Z * TM * 4 * d.H * d.H;
@@ -1405,20 +1295,13 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
                 TM * lo.cin, l > 0 ? lo.cin : 0, w.RHs + (int64_t)l * lsz, TM * d.H, d.H, TM, w.M, HU, po.P, lo.wih,
                 lo.whh, lo.bih, lo.bhh, false, true, l - 1);
   };
-  // after a chunked sweep: layers L-1 .. 1, with layer 0's row sums beside them (rowsum_side), then layer 0
-  auto after_sweep_wgrads = [&](const float* dG0) -> int {
-    summed = rowsum_side(c, s, dG0);
-    reduce_side_begin(c, s);
-    for (int l = d.L - 1; l >= 1; --l) layer_wgrad(l);
-    if (summed) HIP_TRY(hipStreamWaitEvent(s, c->join_ev[0], 0));
-    layer_wgrad(0);
-    summed = false;
-    return reduce_side_end(c, s);
+  // after a chunked sweep: layers L-1 .. 0 on the caller's stream
+  auto after_sweep_wgrads = [&]() {
+    for (int l = d.L - 1; l >= 0; --l) layer_wgrad(l);
   };
   const int nch = (int64_t)w.Z * w.M <= c->kn.wgrad_group_max_rows || !bwd_dual_wave_big(d, w, po, std::min(d.L, d.T) - 1)
                       ? 1
                       : c->kn.bptt_streams;
-  w.push = push_sweep(c, true, nch) ? 1 : 0;
   hipEvent_t wa = nullptr;
   if (nch > 1 && c->tm.on) (void)hipEventRecord(wa = c->tm.get(), s);
   if (nch > 1) TRY(fork_streams(c, s, nch));
@@ -1436,20 +1319,13 @@ int run_backward_dual(smaml_ctx* c, hipStream_t s, const float* theta, const flo
     }
     const int l = d.L - 1 - (e - (d.T - 1));
     if (e < d.T - 1 || l < 0) continue;
-    if (nch > 1 && c->kn.wgrad_overlap) {
-      TRY(wait_streams_layer(c, s, nch, l));
-      layer_wgrad(l);
-    } else if (nch <= 1) {
-      layer_wgrad(l);
-    }
+    if (nch <= 1) layer_wgrad(l);
   }
   if (nch > 1) {
     TRY(join_streams(c, s, nch));
     time_wall(c, s, wa, C_BWD_DUAL_WALL, wfl);
-    if (!c->kn.wgrad_overlap)
-      TRY(after_sweep_wgrads(w.RGs));
+    after_sweep_wgrads();
   }
-  w.push = 0;
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1509,7 +1385,7 @@ extern "C" {
 
 const char* smaml_last_error(void) { return g_err.c_str(); }
 
-int32_t smaml_abi_version(void) { return 6; }
+int32_t smaml_abi_version(void) { return 7; }
 
 const char* smaml_build_info(void) { return smaml::products_info(); }
 
@@ -1622,21 +1498,13 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->bimg_buf) (void)hipFree(c->bimg_buf);
   if (c->xg_buf) (void)hipFree(c->xg_buf);
   if (c->xgd_buf) (void)hipFree(c->xgd_buf);
-  if (c->push_buf) (void)hipFree(c->push_buf);
-  if (c->wpart2) (void)hipFree(c->wpart2);
-  for (int i = 0; i < 2; ++i) {
-    if (c->red.gemm[i]) (void)hipEventDestroy(c->red.gemm[i]);
-    if (c->red.done[i]) (void)hipEventDestroy(c->red.done[i]);
-  }
+  if (c->himg_buf) (void)hipFree(c->himg_buf);
   if (c->bar) (void)hipFree(c->bar);
   for (int i = 0; i < 4; ++i) {
     if (c->cs[i]) (void)hipStreamDestroy(c->cs[i]);
     if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
   }
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-  for (auto& row : c->lay_ev)
-    for (auto& e : row)
-      if (e) (void)hipEventDestroy(e);
   if (c->bar_err_host) (void)hipHostFree(c->bar_err_host);
   ad_cache_drop(c);
   for (float* p : c->keep_mem) (void)hipFree(p);
@@ -1655,7 +1523,7 @@ int smaml_set_graph(smaml_ctx* c, const int64_t* edge_index_host, int64_t num_ed
   std::vector<int32_t> cols;
   std::vector<float> vals;
   TRY(build_ell(edge_index_host, num_edges, c->d.N, cols, vals));
-  ad_cache_drop(c);
+  ad_cache_invalidate(c);
   if (!c->ell_c) {
     HIP_TRY(hipMalloc((void**)&c->ell_c, cols.size() * 4));
     HIP_TRY(hipMalloc((void**)&c->ell_v, vals.size() * 4));
@@ -1704,7 +1572,7 @@ int smaml_set_gcn_params(smaml_ctx* c, const float* gcn_flat) {
   if (!c || !gcn_flat) return fail(SMAML_EINVAL, "NULL argument");
   if (!aligned16(gcn_flat)) return fail(SMAML_EINVAL, "gcn params must be 16-byte aligned");
   c->gcn = gcn_flat;
-  ad_cache_drop(c);  // cached features belong to the previous GCN parameters
+  ad_cache_invalidate(c);  // cached features belong to the previous GCN parameters (the slots stay allocated)
   return SMAML_OK;
 }
 
@@ -1862,7 +1730,7 @@ int smaml_forward(smaml_ctx* c, void* stream, const float* theta, const float* c
 }
 
 int smaml_set_tasks(smaml_ctx* c, int32_t ntasks, const float* const* features_host, const int32_t* t_total_host) {
-  if (c) ad_cache_drop(c);
+  if (c) ad_cache_invalidate(c);
   if (!c || ntasks <= 0 || !features_host || !t_total_host) return fail(SMAML_EINVAL, "bad set_tasks arguments");
   c->feats.assign(features_host, features_host + ntasks);
   c->t_total.assign(t_total_host, t_total_host + ntasks);
@@ -1942,6 +1810,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
   launch_broadcast(s, theta, P, Z, c->fast);
   const double head_fl = 2.0 * Z * c->w.M * d.HfC * d.H;
   const bool so = order == 2;
+  if (so) c->so_fc.assign((size_t)steps, 0);
   for (int k = 0; k < steps; ++k) {
     const float* const* xt = xstep[k];
     if (dropout) set_step_drop(c, k);
@@ -1952,6 +1821,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
     const int slot = steps - 1 - k;
     use_primal(c, slot < nkeep ? slot : SET_MAIN);
     TRY(run_forward(c, s, c->fast, P, xt, consec[k]));
+    if (so) c->so_fc[k] = (int8_t)c->w.fcompact;  // (the layout of so_F slot k, for the sweep)
     TIMED(c, s, C_HEAD, head_fl, launch_head_loss(s, d, c->w, c->fast, P, c->po, xt, 2.f * inv, true));
     TIMED(c, s, C_MISC, 0, launch_loss_final(s, c->w, inv, losses + (int64_t)k * Z));
     TRY(run_backward(c, s, c->fast, P, c->grad));
@@ -2003,7 +1873,7 @@ int smaml_meta_step(smaml_ctx* c, void* stream, const float* theta, int32_t orde
       use_primal(c, slot < nkeep ? slot : SET_MAIN);
       c->w.primal_kept = slot < nkeep ? 1 : 0;
       if (dropout) set_step_drop(c, k);  // the masks of inner step k's forward
-      TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr, consec[k]));
+      TRY(run_forward_dual(c, s, th, c->so_u, P, xt, c->so_F != nullptr, consec[k], c->so_fc[k]));
       TIMED(c, s, C_HEAD, 3.0 * head_fl, launch_head_dual(s, d, c->w, th, c->so_u, P, c->po, xt, 2.f * inv));
       TRY(run_backward_dual(c, s, th, c->so_u, P, c->so_hu));
       if (k > 0)  // v_k = v_{k+1} - lr H_k w_k and w_{k-1} (dot g_{k-1} . v_k, direction): one kernel
@@ -2057,9 +1927,64 @@ static int ad_cache_fill(smaml_ctx* c, hipStream_t s, const int32_t* windows, in
   return SMAML_OK;
 }
 
+// Set-up half of smaml_adapt_steps: size the workspace for `B`-sample steps (and, for the batched cache
+// fill, ad_gcn_batch single-window "tasks") and allocate the per-window feature cache once per context.
+// Both allocations are TOUCHED (memset + stream sync) before returning: the driver may hand out freshly
+// released VRAM that it still has to clear, and that clear otherwise lands in the first kernel that
+// reads the buffer -- i.e. inside the first timed epoch (round 5: 6.1 s of a 6.8 s first epoch on some
+// boxes, 0 on others). Returns with *cache = whether this call's steps use the cache.
+static int ad_prepare(smaml_ctx* c, hipStream_t s, int B, bool* cache_out) {
+  using clk = std::chrono::steady_clock;
+  const Dims& d = c->d;
+  auto t0 = clk::now();
+  const bool fill_batched = B == 1 && !(c->p_gcn > 0.f) && c->ad_gcn_batch > 1;
+  const int64_t had = c->arena_bytes;
+  // (the cache fill's GCN passes run ad_gcn_batch windows as tasks: size the workspace for them
+  // first, since a growing workspace drops the cache)
+  TRY(reserve(c, fill_batched ? c->ad_gcn_batch : 1, B));
+  if (c->arena_bytes != had) {
+    HIP_TRY(hipMemsetAsync(c->arena, 0, (size_t)c->arena_bytes, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  auto t1 = clk::now();
+  const int64_t fsz = (int64_t)d.T * d.N * d.Hc;  // floats of one window's features
+  const int64_t n = c->t_total.empty() ? 0 : c->t_total[0];
+  bool cache = B == 1 && !(c->p_gcn > 0.f) && n > 0;
+  if (cache && c->ad_F && c->ad_cap < n) ad_cache_drop(c);  // a longer stream than the cache was sized for
+  if (cache && !c->ad_F) {
+    size_t freeb = 0, totb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totb));
+    if ((int64_t)freeb > n * fsz * 4 + (8ll << 30) && hipMalloc((void**)&c->ad_F, (size_t)(n * fsz * 4)) == hipSuccess) {
+      c->ad_cap = n;
+      c->ad_valid.assign((size_t)n, 0);
+      HIP_TRY(hipMemsetAsync(c->ad_F, 0, (size_t)(n * fsz * 4), s));
+      HIP_TRY(hipStreamSynchronize(s));
+    } else {
+      (void)hipGetLastError();
+      c->ad_F = nullptr;
+    }
+  }
+  auto t2 = clk::now();
+  c->ad_ph.ms[AD_RESERVE] += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  c->ad_ph.ms[AD_ALLOC] += std::chrono::duration<double, std::milli>(t2 - t1).count();
+  *cache_out = cache && c->ad_F;
+  return SMAML_OK;
+}
+
+int smaml_adapt_prepare(smaml_ctx* c, void* stream, int32_t batch) {
+  TRY(require_ready(c));
+  if (c->feats.empty()) return fail(SMAML_ESTATE, "smaml_set_tasks not called");
+  if (batch <= 0) return fail(SMAML_EINVAL, "bad adapt_prepare batch");
+  TRY(ensure_device(c));
+  bool cache = false;
+  c->ad_ph = AdPhases{};
+  return ad_prepare(c, (hipStream_t)stream, batch, &cache);
+}
+
 int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float* v, int32_t step0, int32_t nsteps,
                       int32_t batch, const int32_t* windows_host, const float* lr_dev, float beta1, float beta2,
                       float eps, float weight_decay, float max_norm, float* losses) {
+  using clk = std::chrono::steady_clock;
   TRY(require_ready(c));
   if (c->feats.empty()) return fail(SMAML_ESTATE, "smaml_set_tasks not called");
   if (!theta || !m || !v || nsteps <= 0 || batch <= 0 || !windows_host || !lr_dev || !losses || step0 < 0)
@@ -2075,31 +2000,22 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
     if (wv < 0 || wv + d.T + d.Hf >= c->t_total[0]) return fail(SMAML_EINVAL, "window start out of range");
     ptrs[i] = c->feats[0] + (int64_t)wv * d.N * d.Cin0;
   }
-  // (the cache fill's GCN passes run ad_gcn_batch windows as tasks: size the workspace for them
-  // first, since a growing workspace drops the cache)
+  c->ad_ph = AdPhases{};
+  bool cache = false;
+  TRY(ad_prepare(c, s, B, &cache));  // no allocation after smaml_adapt_prepare / an earlier call
   const bool fill_batched = B == 1 && !(c->p_gcn > 0.f) && c->ad_gcn_batch > 1;
-  TRY(reserve(c, fill_batched ? c->ad_gcn_batch : 1, B));
   const int64_t P = c->po.P;
   const float inv = 1.f / ((float)d.N * d.HfC * B);
   const bool dropout = c->p_gcn > 0.f || c->p_lstm > 0.f;
   if (dropout) TRY(upload_task_ids(c, s, 1));
   // Batch-1 steps without GCN dropout reuse each window's GCN features across epochs (F2).
   const int64_t fsz = (int64_t)d.T * d.N * d.Hc;  // floats of one window's features
-  bool cache = B == 1 && !(c->p_gcn > 0.f) && c->t_total[0] > 0;
-  if (cache && !c->ad_F) {
-    const int64_t n = c->t_total[0];
-    size_t freeb = 0, totb = 0;
-    HIP_TRY(hipMemGetInfo(&freeb, &totb));
-    if ((int64_t)freeb > n * fsz * 4 + (8ll << 30) && hipMalloc((void**)&c->ad_F, (size_t)(n * fsz * 4)) == hipSuccess) {
-      c->ad_cap = n;
-      c->ad_valid.assign((size_t)n, 0);
-    } else {
-      (void)hipGetLastError();
-      c->ad_F = nullptr;
-    }
+  auto t0 = clk::now();
+  if (cache && fill_batched) {
+    TRY(ad_cache_fill(c, s, windows_host, nsteps));
+    if (c->ad_phase_sync) HIP_TRY(hipStreamSynchronize(s));
   }
-  cache = cache && c->ad_F;
-  if (cache && fill_batched) TRY(ad_cache_fill(c, s, windows_host, nsteps));
+  auto t1 = clk::now();
   set_work(c, 1, B);
   TRY(upload_xtab(c, s, ptrs.data(), nptr));
   for (int k = 0; k < nsteps; ++k) {
@@ -2112,6 +2028,7 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
       if (!c->ad_valid[wv]) {
         TRY(run_gcn(c, s, xt));  // writes the window's features straight into its cache slot
         c->ad_valid[wv] = 1;
+        c->ad_ph.filled += 1;
       }
       TRY(run_lstm(c, s, theta, 0));
     } else {
@@ -2124,9 +2041,21 @@ int smaml_adapt_steps(smaml_ctx* c, void* stream, float* theta, float* m, float*
           launch_adam_l2(s, theta, c->grad, m, v, P, c->w.sqpart, lr_dev + k, step0 + k + 1, beta1, beta2, eps,
                          weight_decay, max_norm, c->w.lpart, c->w.lblocks, inv, losses + k));
   }
+  if (c->ad_phase_sync) HIP_TRY(hipStreamSynchronize(s));
+  auto t2 = clk::now();
+  c->ad_ph.ms[AD_FILL] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  c->ad_ph.ms[AD_STEPS] = std::chrono::duration<double, std::milli>(t2 - t1).count();
   c->w.F = c->F_main;
   c->w.drop = Drop{};
   HIP_TRY(hipGetLastError());
+  return SMAML_OK;
+}
+
+int smaml_adapt_phases(const smaml_ctx* c, double* ms, int32_t cap, int32_t* count, int64_t* filled) {
+  if (!c || cap < 0 || (cap > 0 && !ms)) return fail(SMAML_EINVAL, "bad adapt_phases arguments");
+  for (int i = 0; i < AD_NPH && i < cap; ++i) ms[i] = c->ad_ph.ms[i];
+  if (count) *count = AD_NPH;
+  if (filled) *filled = c->ad_ph.filled;
   return SMAML_OK;
 }
 
@@ -2189,8 +2118,6 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_wide = (int)value;
   } else if (k == "wgrad_pair" && (value == 0 || value == 1)) {
     c->kn.wgrad_pair = (int)value;
-  } else if (k == "wgrad_ws" && (value == 0 || value == 1)) {
-    c->kn.wgrad_ws = (int)value;
   } else if (k == "bwdd_remap" && (value == 0 || value == 1)) {
     c->kn.bwdd_remap = (int)value;
   } else if (k == "small_kw" && value >= 0 && value <= 2) {
@@ -2203,24 +2130,14 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_dedup = (int)value;
   } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
     c->kn.bptt_streams = (int)value;
-  } else if (k == "bptt_push" && value >= 0 && value <= 2) {
-    c->kn.bptt_push = (int)value;
-  } else if (k == "wgrad_threads" && value >= 0 && value <= (1 << 24)) {
-    c->kn.wgrad_threads = (int)value;
-  } else if (k == "wgrad_min_kt" && value >= 1 && value <= 4096) {
-    c->kn.wgrad_min_kt = (int)value;
-  } else if (k == "gcn_side" && (value == 0 || value == 1)) {
-    c->kn.gcn_side = (int)value;
-  } else if (k == "reduce_side" && (value == 0 || value == 1)) {
-    c->kn.reduce_side = (int)value;
-  } else if (k == "rowsum_side" && (value == 0 || value == 1)) {
-    c->kn.rowsum_side = (int)value;
+  } else if (k == "h_img" && (value == 0 || value == 1)) {
+    c->kn.h_img = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
     c->kn.f_compact = (int)value;
-  } else if (k == "wgrad_overlap" && (value == 0 || value == 1)) {
-    c->kn.wgrad_overlap = (int)value;
   } else if (k == "fwd_streams" && value >= 0 && value <= 4) {
     c->kn.fwd_streams = (int)value;
+  } else if (k == "adapt_phase_sync" && (value == 0 || value == 1)) {
+    c->ad_phase_sync = (int)value;
   } else if (k == "adapt_gcn_batch" && value >= 0 && value <= 256) {
     c->ad_gcn_batch = (int)value;
   } else if (k == "wgrad_group_wgs" && value >= 1) {

@@ -411,6 +411,27 @@ struct BStage<C, LB, true> {
   __device__ __forceinline__ void store(char*) const {}
 };
 
+// A operand staging, the same two forms: f32 float4s split at the LDS store, or (DMA, loaders.h HImgA) a
+// pre-split image issued straight into the stage.
+template <class C, class LA, bool DMA = has_dma_image<LA>::value>
+struct AStage {
+  float4 r[C::A_F4];
+  __device__ __forceinline__ void fetch(const LA& la, int m0, int k0, char*) {
+    fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, C::BK>(la, m0, k0, r);
+  }
+  __device__ __forceinline__ void store(char* img) const {
+    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, C::BK, C::MSW>(img, r);
+  }
+};
+template <class C, class LA>
+struct AStage<C, LA, true> {
+  static_assert(C::X6S && C::X6S_NST == 2, "pre-split A images: two LDS stages (issued into the idle one)");
+  __device__ __forceinline__ void fetch(const LA& la, int m0, int k0, char* img) {
+    la.template issue<C::BM, C::A_KC, C::BK, C::NTH>(img, m0, k0);
+  }
+  __device__ __forceinline__ void store(char*) const {}
+};
+
 // The three pieces of the 32-row fragment at tile row `row` (this lane's row = row + (lane & 31)
 // for KC; the fragment's first row for MC), MFMA step s (k = 16s + 8h .. 16s + 8h + 7).
 template <int ROWS, bool KC, int BK, bool SWZ = true>
@@ -478,16 +499,18 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   char* st0 = reinterpret_cast<char*>(smem);
   const int nkt = (kend - kbeg + BKc - 1) / BKc;
   if (nkt <= 0) return;
-  constexpr bool DMA = has_dma_image<LB>::value;
-  float4 ra[C::A_F4];
+  constexpr bool DMA_A = has_dma_image<LA>::value;
+  constexpr bool DMA = DMA_A || has_dma_image<LB>::value;
+  static_assert(!DMA_A || !has_stage_a<Hook>::value, "a pre-split A image has no f32 staging for the hook");
+  AStage<C, LA> ra;
   BStage<C, LB> rb;
   auto store = [&](char* st) {
-    if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra);
-    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc, C::MSW>(st, ra);
+    if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra.r);
+    ra.store(st);
     rb.store(st + SA);
     if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image chunks landed
   };
-  fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg, ra);
+  ra.fetch(la, m0, kbeg, st0);
   rb.fetch(lb, n0, kbeg, st0 + SA);
   store(st0);
   __syncthreads();
@@ -495,9 +518,10 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
     if (more) {
-      fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, kbeg + (kt + 1) * BKc, ra);
       // (two stages: the idle one was last read by tile kt - 1's MFMAs, before the barrier)
-      rb.fetch(lb, n0, kbeg + (kt + 1) * BKc, st0 + (C::X6S_NST == 1 ? 0 : (cur ^ 1) * C::X6S_STAGE) + SA);
+      char* idle = st0 + (C::X6S_NST == 1 ? 0 : (cur ^ 1) * C::X6S_STAGE);
+      ra.fetch(la, m0, kbeg + (kt + 1) * BKc, idle);
+      rb.fetch(lb, n0, kbeg + (kt + 1) * BKc, idle + SA);
     }
     const char* st = st0 + (C::X6S_NST == 1 ? 0 : cur * C::X6S_STAGE);
     if constexpr (C::X6S_NST == 1) {

@@ -95,15 +95,13 @@ enum Variant {
   V_WGRAD,           // k_wgrad launches (any tile)
   V_WGRAD_WIDE,      // k_wgrad with 256 x 256 tiles (also counted as V_WGRAD)
   V_WGRAD_PAIR,      // k_wgrad summing two problems (tangent weight gradient; also counted as V_WGRAD)
-  V_WGRAD_WS,        // k_wgrad_ws, warp-specialised (also counted as V_WGRAD)
   V_FWD_KW,          // k_lstm_fwd_kw (small grids: K split over the waves of one workgroup)
   V_BWD_KW,          // k_lstm_bwd_kw (same, BPTT)
   V_GCN_DEDUP,       // k_gcn_mlp once per distinct stream row of consecutive windows
   V_XG_DEDUP,        // k_xg_dedup: layer 0's input projection once per distinct stream row (big-tile forward)
   V_WGRAD_DEDUP,     // layer 0's input-weight gradient over distinct stream rows (k_dg_rowsum + gathered k_wgrad)
   V_F_COMPACT,       // GCN features stored once per distinct stream row (Work::fcompact)
-  V_BWD_PUSH,        // k_lstm_bwd_push (push BPTT, big tiles)
-  V_BWDD_PUSH,       // k_lstm_bwd_dual_push (push tangent BPTT of a kept step, big tiles)
+  V_FWD_HIMG,        // k_lstm_fwd_step with pre-split h images (HImgs; also counted as V_FWD, V_FWD_IMG)
   NVAR
 };
 
@@ -130,7 +128,6 @@ struct Knobs {
   int gate_img = 0;              // 1: gate GEMMs read pre-split weight images (launch_split_gate)
   int wgrad_wide = 0;            // 1: weight gradients with 256-multiple column counts on 256 x 256 tiles
   int wgrad_pair = 0;            // 1: the two passes of a tangent weight gradient (layers >= 1) as one launch
-  int wgrad_ws = 0;              // 1: warp-specialised weight gradients (k_wgrad_ws) where the shapes allow
   int bwdd_remap = 0;            // 1: tangent BPTT tiles in pair-segment order per XCD (kernels_dual.hip PairRemap)
   int small_kw = 0;              // small-grid LSTM steps as one launch with the K split over waves (kernels_small.hip):
                              // 1 = on, 2 = on with pre-split BPTT weight images (launch_split_bwd), 0 = split-K pairs
@@ -143,19 +140,8 @@ struct Knobs {
                                  // chunks on side streams (a chunk's rows depend on nothing else), so one
                                  // chunk's next diagonal fills the other's tail; weight gradients after the sweep
   int fwd_streams = 0;           // the same for the big-tile forward diagonals (primal and tangent); 0 = auto
-  int wgrad_overlap = 0;         // 1 (with row chunks): layer l's weight gradient on the caller's stream as soon as
-                                 // its BPTT is done, beside the chunks' remaining diagonals
-  int bptt_push = 0;             // 1 (2: the tangent sweep only): big-tile BPTT sweeps (primal, and the tangent of kept steps) as producer-side
-                                 // steps: cell backward first, from the dh partial sums its producers left, then
-                                 // dG . W_hh and dG . W_ih for the two consumers (each dG read once as a GEMM
-                                 // operand instead of twice)
-  int wgrad_min_kt = 8;          // split-K weight gradients: at least this many K-tiles per split
-  int wgrad_threads = 0;         // split-K weight gradients: thread target of one launch (0 = SMAML_WGRAD_THREADS)
-  int gcn_side = 0;              // 1: the fused GCN's t = 0 ELL chain on a side stream beside k_gcn_mlp (disjoint rows)
-  int reduce_side = 0;           // 1: after a chunked sweep, each weight gradient's split-K reduce on a side stream
-                                 // beside the next layer's GEMM (two partial slabs, alternating)
-  int rowsum_side = 0;           // 1: after a chunked sweep, layer 0's dG row sums (k_dg_rowsum) on a side stream
-                                 // beside the weight gradients of layers L-1 .. 1
+  int h_img = 0;                 // 1: the big-tile primal forward (with layer 0's XG table) hands h to the next
+                                 // diagonal as pre-split bf16 images (HImgs)
   int f_compact = 0;             // 1: where every reader of a step's features goes through the distinct stream rows
                                  // (xg_dedup forwards, wgrad_dedup backwards), the GCN stores only those rows
 };
@@ -164,9 +150,6 @@ struct Knobs {
 #endif
 #ifndef SMAML_GCN_FUSED
 #define SMAML_GCN_FUSED 1
-#endif
-#ifndef SMAML_WGRAD_WS_DEFAULT
-#define SMAML_WGRAD_WS_DEFAULT 0  // k_wgrad_ws measured slower than the staged tiles in every arm
 #endif
 #ifndef SMAML_BWDD_REMAP_DEFAULT
 #define SMAML_BWDD_REMAP_DEFAULT 1  // tangent BPTT pair-segment tile order: -0.55 GB of HBM reads per launch,
@@ -183,21 +166,8 @@ struct Knobs {
 #ifndef SMAML_BPTT_STREAMS_DEFAULT
 #define SMAML_BPTT_STREAMS_DEFAULT 2  // A/B (profiles/r05_ab_streams*.log): config 2 1653 -> 1618 ms, config-5 share 4453 -> 4308 ms
 #endif
-#ifndef SMAML_BPTT_PUSH_DEFAULT
-#define SMAML_BPTT_PUSH_DEFAULT 0
-#endif
-#ifndef SMAML_WGRAD_MIN_KT
-#define SMAML_WGRAD_MIN_KT 8  // K-tiles per split-K slice at least (knob wgrad_min_kt)
-#endif
-#ifndef SMAML_GCN_SIDE_DEFAULT
-#define SMAML_GCN_SIDE_DEFAULT 0
-#endif
-#ifndef SMAML_REDUCE_SIDE_DEFAULT
-#define SMAML_REDUCE_SIDE_DEFAULT 0
-#endif
-#ifndef SMAML_ROWSUM_SIDE_DEFAULT
-#define SMAML_ROWSUM_SIDE_DEFAULT 0  // A/B (profiles/r05_ab_rowsum_side.log): config 2 -5 ms, config-5 share -14 ms, but the
-                                     // weight gradients then share the chip with it (their measured rate -4 %): off
+#ifndef SMAML_H_IMG_DEFAULT
+#define SMAML_H_IMG_DEFAULT 0  // A/B (profiles/r06_ab_h_img.log): forward 201.2 -> 207.6 ms with the images: off
 #endif
 #ifndef SMAML_F_COMPACT_DEFAULT
 #define SMAML_F_COMPACT_DEFAULT 1
@@ -228,6 +198,28 @@ struct GateImgs {
   int64_t tstride = 0;              // bytes per task
   int64_t off[MAX_LAYERS][2] = {};  // byte offset of (layer, W_ih | W_hh) in a task's images
 };
+// ---- pre-split h images (round 6; big-tile forward) ----
+// The big-tile forward's epilogue also stores each h(l, t) as the staged-split LDS image of the gate
+// GEMM's A tiles (X6Img<256, KC, 16>: 3 bf16 planes x 256 rows x 16 k = 24 KB per (row tile, K-tile)),
+// so the next diagonal's two readers of it -- layer l at t + 1 (recurrent segment) and layer l + 1 at t
+// (input segment) -- copy their A tiles into LDS with direct-to-LDS loads instead of loading f32 h and
+// splitting it in every workgroup (the split is deterministic: bitwise the same products). A ring of two
+// steps per layer: image (l, t) lives in slot t & 1 and is overwritten by step t + 2, two diagonals later,
+// after both readers ran (stream order; row chunks on side streams touch only their own row tiles).
+// Layout [L][2][Z][ntm][H / 16] images. The f32 h stays (BPTT, weight gradients, head, tangent forward).
+constexpr int H_IMG_BYTES = 3 * 256 * 16 * 2;
+struct HImgs {
+  char* p = nullptr;  // null: off (the gate kernels load and split f32 h)
+  int ntm = 0;        // 256-row tiles per (layer, slot, task)
+  int Z = 0;
+  // image block of (layer l, ring slot, task z): image (tm, kt) at + (tm * (H / 16) + kt) * H_IMG_BYTES
+  __host__ __device__ char* block(int l, int slot, int z, int H) const {
+    return p + ((int64_t)(l * 2 + slot) * Z + z) * ntm * (H / 16) * H_IMG_BYTES;
+  }
+};
+__host__ __device__ inline int64_t h_img_bytes(int L, int Z, int M, int H) {
+  return (int64_t)L * 2 * Z * ((M + 255) / 256) * (H / 16) * H_IMG_BYTES;
+}
 // ---- pre-split BPTT weight images (kernels_small.hip launch_split_bwd; small-grid BPTT) ----
 // Per task, for W_hh of every layer and W_ih of layers >= 1 (the [4H][H] matrices the BPTT step reads
 // as B[k][j]): per K-tile kt (16 gate rows) and unit tile tn (32 units) three bf16 planes of
@@ -270,6 +262,7 @@ struct Work {
   int fcompact = 0;                // F holds only the distinct rows of those windows, in XgDedup's row order
                                    // (rows [0, (2B + T - 2) N) of each task's slab): read through XgDedup only
   GateImgs gimg{};         // pre-split images of the weights the gate GEMMs read (launch_split_gate)
+  HImgs himg{};            // pre-split h images of the big-tile forward (run_lstm, option h_img)
   const float* gimg_src = nullptr; // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src = nullptr;// ... and gimg.u (the sweep's tangent direction)
   int64_t* vcount = nullptr;       // [NVAR] launch counters (ctx-owned; may be null)
@@ -296,12 +289,6 @@ struct Work {
   // dropout (zero thresholds: off) and the masked head inputs drop(h_T), drop(R h_T) [Z][M][H]
   Drop drop{};
   float *hTd = nullptr, *RhTd = nullptr;
-  // push BPTT (knob bptt_push, BptPush below): this sweep's steps leave dh partial sums for their
-  // consumers instead of having them re-read dG; set per sweep by the caller
-  int push = 0;
-  float *Prec = nullptr, *Pup = nullptr;     // [L][Z][M][H] dG_t . W_hh(l) for (l, t-1); [2][L][Z][M][H]
-                                             // dG_t . W_ih(l) for (l-1, t), by the parity of t
-  float *RPrec = nullptr, *RPup = nullptr;   // the tangent sweep's R(dh) partial sums, same layouts
 };
 
 inline void count_variant(const Work& w, Variant v) {
@@ -560,7 +547,6 @@ struct WgradPlan {
   Drop drop{};          // B1 = drop(h_{drop_layer}) when drop_layer >= 0 and LSTM dropout is on
   int drop_layer = -1;  // (defaults: no dropout -- launch_wgrad's callers never set these)
   bool wide = false;    // 256 x 256 tiles (CfgTW) instead of 512 x 128 (kernels.hip plan_wgrad)
-  bool ws = false; // warp-specialised 256 x 128 tiles (k_wgrad_ws; dropout-free launches only)
   // pair (pair_wgrad): slices [nsplit1, nsplit) sum A2^T [B1s | B2s] (same shape and strides) into
   // the same gradient; A2 == nullptr: one problem
   const float* A2 = nullptr;
@@ -588,7 +574,6 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p);
 // S[z] = row sums of layer 0's dG slab (dG0 = [T][M][4H] per task, a_zstride floats apart) over the
 // (window, step) slots of each distinct stream row, in XgDedup's row order ([(2B + T - 2) N][4H] per task)
 void launch_dg_rowsum(hipStream_t s, const Dims& d, const Work& w, const float* dG0, int64_t a_zstride, float* S);
-bool wgrad_ws_ok(int Mrows, int c1, int c2);  // shapes the warp-specialised weight gradient takes
 void launch_wgrad_reduce(hipStream_t s, const WgradPlan& p);
 // clip_grad_norm_ + SGD of every task as one grid-barrier kernel (k_inner_sgd), or its two phases as
 // two launches (BarPlan)

@@ -293,10 +293,14 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
 // one 16-B c_{t-1} load and six 16-B stores (i, f, g, o, c, h). XG: the pre-activations also get the
 // row's XgDedup entries (layer 0's input projection, xg = the step's block of window rows): four more
 // 16-B loads per item.
-template <int H, class CG, bool XG = false>
+// HIMG: h also goes to the pre-split image block himg (kernels.h HImgs; this step's layer, ring slot and
+// task): three 8-B plane stores per item at the staged split's LDS offsets of (tile row, unit).
+template <int H, class CG, bool XG = false, bool HIMG = false>
 __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __restrict__ th, const LayerOff& lo,
                                            float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
-                                           int m0, int ug, int t, int M, float* smem, const float* xg = nullptr) {
+                                           int m0, int ug, int t, int M, float* smem, const float* xg = nullptr,
+                                           char* __restrict__ himg = nullptr) {
+  static_assert(!HIMG || CG::BM == 256, "h images are 256-row tiles");
   const int j = ug * 32 + (int)(threadIdx.x & 31);
   float bsum[4];
 #pragma unroll
@@ -349,6 +353,22 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
         sto(Gz, og + 12u * H, go);
         sto(Cz, oh, c);
         sto(Hz, oh, hh);
+        if constexpr (HIMG) {
+          // split the STORED (rounded) h: without the barrier, fp-contract fuses o * tanh(c) into the split's
+          // first subtraction (an fma of the exact product) and the pieces would differ from those the
+          // readers' own split of the f32 h forms
+          float4 hv = hh;
+          asm volatile("" : "+v"(hv.x), "+v"(hv.y), "+v"(hv.z), "+v"(hv.w));
+          uint2 p0, p1, p2;
+          split4(hv, p0, p1, p2);
+          const int ki = (int)jq & 15;  // (H / 16 K-tiles of 16 units: K-tile jq >> 4 of the readers' h segment)
+          char* o = himg + ((int64_t)(m0 >> 8) * (H / 16) + (jq >> 4)) * H_IMG_BYTES + ml * 32 +
+                    16 * ((ki >> 3) ^ ((ml >> 3) & 1)) + 2 * (ki & 7);
+          constexpr int PL = H_IMG_BYTES / 3;
+          *reinterpret_cast<uint2*>(o) = p0;
+          *reinterpret_cast<uint2*>(o + PL) = p1;
+          *reinterpret_cast<uint2*>(o + 2 * PL) = p2;
+        }
       });
 }
 
@@ -357,12 +377,16 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
 #endif                    // 2 = without its GEMM
 // XG (xg != null): layer 0's input projection of this step's windows comes from the XgDedup table
 // (launch_xg_dedup): the accumulators start from it and the K loop covers the recurrent segment only.
-template <int H, bool DROP, bool IMG = false>
+// HIMG (with IMG and the XG table): A tiles as pre-split h images (kernels.h HImgs) -- x = h(l - 1, t) from
+// layer l - 1's ring slot t & 1, h_{t-1} from layer l's slot (t - 1) & 1 -- and h(l, t) written to slot t & 1.
+template <int H, bool DROP, bool IMG = false, bool HIMG = false>
 __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                               float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
                                               const float* __restrict__ theta, int64_t tstride, FwdWave wv, int T,
                                               int M, const Drop& dr, float* smem, const GateImgs* gi = nullptr,
-                                              const float* xg = nullptr, int64_t xg_zstride = 0, int xg_N = 0) {
+                                              const float* xg = nullptr, int64_t xg_zstride = 0, int xg_N = 0,
+                                              const HImgs* hi = nullptr) {
+  static_assert(!HIMG || (IMG && !DROP), "h images: with the gate weight images, no dropout");
   int l, t, b0;
   LayerOff lo;
   const Blk bk = xcd_block();
@@ -390,14 +414,17 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
   Acc<CfgGate> acc;
   int kbeg = 0;  // (XG: the K loop starts past the input segment)
   acc.zero();
-  if (SMAML_DIAG_FWD == 2) {  // timing diagnostic: cell epilogue only (no K loop)
-    fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, nullptr);
-    return;
-  }
   // (the table is added in the epilogue: loading it into the accumulators before the K loop keeps 64 more
   // registers live through the loop's prologue and spills)
   const float* xgt = !DROP && xg && l == 0 ? xg + (int64_t)z * xg_zstride + xg_dedup_row0(t, M, xg_N) * (4 * H) : nullptr;
   if (xgt) kbeg = cin;
+  if (SMAML_DIAG_FWD == 2) {  // timing diagnostic: cell epilogue only (no K loop)
+    if constexpr (HIMG)
+      fwd_cell_t<H, CfgGate, true, true>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt, hi->block(l, t & 1, z, H));
+    else
+      fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
+    return;
+  }
   if (DROP && l > 0) {
     // nn.LSTM inter-layer dropout: layer l reads drop(h_{l-1, t})
     const XDrop xd{drop_site(dr.seed, 2, dr.step, l - 1), dr.thr_lstm, dr.sc_lstm,
@@ -416,7 +443,13 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
           o1 = gi->off[q][1];
         }
       const SegGateImg<2> lbi{{ib + o0, ib + o1}, {cin, H}};
-      gemm_mainloop<CfgGate>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
+      if constexpr (HIMG) {  // (layer 0: the XG table covers the input segment, kbeg = cin)
+        const char* ph = hi->block(l, (t + 1) & 1, z, H);
+        const HImgA<2> lai{{l > 0 ? hi->block(l - 1, t & 1, z, H) : ph, ph}, {cin, H}};
+        gemm_mainloop<CfgGate>(lai, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
+      } else {
+        gemm_mainloop<CfgGate>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
+      }
     } else {
       const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
       gemm_mainloop<CfgGate>(la, lbt, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
@@ -432,7 +465,9 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     if (sum == 12345.678f) Gz[threadIdx.x] = sum;  // (never true in practice; the MFMAs stay)
     return;
   }
-  if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1) {
+  if constexpr (HIMG) {
+    fwd_cell_t<H, CfgGate, true, true>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt, hi->block(l, t & 1, z, H));
+  } else if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1) {
     fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
   } else {
     static_assert(!SMAML_XG_DEDUP_DEFAULT || (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1),
@@ -467,21 +502,23 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
 
 // The dropout variant holds the mask state beside the 4-gate tile: it gets the register budget
 // of 3 waves/SIMD instead of 4 (no spill).
-template <int H, bool IMG>
+template <int H, bool IMG, bool HIMG = false>
 __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                                       float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi, XgDedup xd) {
+                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi, XgDedup xd,
+                                                      HImgs hi) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
-  lstm_fwd_step<H, false, IMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi, xd.xg, xd.zstride,
-                               xd.N);
+  lstm_fwd_step<H, false, IMG, HIMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi, xd.xg,
+                                     xd.zstride, xd.N, &hi);
 }
 
 // Layer 0's input projection of a step whose every task reads B consecutive windows, once per distinct
 // stream row (kernels.h XgDedup): out[z][r][g H + j] = F_row(r) . W_ih0[g H + j] with the gate GEMM's own
-// tile (CfgGate), column mapping, K order and weight images, so the gate kernel that starts its
-// accumulators from these rows and adds the recurrent segment computes bitwise what it computes
-// with the input segment in its own K loop. Compact row r: r < M -> F[0][r] (the t = 0 rows, window
+// tile (CfgGate), column mapping, K order and weight images. The tangent gate kernel starts its
+// accumulators from these rows and adds the recurrent segment: bitwise what it computes with the input
+// segment in its own K loop. The primal gate kernel adds the row in its epilogue (after the recurrent
+// products and the bias; loading it into the accumulators spilled): equal up to f32 rounding. Compact row r: r < M -> F[0][r] (the t = 0 rows, window
 // b = r / N); else stream row s = (r - M) / N + 1, read from the (window, step) slot (s - t, t) with
 // t = min(s, T - 1) (the GCN wrote every slot of that stream row with the same features).
 struct XgRowsA {
@@ -843,13 +880,20 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   count_variant(w, V_FWD);
   XgDedup xd = w.xgd;
   if (xd.src != theta) xd.xg = nullptr;  // (a table of other weights is never read)
-  if (w.gimg.th && w.gimg_src == theta) {
+  if (w.himg.p) {
+    // (run_lstm set the images for the whole sweep only with the gate images and the XG table of theta and
+    // every diagonal on these tiles: every reader of an image runs after its writer)
+    count_variant(w, V_FWD_IMG);
+    count_variant(w, V_FWD_HIMG);
+    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, true, true><<<grid, CfgGate::NTH, 0, s>>>(
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd, w.himg)));
+  } else if (w.gimg.th && w.gimg_src == theta) {
     count_variant(w, V_FWD_IMG);
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, true><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd)));
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd, HImgs{})));
   } else {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, false><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd)));
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd, HImgs{})));
   }
 }
 
@@ -1448,120 +1492,6 @@ __global__ SMAML_BWD_ATTR __launch_bounds__(CfgNN::NTH) void k_lstm_bwd_step(con
     bwd_cell<H, CfgNN, false>(acc, smem, Gz, dGz, dhz, Cz, dHhead + (int64_t)z * M * H, dcz, m0, n0, t, T, M);
 }
 
-// ---- push BPTT (knob bptt_push) ---------------------------------------------------------------
-// The pull step above reads dG(l+1, t) and dG(l, t+1) as GEMM operands, so every dG is read twice
-// from HBM (once by each consumer) besides the weight gradient's read. The push step inverts it: step
-// (l, t) first runs its cell backward from the dh partial sums its two producers left,
-//   dh(l, t) = Pup(l, t) + Prec(l, t) [+ dh_T of the head at the top layer's last step],
-// writes dG(l, t), and then forms its consumers' partial sums from that dG tile (re-read from the
-// L2 it was just written through):
-//   Prec(l, t-1) = dG(l, t) . W_hh(l),   Pup(l-1, t) = dG(l, t) . W_ih(l)   ([M][H] each).
-// Same products, same diagonal order; the sum dh = Pup + Prec rounds once more than the fused K loop
-// (not bitwise equal to the pull step). Buffers (Work::Prec / Pup): Prec[l] is read and then written
-// by the same workgroup (the row tile of layer l's one problem per diagonal); Pup by the parity of t, so
-// a diagonal's writers (l + 1, t - 1) and readers (l, t) of layer l's slot never share one.
-#ifndef SMAML_BWD_PUSH_WPE
-#define SMAML_BWD_PUSH_WPE 3  // 3 workgroups of 4 waves per CU (<= 168 registers; 2 without the bound)
-#endif
-template <int H, class C, bool CHECK>
-__device__ __forceinline__ void bwd_cell_push_(const float* Gz, float* dGz, float* __restrict__ dhz,
-                                               const float* __restrict__ Cz, const float* __restrict__ hd,
-                                               const float* __restrict__ pu, const float* __restrict__ pr,
-                                               float* __restrict__ dcz, int m0, int n0, int t, int T, int M) {
-  constexpr int G4 = 4 * H;
-  constexpr int GPR = C::BN / 4;
-  constexpr int NIT = C::BM * GPR / C::NTH;
-  static_assert(NIT * C::NTH == C::BM * GPR, "epilogue items");
-  const bool first = (t == T - 1), past = t > 0;
-  const int64_t pM = past ? (int64_t)M * H : 0;
-  const int64_t tM = (int64_t)t * M;
-#pragma unroll 1
-  for (int k = 0; k < NIT; ++k) {
-    const int item = (int)threadIdx.x + C::NTH * k;
-    const int r = item / GPR;
-    int m = m0 + r, j = n0 + 4 * (item % GPR);
-    const bool ok = !CHECK || (m < M && j < H);
-    if (CHECK) {  // out-of-range items read a valid element (their results are not stored)
-      m = min(m, M - 1);
-      j = min(j, H - 4);
-    }
-    const int64_t row = tM + m, oc = (int64_t)m * H + j;
-    const float* gp = Gz + row * G4 + j;
-    float4 g[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) g[q] = ld4(gp + q * H);
-    const float4 cp = sel4(past, ld4(Cz + row * H - pM + j)), dc = sel4(!first, ld4(dcz + oc));
-    float4 dh = f4zero();
-    if (pu) dh = ld4(pu + oc);
-    if (pr) dh = add4(dh, ld4(pr + oc));
-    if (hd) dh = add4(dh, ld4(hd + oc));
-    if (!ok) continue;
-    float4 o[4], odc;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gi = f4get(g[0], e), gf = f4get(g[1], e), gg = f4get(g[2], e), go = f4get(g[3], e);
-      const float d = f4get(dh, e);
-      const float tc = tanhf_(lstm_cell_c(gi, gf, gg, f4get(cp, e)));
-      const float dct = f4get(dc, e) + d * go * (1.f - tc * tc);
-      f4set(o[0], e, dct * gg * gi * (1.f - gi));
-      f4set(o[1], e, dct * f4get(cp, e) * gf * (1.f - gf));
-      f4set(o[2], e, dct * gi * (1.f - gg * gg));
-      f4set(o[3], e, d * tc * go * (1.f - go));
-      f4set(odc, e, dct * gf);
-    }
-    float* dp = dGz + row * G4 + j;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) st4(dp + q * H, o[q]);
-    st4(dcz + oc, odc);
-    if (dhz) st4(dhz + row * H + j, dh);
-  }
-}
-
-template <int H, class C>
-__global__ __attribute__((amdgpu_waves_per_eu(SMAML_BWD_PUSH_WPE))) __launch_bounds__(C::NTH) void k_lstm_bwd_push(
-    const float* GsAll, float* dGAll, float* __restrict__ dhAll, const float* __restrict__ CsAll,
-    const float* __restrict__ dHhead, float* __restrict__ dcAll, float* Prec, float* Pup, int64_t lsz,
-    const float* __restrict__ theta, int64_t tstride, BwdWave wv, int L, int T, int M) {
-  __shared__ float smem[epi_smem_floats<C>()];
-  constexpr int G4 = 4 * H;
-  const Blk bk = xcd_block();
-  int mb;
-  const int p = bwd_block(wv, bk.x, mb);
-  mb += wv.tm0;
-  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
-  const LayerOff lo = wave_sel(wv.lo, p);
-  const int z = bk.z, Z = (int)gridDim.z;
-  const int m0 = mb * C::BM, n0 = bk.y * C::BN;
-  const int64_t slab = (int64_t)z * T * M, MH = (int64_t)M * H;
-  const float* th = theta + (int64_t)z * tstride;
-  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;
-  float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;
-  float* dhz = dhAll ? dhAll + (int64_t)l * lsz + slab * H : nullptr;
-  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
-  float* dcz = dcAll + ((int64_t)l * Z + z) * MH;
-  float* prec = Prec + ((int64_t)l * Z + z) * MH;
-  const float* pu = l + 1 < L ? Pup + ((int64_t)((t & 1) * L + l) * Z + z) * MH : nullptr;
-  const float* pr = t + 1 < T ? prec : nullptr;
-  const float* hd = (l == L - 1 && t == T - 1) ? dHhead + (int64_t)z * MH : nullptr;
-  if (m0 + C::BM <= M && n0 + C::BN <= H)
-    bwd_cell_push_<H, C, false>(Gz, dGz, dhz, Cz, hd, pu, pr, dcz, m0, n0, t, T, M);
-  else
-    bwd_cell_push_<H, C, true>(Gz, dGz, dhz, Cz, hd, pu, pr, dcz, m0, n0, t, T, M);
-  __syncthreads();  // this tile's dG rows (every column) are written: the consumers' GEMMs read them
-  const SegKCt<1> la{{dGz + (int64_t)t * M * G4}, {G4}, M};
-  Acc<C> acc;
-  if (t > 0) {
-    acc.zero();
-    gemm_mainloop<C>(la, SegMCt<1>{{th + lo.whh}, {G4}, H}, m0, n0, 0, G4, acc, smem);
-    store_acc_rows<C>(acc, prec, m0, n0, M, H);
-  }
-  if (l > 0) {
-    acc.zero();
-    gemm_mainloop<C>(la, SegMCt<1>{{th + lo.wih}, {G4}, lo.cin}, m0, n0, 0, G4, acc, smem);
-    store_acc_rows<C>(acc, Pup + ((int64_t)((t & 1) * L + l - 1) * Z + z) * MH, m0, n0, M, lo.cin);
-  }
-}
-
 // Split-K BPTT step for small grids (see k_lstm_fwd_part): partial dh over a K-tile range of the
 // fused [above | next] GEMM, then k_lstm_bwd_cell sums the partials in order and runs bwd_cell.
 template <int H, class CfgNN>
@@ -1712,27 +1642,28 @@ void launch_lstm_bwd_wave(hipStream_t s, const Dims& d, const Work& w, int e, co
   const int ntm = (w.M + CfgBwd::BM - 1) / CfgBwd::BM, ntn = (d.H + CfgBwd::BN - 1) / CfgBwd::BN;
   bwd_wave(d, w, po, e, ntm, false, wv);
   if (wv.n == 0) return;
-  // row chunks (nch > 1) always run the big tiles: every diagonal of a chunk must touch only its rows,
-  // or a chunk's next diagonal would race with another stream's whole-row launch
-  const bool big = nch > 1 || (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min;
-  if (nch > 1) {  // this launch's row tiles only
+#define SMAML_BWD_STEP(CFG, D_)                                                                               \
+  SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
+                            w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
+  if (nch > 1) {
+    // A row chunk launches ONLY its own row tiles, always on the big tiles, whatever the diagonal's size:
+    // a whole-row launch here would race the other chunks' streams (round 5's config-5 corner diagonals).
+    // No other branch of this function is reachable for a chunk.
     const int lo = (int)((int64_t)ntm * chunk / nch), hi = (int)((int64_t)ntm * (chunk + 1) / nch);
     if (hi <= lo) return;
     bwd_wave(d, w, po, e, hi - lo, false, wv);
     wv.tm0 = lo;
-  }
-  if (w.push) {  // (the caller chose the push form for the whole sweep: big tiles, no dropout)
-    count_variant(w, V_BWD_PUSH);
+    count_variant(w, V_BWD_BIG);
     dim3 grid(wv.off[wv.n], ntn, w.Z);
-    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_push<HT, CfgBwd><<<grid, CfgBwd::NTH, 0, s>>>(
-                              w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, w.Prec, w.Pup, lsz, theta, tstride, wv, d.L, d.T,
-                              w.M)));
+    if (w.drop.lstm()) {
+      SMAML_BWD_STEP(CfgBwd, true);
+    } else {
+      SMAML_BWD_STEP(CfgBwd, false);
+    }
     return;
   }
-#define SMAML_BWD_STEP(CFG, D_)                                                                               \
-  SMAML_DISPATCH_H(d.H, k_lstm_bwd_step<HT, CFG, D_><<<grid, CFG::NTH, 0, s>>>(                                  \
-                            w.Gs, w.dG, w.dh, w.Cs, w.dH, w.dc, lsz, theta, tstride, wv, d.L, d.T, w.M, w.drop))
   // threshold in 64-row tile units (the knob predates the 128-row tile)
+  const bool big = (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwd::BM / 64) >= w.kn.bwd_big_min;
   if (big) {
     count_variant(w, V_BWD_BIG);
     dim3 grid(wv.off[wv.n], ntn, w.Z);
@@ -2176,216 +2107,6 @@ void launch_dg_rowsum(hipStream_t s, const Dims& d, const Work& w, const float* 
                                   (int64_t)rows * G4);
 }
 
-// ---- warp-specialised weight gradients (round 4) ---------------------------------------------
-// The staged mainloop above has every wave load, split and store its share of the next K-tile AFTER its
-// MFMAs, and the two waves of a SIMD belong to the same workgroup, so they reach that VALU phase
-// together and the MFMA pipe idles through it (MFMA busy 0.57; ~170 VALU per 48 MFMAs per wave).
-// Here one 8-wave workgroup per CU splits the roles: waves 0-3 (one per SIMD) only read bf16 fragments
-// and issue MFMAs -- a 256 x 128 output tile, 64 x 128 per wave, 48 v_mfma_f32_32x32x16_bf16 per K-tile,
-// back to back -- while waves 4-7 (the other wave of each SIMD) load the operand tiles two K-tiles
-// ahead into registers, split them into the bf16 planes and store them into a 3-stage LDS ring. The
-// producer's VALU issues in the 24 of every 32 cycles an MFMA leaves the SIMD's vector issue free. One
-// workgroup barrier per K-tile: stage kt % 3 is read by the MFMA waves in iteration kt while the
-// producers fill stage (kt + 2) % 3, last read in iteration kt - 1. The producers also form the bias
-// column sums (each producer thread always stages the same 4 gate rows). Same products in the same
-// per-accumulator order as k_wgrad: bitwise-identical weight sums, bias sums up to summation order.
-// Layout conditions (wgrad_ws_ok): 4H % 256 == 0 and both column segments multiples of 128.
-#ifndef SMAML_WGRAD_WS
-#define SMAML_WGRAD_WS 1
-#endif
-#ifndef SMAML_WS_PRIO
-#define SMAML_WS_PRIO 1  // 1: MFMA waves at raised priority over their MFMA phase; 2: producer waves raised instead
-#endif
-#ifndef SMAML_WS_MW
-#define SMAML_WS_MW 8  // MFMA waves of k_wgrad_ws: 4 (64 x 128 each, one per SIMD) or 8 (32 x 128, two per SIMD)
-#endif
-template <int MW>
-using CfgWSm = GemmCfg<256, 128, MW, 1, false, false, 16, 2, 3, false>;  // the MFMA waves' view of the tile
-using CfgWS = CfgWSm<SMAML_WS_MW>;
-constexpr int WS_NST = 3;
-constexpr int WS_SA = CfgWS::AImg::BYTES, WS_SB = CfgWS::BImg::BYTES, WS_STAGE = WS_SA + WS_SB;
-constexpr int WS_NP = 8;                          // producer waves
-constexpr int WS_NTH = 64 * (SMAML_WS_MW + WS_NP);  // MFMA waves + producer waves
-constexpr int WS_NPT = 64 * WS_NP;                 // producer threads (512)
-static_assert(WS_NPT == 256 * 16 / 8, "one 8-row A chunk per producer thread per K-tile");
-static_assert(WS_NST * WS_STAGE <= 160 * 1024 - 8192, "LDS ring");
-
-bool wgrad_ws_ok(int Mrows, int c1, int c2) {
-  return SMAML_WGRAD_WS && CfgTN::X6S && Mrows % 256 == 0 && c1 % 128 == 0 && c2 % 128 == 0 && c1 + c2 > 0;
-}
-
-// A producer thread's share of one K-tile: one 8-row chunk of A (k-row p / 32, gate rows 8 (p % 32)
-// .. +7) and, for the first 256 producer threads (uniform per wave), one 8-row chunk of B (k-row
-// p / 16, tile columns 8 (p % 16) .. +7). 8 rows = 16 B per bf16 plane: one ds_write_b128 per plane
-// (the wide store runs at full rate from one wave per SIMD; ds_write_b64 needs ~4).
-struct WsRegs {
-  float4 a[2], b[2];
-};
-
-__device__ __forceinline__ float4 sel0(bool keep, const float4& v) {
-  return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
-}
-__device__ __forceinline__ void ws_fetch(const float* __restrict__ A, int Mrows, const WgB& b, int m0, int n0,
-                                         int64_t k0, int p, WsRegs& r) {
-  // Branch-free (no control flow between a load and its use, so the waitcnt pass keeps the two K-tiles
-  // of prefetch in flight): rows are clamped into the matrix and out-of-range ones selected to zero.
-  // A: rows k < K.
-  {
-    const int64_t k = k0 + p / 32;
-    const bool ok = k < b.K;
-    const float* src = A + (ok ? k : b.K - 1) * Mrows + m0 + 8 * (p % 32);
-    r.a[0] = sel0(ok, ld4(src));
-    r.a[1] = sel0(ok, ld4(src + 4));
-  }
-  // B: source rows kk = k - shift in [0, kmax] of the tile's column segment (h_{t-1} rows before
-  // Mshift and rows k >= K are zeros; an absent segment, the tangent pass's Rx at layer 0, is zeros)
-  const bool seg1 = n0 < b.c1;  // tile inside one column segment (uniform)
-  const float* base = seg1 ? b.B1 : b.B2;
-  const int ld = seg1 ? b.c1 : b.c2;
-  const int64_t shift = seg1 ? 0 : b.Mshift, kmax = b.K - 1 - shift;
-  const int64_t kk = k0 + (p & 255) / 16 - shift;
-  const bool ok = base != nullptr && kk >= 0 && kk <= kmax && p < 256;
-  const float* src = (base ? base : A) + (ok ? kk * ld : 0) + (seg1 ? n0 : n0 - b.c1) + 8 * (p % 16);
-  r.b[0] = sel0(ok, ld4(src));
-  r.b[1] = sel0(ok, ld4(src + 4));
-}
-
-__device__ __forceinline__ void split8_store(char* img, int plane, int off, const float4& lo, const float4& hi) {
-  uint2 a0, a1, a2, b0, b1, b2;
-  split4(lo, a0, a1, a2);
-  split4(hi, b0, b1, b2);
-  *reinterpret_cast<uint4*>(img + off) = make_uint4(a0.x, a0.y, b0.x, b0.y);
-  *reinterpret_cast<uint4*>(img + plane + off) = make_uint4(a1.x, a1.y, b1.x, b1.y);
-  *reinterpret_cast<uint4*>(img + 2 * plane + off) = make_uint4(a2.x, a2.y, b2.x, b2.y);
-}
-
-__device__ __forceinline__ void ws_store(char* st, int p, const WsRegs& r, float4 (&cs)[2]) {
-  using IA = CfgWS::AImg;
-  using IB = CfgWS::BImg;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    cs[h].x += r.a[h].x;
-    cs[h].y += r.a[h].y;
-    cs[h].z += r.a[h].z;
-    cs[h].w += r.a[h].w;
-  }
-  split8_store(st, IA::PLANE, IA::mc(p / 32, 16 * (p % 32)), r.a[0], r.a[1]);
-  if (p < 256) split8_store(st + WS_SA, IB::PLANE, IB::mc(p / 16, 16 * (p % 16)), r.b[0], r.b[1]);
-}
-
-// Ring barrier: LDS stores retired (lgkmcnt), then s_barrier -- NOT __syncthreads, whose workgroup
-// release fence also drains vmcnt, i.e. would wait for the producers' prefetch loads issued two K-tiles
-// ahead and expose their full latency every K-tile.
-__device__ __forceinline__ void ws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-__global__ __launch_bounds__(WS_NTH) void k_wgrad_ws(const float* __restrict__ A, int64_t a_zstride, int Mrows, WgB lb,
-                                                     int64_t b1_zstride, int64_t b2_zstride, int64_t kchunk, int ntn,
-                                                     int ntile, int nsplit, int ngroups, float* __restrict__ part,
-                                                     int ldp, int with_bias, WgPair pr) {
-  __shared__ __attribute__((aligned(16))) char ring[WS_NST * WS_STAGE];
-  const int L = (int)blockIdx.x;
-  const int j = L >> 3;  // XCD-aware: the tiles of one (split, task) group 8 blocks apart (wgrad_block)
-  const int g = (j / ntile) * 8 + (L & 7), tile = j - (j / ntile) * ntile;
-  if (g >= ngroups) return;
-  const int z = g / nsplit, split = g - z * nsplit;
-  const int tm = tile / ntn, tn = tile - tm * ntn;
-  const bool sec = pr.A2 != nullptr && split >= pr.nsplit1;
-  if (sec) {
-    A = pr.A2;
-    lb.B1 = pr.B1s;
-    lb.B2 = pr.B2s;
-    with_bias = 0;
-  }
-  const float* Az = A + (int64_t)z * a_zstride;
-  WgB b = lb;
-  if (b.B1) b.B1 += (int64_t)z * b1_zstride;
-  if (b.B2) b.B2 += (int64_t)z * b2_zstride;
-  const int64_t kbeg = (int64_t)(sec ? split - pr.nsplit1 : split) * kchunk;
-  const int64_t kend = kbeg + kchunk < lb.K ? kbeg + kchunk : lb.K;
-  const int nkt = (int)((kend - kbeg + 15) / 16);
-  // an even K-tile count (ws plans use 32-row-multiple slices, so only the last slice can be odd; its
-  // padding tile lies past K and is zeros)
-  const int nkt2 = (nkt + 1) & ~1;
-  const int m0 = tm * 256, n0 = tn * 128;
-  const bool mfma_wave = threadIdx.x < 64 * SMAML_WS_MW;
-  float* P = part + ((int64_t)z * nsplit + split) * (int64_t)Mrows * ldp;
-  if (mfma_wave) {
-    Acc<CfgWS> acc;
-    acc.zero();
-    ws_barrier();  // stages 0 and 1 filled
-    for (int kt = 0; kt < nkt2; ++kt) {
-      const char* st = ring + (kt % WS_NST) * WS_STAGE;
-#if SMAML_WS_PRIO == 1
-      __builtin_amdgcn_s_setprio(1);
-#endif
-      mma_tile_x6s<CfgWS>(st, st + WS_SA, acc);
-#if SMAML_WS_PRIO == 1
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      ws_barrier();
-    }
-    __syncthreads();  // (matches the producers' bias-reduce barrier)
-#pragma unroll
-    for (int i = 0; i < CfgWS::WTM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < CfgWS::WTN; ++jj) {
-        const int c = n0 + acc_col<CfgWS>(jj);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) P[(int64_t)(m0 + acc_row<CfgWS>(i, r)) * ldp + c] = acc.v[i][jj][r];
-      }
-    return;
-  }
-  // producers
-  const int p = (int)threadIdx.x - 64 * SMAML_WS_MW;
-#if SMAML_WS_PRIO == 2
-  __builtin_amdgcn_s_setprio(1);
-#endif
-  float4 cs[2] = {f4zero(), f4zero()}, nocs[2] = {f4zero(), f4zero()};
-  WsRegs r0, r1;
-  // prologue: tiles 0 and 1 into stages 0 and 1, tiles 2 and 3 in flight (a tile past the slice is
-  // loaded but never stored into a stage the MFMA waves read: its rows are zeros (k >= K) or are
-  // another slice's, unread, and its column sums go to nocs)
-  ws_fetch(Az, Mrows, b, m0, n0, kbeg, p, r0);
-  ws_fetch(Az, Mrows, b, m0, n0, kbeg + 16, p, r1);
-  ws_store(ring, p, r0, cs);
-  ws_fetch(Az, Mrows, b, m0, n0, kbeg + 32, p, r0);
-  ws_store(ring + WS_STAGE, p, r1, nkt > 1 ? cs : nocs);
-  ws_fetch(Az, Mrows, b, m0, n0, kbeg + 48, p, r1);
-  ws_barrier();
-  // iteration kt: store tile kt + 2 (registers loaded two iterations earlier) into stage (kt + 2) % 3,
-  // then load tile kt + 4 into the freed registers; unrolled by two (nkt2 is even) so each register
-  // set is static and no load sits under a branch
-  for (int kt = 0; kt < nkt2; kt += 2) {
-    ws_store(ring + ((kt + 2) % WS_NST) * WS_STAGE, p, r0, kt + 2 < nkt ? cs : nocs);
-    ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 4) * 16, p, r0);
-    ws_barrier();
-    ws_store(ring + ((kt + 3) % WS_NST) * WS_STAGE, p, r1, kt + 3 < nkt ? cs : nocs);
-    ws_fetch(Az, Mrows, b, m0, n0, kbeg + (int64_t)(kt + 5) * 16, p, r1);
-    ws_barrier();
-  }
-  // bias column sums: gate rows 8q .. 8q+7 (q = p % 32) over the 16 producer threads sharing q
-  float* red = reinterpret_cast<float*>(ring);
-  st4(red + 8 * p, cs[0]);
-  st4(red + 8 * p + 4, cs[1]);
-  __syncthreads();
-  if (tn == 0 && p < 64) {  // thread p: gate rows 4p .. 4p+3 = half (p & 1) of chunk q = p / 2
-    const int q = p >> 1, hh = p & 1;
-    float4 v = ld4(red + 8 * q + 4 * hh);
-#pragma unroll
-    for (int t = 1; t < 16; ++t) {
-      const float4 u = ld4(red + 8 * (q + 32 * t) + 4 * hh);
-      v.x += u.x;
-      v.y += u.y;
-      v.z += u.z;
-      v.w += u.w;
-    }
-    const float e[4] = {v.x, v.y, v.z, v.w};
-    const int ncols = lb.c1 + lb.c2;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) P[(int64_t)(m0 + 4 * p + c) * ldp + ncols] = with_bias ? e[c] : 0.f;
-  }
-}
-
 // Several weight gradients in ONE launch (the LSTM layers of a small-grid backward: at batch 1 each
 // layer alone fills too little of the chip and its K loop is short). Problem q owns blocks
 // [blk[q], blk[q+1]) and partial slabs from part + poff[q].
@@ -2474,11 +2195,9 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
                 WgradPlan& p, bool multi) {
   const int ncols = c1 + c2;
   const int ldp = ncols + 1;
-  // (no masked-B variant of k_wgrad_ws: with LSTM dropout on, the staged tiles below)
-  const bool ws = !multi && w.kn.wgrad_ws && !w.drop.lstm() && wgrad_ws_ok(Mrows, c1, c2);
-  const bool wide = !ws && !multi && SMAML_WGRAD_WIDE && w.kn.wgrad_wide && CfgTW::X6S && ncols % CfgTW::BN == 0 &&
+  const bool wide = !multi && SMAML_WGRAD_WIDE && w.kn.wgrad_wide && CfgTW::X6S && ncols % CfgTW::BN == 0 &&
                     Mrows % CfgTW::BM == 0;
-  const int BMc = ws ? CfgWS::BM : wide ? CfgTW::BM : CfgTN::BM, BNc = ws ? CfgWS::BN : wide ? CfgTW::BN : CfgTN::BN;
+  const int BMc = wide ? CfgTW::BM : CfgTN::BM, BNc = wide ? CfgTW::BN : CfgTN::BN;
 
   static_assert(CfgTW::BK == CfgTN::BK, "one split-K K-tile for both tiles");
   const int ntm = (Mrows + BMc - 1) / BMc;
@@ -2486,16 +2205,14 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   const int64_t ktiles = (K + CfgTN::BK - 1) / CfgTN::BK;
   // aim for SMAML_WGRAD_THREADS threads in all, at least 8 K-tiles per split, bounded by the slab buffer
   const int nth = wide ? CfgTW::NTH : CfgTN::NTH;
-  const int64_t target = w.kn.wgrad_threads > 0 ? w.kn.wgrad_threads : SMAML_WGRAD_THREADS;
-  int64_t nsplit = (target / nth) / ((int64_t)ntm * ntn * w.Z);
+  int64_t nsplit = (SMAML_WGRAD_THREADS / nth) / ((int64_t)ntm * ntn * w.Z);
   if (nsplit < 1) nsplit = 1;
-  const int64_t min_kt = std::max(1, w.kn.wgrad_min_kt);
+  constexpr int64_t min_kt = 8;
   if (nsplit > ktiles / min_kt) nsplit = ktiles / min_kt > 0 ? ktiles / min_kt : 1;
   const int64_t per_split = (int64_t)w.Z * Mrows * ldp;
   if (nsplit * per_split > w.wpart_floats) nsplit = w.wpart_floats / per_split;
   if (nsplit < 1) nsplit = 1;
   int64_t kt_per = (ktiles + nsplit - 1) / nsplit;
-  if (ws) kt_per += kt_per & 1;  // k_wgrad_ws runs K-tiles in pairs: every slice but the last even
   const int64_t kchunk = kt_per * CfgTN::BK;
   nsplit = (K + kchunk - 1) / kchunk;
   p.A = A;
@@ -2525,14 +2242,12 @@ void plan_wgrad(const Work& w, const float* A, int64_t a_zstride, int Mrows, con
   p.nsplit = (int)nsplit;
   p.kchunk = kchunk;
   p.wide = wide;
-  p.ws = ws;
 }
 
 bool pair_wgrad(WgradPlan& p, const Work& w, const float* A2, const float* B1s, const float* B2s) {
   const int64_t ktiles = (p.K + CfgTN::BK - 1) / CfgTN::BK;
   const int64_t n1 = std::max<int64_t>(1, p.nsplit / 2);
   int64_t kt_per = (ktiles + n1 - 1) / n1;
-  if (p.ws) kt_per += kt_per & 1;  // (k_wgrad_ws: even slices)
   const int64_t kchunk = kt_per * CfgTN::BK;
   const int64_t nsplit1 = (p.K + kchunk - 1) / kchunk;
   // 2 * nsplit1 slices can exceed the planned count (a plan of one slice gives two); check them
@@ -2576,10 +2291,6 @@ void launch_wgrad_gemm(hipStream_t s, const WgradPlan& p) {
                                                               p.b2_zstride, p.kchunk, p.ntn, ntile, p.nsplit, ngroups,
                                                               p.part, p.ldp, p.with_bias ? 1 : 0, p.drop, -1, np,
                                                               p.gather);
-  } else if (p.ws) {
-    k_wgrad_ws<<<grid, WS_NTH, 0, s>>>(p.A, p.a_zstride, p.Mrows, lb, p.b1_zstride, p.b2_zstride, p.kchunk, p.ntn,
-                                       ntile, p.nsplit, ngroups, p.part, p.ldp, p.with_bias ? 1 : 0,
-                                       WgPair{p.A2, p.B1s, p.B2s, p.nsplit1});
   } else if (p.wide) {
     if (drop)
       SMAML_WGRAD_LAUNCH(CfgTW, true);

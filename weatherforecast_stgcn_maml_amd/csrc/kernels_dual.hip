@@ -809,127 +809,6 @@ __global__ SMAML_BWDD_ATTR __launch_bounds__(CfgNND::NTH) void k_lstm_bwd_dual(c
   }
 }
 
-// Push form of the kept step's tangent BPTT (knob bptt_push; see kernels.hip k_lstm_bwd_push): the
-// tangent cell backward first, R(dh)(l, t) = RPup(l, t) + RPrec(l, t) [+ R dh_T of the head], writing
-// R(dG) over R(G) and both carries; then the consumers' partial sums from R(dG)(l, t) and the kept
-// dG(l, t), each read once as a GEMM operand:
-//   RPrec(l, t-1) = R(dG) . W_hh(l) + dG . U_hh(l),   RPup(l-1, t) = R(dG) . W_ih(l) + dG . U_ih(l).
-template <int H, class C, bool CHECK>
-__device__ __forceinline__ void bwd_dual_push_cell_(const float* Gz, float* RGz, const float* __restrict__ dhz,
-                                                    const float* __restrict__ Cz, const float* __restrict__ RCz,
-                                                    const float* __restrict__ rhd, const float* __restrict__ rpu,
-                                                    const float* __restrict__ rpr, float* __restrict__ dcz,
-                                                    float* __restrict__ rdcz, int m0, int n0, int t, int T, int M) {
-  constexpr int G4 = 4 * H;
-  constexpr int GPR = C::BN / 4;
-  constexpr int NIT = C::BM * GPR / C::NTH;
-  static_assert(NIT * C::NTH == C::BM * GPR, "epilogue items");
-  const bool first = (t == T - 1), past = t > 0;
-  const int64_t pM = past ? (int64_t)M * H : 0;
-  const int64_t tM = (int64_t)t * M;
-#pragma unroll 1
-  for (int k = 0; k < NIT; ++k) {
-    const int item = (int)threadIdx.x + C::NTH * k;
-    const int r = item / GPR;
-    int m = m0 + r, j = n0 + 4 * (item % GPR);
-    const bool ok = !CHECK || (m < M && j < H);
-    if (CHECK) {
-      m = min(m, M - 1);
-      j = min(j, H - 4);
-    }
-    const int64_t row = tM + m, oc = (int64_t)m * H + j;
-    float4 g[4], rg[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      g[q] = ld4(Gz + row * G4 + j + q * H);
-      rg[q] = ld4(RGz + row * G4 + j + q * H);
-    }
-    const float4 dh4 = ld4(dhz + row * H + j);
-    const float4 cp4 = sel4(past, ld4(Cz + row * H - pM + j)), rcp4 = sel4(past, ld4(RCz + row * H - pM + j));
-    const float4 dc4 = sel4(!first, ld4(dcz + oc)), rdc4 = sel4(!first, ld4(rdcz + oc));
-    float4 rdh4 = f4zero();
-    if (rpu) rdh4 = ld4(rpu + oc);
-    if (rpr) rdh4 = add4(rdh4, ld4(rpr + oc));
-    if (rhd) rdh4 = add4(rdh4, ld4(rhd + oc));
-    if (!ok) continue;
-    float4 o[4], odc, ordc;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float dh = f4get(dh4, e), rdh = f4get(rdh4, e);
-      const float gi = f4get(g[0], e), gf = f4get(g[1], e), gg = f4get(g[2], e), go = f4get(g[3], e);
-      const float ri = f4get(rg[0], e), rf = f4get(rg[1], e), rgg = f4get(rg[2], e), ro = f4get(rg[3], e);
-      const float cp = f4get(cp4, e), rcp = f4get(rcp4, e);
-      const float c = lstm_cell_c(gi, gf, gg, cp), rc = lstm_cell_rc(gi, gf, gg, cp, ri, rf, rgg, rcp);
-      const float tc = tanhf_(c);
-      const float s2 = 1.f - tc * tc;
-      const float rtc = s2 * rc;
-      const float dct = f4get(dc4, e) + dh * go * s2;
-      const float rdct = f4get(rdc4, e) + rdh * go * s2 + dh * ro * s2 - 2.f * dh * go * tc * rtc;
-      const float si = gi * (1.f - gi), sf = gf * (1.f - gf), so = go * (1.f - go), sg = 1.f - gg * gg;
-      f4set(o[0], e, rdct * gg * si + dct * rgg * si + dct * gg * (1.f - 2.f * gi) * ri);
-      f4set(o[1], e, rdct * cp * sf + dct * rcp * sf + dct * cp * (1.f - 2.f * gf) * rf);
-      f4set(o[2], e, rdct * gi * sg + dct * ri * sg - 2.f * dct * gi * gg * rgg);
-      f4set(o[3], e, rdh * tc * so + dh * rtc * so + dh * tc * (1.f - 2.f * go) * ro);
-      f4set(odc, e, dct * gf);
-      f4set(ordc, e, rdct * gf + dct * rf);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) st4(RGz + row * G4 + j + q * H, o[q]);
-    st4(dcz + oc, odc);
-    st4(rdcz + oc, ordc);
-  }
-}
-
-template <int H, class C>
-__global__ SMAML_BWDD_ATTR __launch_bounds__(C::NTH) void k_lstm_bwd_dual_push(
-    const float* GsAll, const float* dGAll, const float* __restrict__ dhAll, float* RGsAll,
-    const float* __restrict__ CsAll, const float* __restrict__ RCsAll, const float* __restrict__ RdHhead,
-    float* __restrict__ dcAll, float* __restrict__ RdcAll, float* RPrec, float* RPup, int64_t lsz,
-    const float* __restrict__ theta, const float* __restrict__ U, int64_t tstride, BwdWave wv, int L, int T, int M) {
-  __shared__ float smem[C::SMEM_FLOATS];
-  constexpr int G4 = 4 * H;
-  const Blk bk = xcd_block();
-  int mb;
-  const int p = bwd_block(wv, bk.x, mb);
-  mb += wv.tm0;
-  const int l = wave_sel(wv.l, p), t = wave_sel(wv.t, p);
-  const LayerOff lo = wave_sel(wv.lo, p);
-  const int z = bk.z, Z = (int)gridDim.z;
-  const int m0 = mb * C::BM, n0 = bk.y * C::BN;
-  const int64_t slab = (int64_t)z * T * M, MH = (int64_t)M * H;
-  const float* th = theta + (int64_t)z * tstride;
-  const float* u = U + (int64_t)z * tstride;
-  const float* Gz = GsAll + (int64_t)l * lsz * 4 + slab * G4;
-  const float* dGz = dGAll + (int64_t)l * lsz * 4 + slab * G4;
-  float* RGz = RGsAll + (int64_t)l * lsz * 4 + slab * G4;
-  const float* dhz = dhAll + (int64_t)l * lsz + slab * H;
-  const float* Cz = CsAll + (int64_t)l * lsz + slab * H;
-  const float* RCz = RCsAll + (int64_t)l * lsz + slab * H;
-  float* dcz = dcAll + ((int64_t)l * Z + z) * MH;
-  float* rdcz = RdcAll + ((int64_t)l * Z + z) * MH;
-  float* rprec = RPrec + ((int64_t)l * Z + z) * MH;
-  const float* rpu = l + 1 < L ? RPup + ((int64_t)((t & 1) * L + l) * Z + z) * MH : nullptr;
-  const float* rpr = t + 1 < T ? rprec : nullptr;
-  const float* rhd = (l == L - 1 && t == T - 1) ? RdHhead + (int64_t)z * MH : nullptr;
-  if (m0 + C::BM <= M && n0 + C::BN <= H)
-    bwd_dual_push_cell_<H, C, false>(Gz, RGz, dhz, Cz, RCz, rhd, rpu, rpr, dcz, rdcz, m0, n0, t, T, M);
-  else
-    bwd_dual_push_cell_<H, C, true>(Gz, RGz, dhz, Cz, RCz, rhd, rpu, rpr, dcz, rdcz, m0, n0, t, T, M);
-  __syncthreads();  // this tile's R(dG) rows are written: the consumers' GEMMs read them
-  const SegKCt<2> la{{RGz + (int64_t)t * M * G4, dGz + (int64_t)t * M * G4}, {G4, G4}, M};
-  Acc<C> acc;
-  if (t > 0) {
-    acc.zero();
-    gemm_mainloop<C>(la, SegMCt<2>{{th + lo.whh, u + lo.whh}, {G4, G4}, H}, m0, n0, 0, 2 * G4, acc, smem);
-    store_acc_rows<C>(acc, rprec, m0, n0, M, H);
-  }
-  if (l > 0) {
-    acc.zero();
-    gemm_mainloop<C>(la, SegMCt<2>{{th + lo.wih, u + lo.wih}, {G4, G4}, lo.cin}, m0, n0, 0, 2 * G4, acc, smem);
-    store_acc_rows<C>(acc, RPup + ((int64_t)((t & 1) * L + l - 1) * Z + z) * MH, m0, n0, M, lo.cin);
-  }
-}
-
 template <class Cfg, bool KEPT>
 static void bwd_dual_grid(hipStream_t s, const Dims& d, const Work& w, const BwdWave& wv, int ntn, const float* theta,
                           const float* U, int64_t tstride) {
@@ -971,23 +850,20 @@ void launch_lstm_bwd_dual_wave(hipStream_t s, const Dims& d, const Work& w, int 
   bwd_wave(d, w, po, e, ntm, true, wv);
   if (wv.n == 0) return;
   const bool kept = w.primal_kept != 0;
-  // (64-row tile units; row chunks always on the big tiles, see launch_lstm_bwd_wave)
-  const bool big = nch > 1 || (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min;
-  if (nch > 1) {  // this launch's row tiles only
+  if (nch > 1) {  // a row chunk: its own row tiles only, always the big tiles (see launch_lstm_bwd_wave)
     const int lo = (int)((int64_t)ntm * chunk / nch), hi = (int)((int64_t)ntm * (chunk + 1) / nch);
     if (hi <= lo) return;
     bwd_wave(d, w, po, e, hi - lo, true, wv);
     wv.tm0 = lo;
-  }
-  if (w.push && kept) {  // (the caller chose the push form for the whole sweep: big tiles, no dropout)
-    count_variant(w, V_BWDD_PUSH);
-    const int64_t lsz = (int64_t)w.Z * d.T * w.M * d.H;
-    dim3 grid(wv.off[wv.n], ntn, w.Z);
-    SMAML_DISPATCH_H(d.H, (k_lstm_bwd_dual_push<HT, CfgBwdD><<<grid, CfgBwdD::NTH, 0, s>>>(
-                              w.Gs, w.dG, w.dh, w.RGs, w.Cs, w.RCs, w.RdH, w.dc, w.Rdc, w.RPrec, w.RPup, lsz, theta,
-                              U, tstride, wv, d.L, d.T, w.M)));
+    count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
+    if (kept)
+      bwd_dual_grid<CfgBwdD, true>(s, d, w, wv, ntn, theta, U, tstride);
+    else
+      bwd_dual_grid<CfgBwdD, false>(s, d, w, wv, ntn, theta, U, tstride);
     return;
   }
+  // (64-row tile units)
+  const bool big = (int64_t)wv.n * ntm * ntn * w.Z * (CfgBwdD::BM / 64) >= w.kn.bwdd_big_min;
   if (big) {
     count_variant(w, kept ? V_BWDD_BIG_KEPT : V_BWDD_BIG);
     if (kept)

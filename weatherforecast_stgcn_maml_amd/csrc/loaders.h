@@ -376,6 +376,34 @@ struct SegGateImg {
   }
 };
 
+// Gate-GEMM A operand [x | h_{t-1}] as pre-split h images (kernels.h HImgs): segment s's image block at
+// p[s], image (row tile m0 / 256, K-tile kt) at + ((m0 >> 8) * (w[s] / 16) + kt) * H_IMG_BYTES, the exact
+// bytes of the staged split's LDS image; every wave copies its share of the 24 1-KB chunks with
+// global_load_lds_dwordx4 (64 lanes x 16 B, lane-contiguous in LDS).
+template <int NS>
+struct HImgA {
+  static constexpr bool kDmaImage = true;
+  const char* p[NS];
+  int w[NS];
+  template <int ROWS, bool KC, int BK, int NTH>
+  __device__ __forceinline__ void issue(char* dst, int m0, int k0) const {
+    static_assert(ROWS == 256 && KC && BK == 16, "h images: 256 rows x 16 k");
+    const char* b;
+    int ws, kk;
+    seg_pick<NS>(p, w, k0, b, ws, kk);
+    const char* src = b + ((int64_t)(m0 >> 8) * (ws / BK) + kk / BK) * H_IMG_BYTES;
+    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    constexpr int CH = H_IMG_BYTES / 1024, NW = NTH / 64;
+#pragma unroll
+    for (int c = 0; c < (CH + NW - 1) / NW; ++c) {
+      const int ch = wave + NW * c;
+      if (CH % NW == 0 || ch < CH)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + ch * 1024 + 16 * lane), (lds_void_t*)(dst + ch * 1024),
+                                         16, 0, 0);
+    }
+  }
+};
+
 // Dropout mask on the x segment of an LSTM layer's input: x = drop(h_{l-1}) of one
 // (task, t) slab; element (m, k) has index base + m*H + k (kernels.h Drop, kind 2).
 struct XDrop {
@@ -632,17 +660,6 @@ __device__ __forceinline__ void sto(float* base, uint32_t byteoff, const float4&
 // Per pass a lane has 2 items: ld(ml, u) issues both items' loads before st(ml, u, pre, v) stores
 // either (ml = tile row, u = tile unit, pre[g] = gate g of units u .. u+3). Starts with a barrier
 // (the mainloop's last LDS reads), leaves the LDS in use until the caller's next barrier.
-#ifndef SMAML_EPI_WAVE_SYNC
-#define SMAML_EPI_WAVE_SYNC 0  // 1: the exchange below syncs each wave alone (its LDS region is its own, and every
-#endif                         // mainloop ends with a workgroup barrier), not the whole workgroup
-// Orders one wave's LDS writes before its own later LDS reads (and vice versa): the DS unit runs a
-// wave's instructions in order, so only the compiler must not move them across.
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <class C, class LD, class ST>
 __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (&badd)[4], float* smem, LD&& ld,
                                                 ST&& st) {
@@ -653,7 +670,7 @@ __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     // p = 0: the mainloop's LDS reads are done; p = 1: pass 0's reads are done
-    if constexpr (SMAML_EPI_WAVE_SYNC) wave_lds_sync(); else __syncthreads();
+    __syncthreads();
 #pragma unroll
     for (int r = 8 * p; r < 8 * p + 8; ++r) {
       const int rl = racc(r) + 4 * h - 16 * p;
@@ -661,7 +678,7 @@ __device__ __forceinline__ void gate_epilogue_t(const Acc<C>& acc, const float (
 #pragma unroll
       for (int g = 0; g < 4; ++g) ws[rl * 128 + (g ^ sw) * 32 + jj] = acc.v[0][g][r] + badd[g];
     }
-    if constexpr (SMAML_EPI_WAVE_SYNC) wave_lds_sync(); else __syncthreads();
+    __syncthreads();
     decltype(ld(0, 0)) v[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
