@@ -57,9 +57,9 @@ def test_packed_parameters_cached_until_changed():
 
 
 def test_untracked_data_writes_are_picked_up():
-    """writes through ``.data`` do not move the version counter. Grad-enabled calls (the
-    training forward, whose vector the backward also uses) always re-pack; under no_grad a storage
-    swap is seen through the data pointer and an in-place ``.data`` write needs invalidate_packed()."""
+    """writes through ``.data`` do not move the version counter. Every call re-packs into
+    the cached buffer, so untracked writes are seen with and without grad (no invalidate_packed() needed);
+    the returned flag marks changes autograd or a storage swap reveals."""
     m, d = _model()
     dev = torch.device("cpu")
     w = m.lstm.weight_hh_l1
@@ -71,10 +71,9 @@ def test_untracked_data_writes_are_picked_up():
     assert fresh and th2 is th and float(th2[off]) == 0.25
     with torch.no_grad():
         m._packed(0, m._trainable_params(), d, dev)
-        w.data -= 0.25                             # untracked, under no_grad: the cache keeps the old copy ...
-        assert float(m._packed(0, m._trainable_params(), d, dev)[0][off]) == 0.25
-        m.invalidate_packed()                      # ... until invalidated
-        assert float(m._packed(0, m._trainable_params(), d, dev)[0][off]) == 0.0
+        w.data -= 0.25                             # untracked, under no_grad: picked up by the re-pack
+        th_ng, changed = m._packed(0, m._trainable_params(), d, dev)
+        assert th_ng is th and float(th_ng[off]) == 0.0 and not changed
         w.data = torch.full_like(w, 2.0)           # storage swap: seen through data_ptr
         th3, fresh3 = m._packed(0, m._trainable_params(), d, dev)
         assert fresh3 and float(th3[off]) == 2.0

@@ -2363,6 +2363,7 @@ struct Rccl {
   int (*comm_abort)(void*) = nullptr;                                      // ncclCommAbort
   int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
   int (*comm_destroy)(void*) = nullptr;
+  int (*comm_finalize)(void*) = nullptr;                                   // ncclCommFinalize (optional)
   const char* (*error_string)(int) = nullptr;
   bool nonblocking() const { return comm_init_rank_config && get_async_error && comm_abort; }
 };
@@ -2387,6 +2388,7 @@ int rccl(Rccl** out) {
       r.comm_abort = (int (*)(void*))dlsym(r.h, "ncclCommAbort");
       r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(r.h, "ncclAllReduce");
       r.comm_destroy = (int (*)(void*))dlsym(r.h, "ncclCommDestroy");
+      r.comm_finalize = (int (*)(void*))dlsym(r.h, "ncclCommFinalize");
       r.error_string = (const char* (*)(int))dlsym(r.h, "ncclGetErrorString");
     }
   }
@@ -2483,9 +2485,22 @@ int smaml_comm_destroy(smaml_ctx* c) {
   if (!c->comm) return SMAML_OK;
   Rccl* r = nullptr;
   TRY(rccl(&r));
-  int rc = r->comm_destroy(c->comm);
-  if (c->comm_nb && rc == NCCL_IN_PROGRESS) rc = 0;  // a non-blocking destroy finishes on its own
+  void* comm = c->comm;
   c->comm = nullptr;
+  if (c->comm_nb && r->comm_finalize) {
+    // non-blocking protocol: finalize (flushes outstanding work, reports its errors), poll it to completion
+    // under the same bound as the init, then destroy; a finalize that never completes is aborted
+    int rc = nccl_wait(r, comm, r->comm_finalize(comm), c->comm_timeout_ms);
+    if (rc != 0) {
+      (void)r->comm_abort(comm);
+      if (rc < 0)
+        return fail(SMAML_EHIP, "ncclCommFinalize: timed out after " + std::to_string(c->comm_timeout_ms) +
+                                    " ms (communicator aborted)");
+      return nccl_fail(r, rc, "ncclCommFinalize");
+    }
+  }
+  int rc = r->comm_destroy(comm);
+  if (c->comm_nb && rc == NCCL_IN_PROGRESS) rc = 0;  // (after finalize the destroy only frees resources)
   return rc ? nccl_fail(r, rc, "ncclCommDestroy") : SMAML_OK;
 }
 

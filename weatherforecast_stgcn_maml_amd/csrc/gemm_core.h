@@ -337,7 +337,16 @@ __device__ __forceinline__ void mma_tile(const float* as, const float* bs, Acc<C
 // costs 5.5 VALU per element per workgroup instead of per wave that reads the fragment.
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef SMAML_DIAG_NOSPLIT
+#define SMAML_DIAG_NOSPLIT 0  // timing diagnostic only (wrong results): 1 = the staged split stores raw bits, no VALU
+#endif
 __device__ __forceinline__ void split4(const float4& v, uint2& p0, uint2& p1, uint2& p2) {
+  if constexpr (SMAML_DIAG_NOSPLIT) {
+    p0 = make_uint2(__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y));
+    p1 = make_uint2(__builtin_bit_cast(uint32_t, v.z), __builtin_bit_cast(uint32_t, v.w));
+    p2 = p0;
+    return;
+  }
   const float x[4] = {v.x, v.y, v.z, v.w};
   uint32_t q0[2], q1[2], q2[2];
 #pragma unroll
@@ -550,59 +559,86 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   }
 }
 
-// The staged mainloop with the global loads issued TWO K-tiles ahead (two register sets): a K-tile's
-// loads are issued before the MFMA phase of the tile before the one they feed, so they have two MFMA
-// phases (not one) to land before the split + LDS store needs them. Two LDS stages, one barrier per
-// K-tile; unrolled by two so each register set is static. The fetch and the store run unconditionally
-// (a fetch past the slice reads rows the loaders return as zeros or rows of another slice; its store
-// goes to the idle stage nobody reads), so no load sits under a branch and the waitcnt pass keeps the
-// next tile's loads in flight across the barrier. Same products in the same order as
-// gemm_mainloop_x6s: bitwise-identical results.
+// Staggered staged mainloop (MI355X_MICROARCH "Two waves per SIMD", item 9). An 8-wave workgroup puts
+// waves w and w + NW/2 on one SIMD; in gemm_mainloop_x6s both run [MFMAs of tile k; split + LDS store of
+// tile k + 1] in lockstep, so the SIMD's matrix pipe idles through both waves' split VALU. Here the
+// second half of the waves runs each iteration the other way round -- [split + store of tile k + 1;
+// MFMAs of tile k] -- with tile k + 1's operands fetched one iteration earlier (the same number of
+// staging registers: each wave holds exactly one tile in flight), so on every SIMD one wave splits while
+// its partner issues MFMAs. Both orders are legal inside an iteration: tile k + 1 goes to the idle stage,
+// last read before the previous barrier. Same loads, splits and products per accumulator as
+// gemm_mainloop_x6s: bitwise-identical results. f32-staged operands only (a DMA image issued two
+// tiles ahead would land in the stage the current MFMAs read).
 template <class C, int IG, class LA, class LB, class Hook>
-__device__ __forceinline__ void gemm_mainloop_x6s_pf2(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
-                                                      Acc<C>& acc, float* smem, Hook& hook) {
-  static_assert(C::X6S && C::X6S_NST == 2 && !has_dma_image<LB>::value, "pf2: staged, two stages, f32 B");
+__device__ __forceinline__ void gemm_mainloop_x6s_stag(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
+                                                       Acc<C>& acc, float* smem, Hook& hook) {
+  constexpr bool DMA_B = has_dma_image<LB>::value;
+  static_assert(C::X6S && C::X6S_NST == 2 && !has_dma_image<LA>::value, "staggered loop: staged f32 A, two stages");
+  static_assert(C::NTH == 512, "staggered loop: two waves per SIMD (8 waves)");
   constexpr int BKc = C::BK;
   constexpr int SA = C::AImg::BYTES;
   char* st0 = reinterpret_cast<char*>(smem);
   const int nkt = (kend - kbeg + BKc - 1) / BKc;
   if (nkt <= 0) return;
-  float4 ra0[C::A_F4], ra1[C::A_F4];
-  BStage<C, LB> rb0, rb1;
-  auto fetch = [&](float4 (&ra)[C::A_F4], BStage<C, LB>& rb, int k0) {
-    fetch_tile<C::BM, C::A_F4, C::NTH, C::A_KC, BKc>(la, m0, k0, ra);
-    rb.fetch(lb, n0, k0, nullptr);
+  const bool late = (threadIdx.x >> 6) >= 4;  // waves 4-7: store first, then the MFMAs
+  AStage<C, LA> ra;
+  BStage<C, LB> rb;
+  auto stage = [&](int kt) { return st0 + (kt & 1) * C::X6S_STAGE; };
+  // f32 operands go to registers; a DMA B image (pre-split weights) is issued straight into tile kt's
+  // stage -- only ever one tile ahead, into the idle stage, by early and late waves alike
+  auto fetch_a = [&](int kt) {
+    ra.fetch(la, m0, kbeg + kt * BKc, nullptr);
+    if constexpr (!DMA_B) rb.fetch(lb, n0, kbeg + kt * BKc, nullptr);
   };
-  auto store = [&](char* st, const float4 (&ra)[C::A_F4], const BStage<C, LB>& rb, bool sum) {
-    if constexpr (has_stage_a<Hook>::value)
-      if (sum) hook.template stage_a<C::A_F4>(ra);
-    store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, BKc, C::MSW>(st, ra);
-    rb.store(st + SA);
+  auto issue_b = [&](int kt) {
+    if constexpr (DMA_B) rb.fetch(lb, n0, kbeg + kt * BKc, stage(kt) + SA);
+  };
+  auto store = [&](int kt) {
+    if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra.r);
+    ra.store(stage(kt));
+    rb.store(stage(kt) + SA);
   };
   auto mma = [&](int kt) {
 #if SMAML_PRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
-    mma_tile_x6s<C, IG>(st0 + (kt & 1) * C::X6S_STAGE, st0 + (kt & 1) * C::X6S_STAGE + SA, acc);
+    mma_tile_x6s<C, IG>(stage(kt), stage(kt) + SA, acc);
 #if SMAML_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
   };
-  fetch(ra0, rb0, kbeg);
-  fetch(ra1, rb1, kbeg + BKc);
-  store(st0, ra0, rb0, true);
+  fetch_a(0);
+  issue_b(0);
+  store(0);
+  if constexpr (DMA_B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (late && nkt > 1) fetch_a(1);
   __syncthreads();
-  // iteration kt: tile kt in stage kt & 1, tile kt + 1 in the other register set; load tile kt + 2
-  // into this set, MFMAs of tile kt, store tile kt + 1 into the idle stage, barrier
-  for (int kt = 0; kt < nkt; kt += 2) {
-    fetch(ra0, rb0, kbeg + (kt + 2) * BKc);
-    mma(kt);
-    store(st0 + ((kt + 1) & 1) * C::X6S_STAGE, ra1, rb1, kt + 1 < nkt);
-    __syncthreads();
-    if (kt + 1 >= nkt) break;
-    fetch(ra1, rb1, kbeg + (kt + 3) * BKc);
-    mma(kt + 1);
-    store(st0 + (kt & 1) * C::X6S_STAGE, ra0, rb0, kt + 2 < nkt);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bool more = kt + 1 < nkt;
+    if (late) {
+      if (more) {
+        issue_b(kt + 1);
+        store(kt + 1);  // (tile kt + 1's f32 operands arrived under the previous iteration's MFMAs)
+      }
+      // (tile kt + 2's loads stay behind the image copies in issue order: the counted wait below)
+      if constexpr (DMA_B) asm volatile("" ::: "memory");
+      if (kt + 2 < nkt) fetch_a(kt + 2);
+      mma(kt);
+      if constexpr (DMA_B) {  // this wave's image chunks of tile kt + 1 landed (tile kt + 2's A loads may not)
+        if (kt + 2 < nkt)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::A_F4) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      if (more) {
+        fetch_a(kt + 1);
+        issue_b(kt + 1);
+      }
+      mma(kt);
+      if (more) store(kt + 1);
+      if constexpr (DMA_B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   }
 }

@@ -375,6 +375,9 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
 #ifndef SMAML_DIAG_FWD
 #define SMAML_DIAG_FWD 0  // timing diagnostics only (wrong results): 1 = forward step without its epilogue,
 #endif                    // 2 = without its GEMM
+#ifndef SMAML_GATE_STAGGER
+#define SMAML_GATE_STAGGER 0  // primal gate K loop on the staggered staged loop (gemm_mainloop_x6s_stag)
+#endif
 // XG (xg != null): layer 0's input projection of this step's windows comes from the XgDedup table
 // (launch_xg_dedup): the accumulators start from it and the K loop covers the recurrent segment only.
 // HIMG (with IMG and the XG table): A tiles as pre-split h images (kernels.h HImgs) -- x = h(l - 1, t) from
@@ -447,6 +450,9 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
         const char* ph = hi->block(l, (t + 1) & 1, z, H);
         const HImgA<2> lai{{l > 0 ? hi->block(l - 1, t & 1, z, H) : ph, ph}, {cin, H}};
         gemm_mainloop<CfgGate>(lai, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
+      } else if constexpr (SMAML_GATE_STAGGER) {
+        NoHook nh;
+        gemm_mainloop_x6s_stag<CfgGate, -1>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem, nh);
       } else {
         gemm_mainloop<CfgGate>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
       }
@@ -1930,14 +1936,14 @@ constexpr int wgrad_smem_floats() {
 // Pair (A2 != null): slices [nsplit1, nsplit) of each task sum a second problem of the same shape,
 // A2^T [B1s | B2s] (the tangent weight gradient's dG^T [Rx | Rh] beside R(dG)^T [x | h]), into the
 // same partial slabs; its slices carry no bias column (zeros).
-#ifndef SMAML_WGRAD_PF2
-#define SMAML_WGRAD_PF2 0  // weight-gradient staged mainloop with loads two K-tiles ahead (gemm_mainloop_x6s_pf2)
+#ifndef SMAML_WGRAD_STAGGER
+#define SMAML_WGRAD_STAGGER 0  // weight gradients on the staggered staged loop (gemm_mainloop_x6s_stag)
 #endif
 template <class C, class LA, class LB, class Hook>
 __device__ __forceinline__ void wgrad_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
                                                Acc<C>& acc, float* smem, Hook& hook) {
-  if constexpr (SMAML_WGRAD_PF2 && C::X6S && C::X6S_NST == 2)
-    gemm_mainloop_x6s_pf2<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
+  if constexpr (SMAML_WGRAD_STAGGER && C::X6S && C::X6S_NST == 2 && C::NTH == 512)
+    gemm_mainloop_x6s_stag<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
   else
     gemm_mainloop<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
 }

@@ -182,32 +182,29 @@ class HybridSTGCN_LSTM(nn.Module):
         return out
 
     def _packed(self, which, named, dims, device):
-        """The flat (padded) parameter vector of `named` on `device`, packed into one cached buffer.
-        With grad enabled (training: the vector is also what the backward differentiates at) it is
-        re-packed on every call -- one multi-tensor copy -- so writes that autograd does not see
-        (``p.data.copy_(...)``, ``p.data -= lr * g``, numpy arrays aliasing a parameter) are always
-        picked up. Under no_grad (inference loops) it is re-packed only when a parameter object was
-        replaced, its storage moved (``p.data = t``) or it was written in place through autograd's
-        version counter (optimizer steps, load_state_dict); after an untracked ``.data`` write call
-        ``invalidate_packed()``. Returns (flat, re-packed?)."""
+        """The flat (padded) parameter vector of `named` on `device`, packed into one cached buffer. It is
+        re-packed on every call (one multi-tensor copy into the same buffer), so writes that autograd does
+        not see (``p.data.copy_(...)``, ``p.data -= lr * g``, numpy arrays aliasing a parameter) are always
+        picked up, with or without grad. Returns (flat, changed?): changed is True when a parameter object
+        was replaced, its storage moved or it was written in place through autograd's version counter
+        (optimizer steps, load_state_dict) -- always True with grad enabled (the backward differentiates at
+        this vector) -- and tells callers that hand the buffer to the library by pointer to re-register it."""
         cache = self.__dict__.setdefault("_pack_cache", {})
         objs = [p for _, p in named]
         key = [(p._version, p.data_ptr()) for p in objs]
         ent = cache.get(which)
-        if (not torch.is_grad_enabled() and ent is not None and ent["device"] == device
+        same = (not torch.is_grad_enabled() and ent is not None and ent["device"] == device
                 and len(ent["objs"]) == len(objs) and all(a is b for a, b in zip(ent["objs"], objs))
-                and ent["key"] == key):
-            return ent["flat"], False
+                and ent["key"] == key)
         total = (params.trainable_layout(dims) if which == 0 else params.gcn_layout(dims))[1]
         reuse = ent["flat"] if ent is not None and ent["device"] == device and ent["flat"].numel() == total else None
         flat = params.pack({n: p.detach() for n, p in named}, dims, which=which, device=device, out=reuse)
         cache[which] = {"device": device, "objs": objs, "key": key, "flat": flat}
-        return flat, True
+        return flat, not same
 
     def invalidate_packed(self):
-        """Drop the packed parameter vectors: the next forward re-packs them. Needed only after a
-        parameter write that autograd does not track (through ``.data`` or an aliasing array) followed
-        by a forward under no_grad; grad-enabled forwards always re-pack."""
+        """Drop the packed parameter vectors (the next forward allocates and packs them afresh). Every
+        forward re-packs anyway, so this only releases the buffers."""
         self.__dict__.pop("_pack_cache", None)
 
     # ------------------------------------------------------------------ module API
