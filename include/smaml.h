@@ -293,7 +293,7 @@ int smaml_timing_collect(smaml_ctx* ctx, double* ms, double* flops, int64_t* cou
  * kernels.h enum Variant (_capi.VARIANTS): fwd, fwd_drop, fwd_split, fwd_img, fwd_dual,
  * fwd_dual_kept, fwd_dual_img, bwd_big, bwd_small, bwd_split, bwd_dual_big, bwd_dual_big_kept,
  * bwd_dual_small, bwd_dual_small_kept, wgrad, wgrad_wide, wgrad_pair, fwd_kw, bwd_kw, gcn_dedup,
- * xg_dedup, wgrad_dedup, f_compact, fwd_himg.
+ * xg_dedup, wgrad_dedup, f_compact.
  * Writes min(cap, count) entries, *count = number of variants; reset != 0 zeroes them. Host-side
  * counters: no synchronisation. Lets tests assert which configurations ran. */
 int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* count, int32_t reset);
@@ -359,15 +359,10 @@ int smaml_variant_counts(smaml_ctx* ctx, int64_t* counts, int32_t cap, int32_t* 
  *   "f_compact":                   where every reader of a step's GCN features goes through the distinct
  *                                  stream rows (xg_dedup forwards on the big tiles, wgrad_dedup
  *                                  backwards), the GCN stores each distinct row once instead of to every
- *                                  (sample, step) holding it (1, the default; bitwise equal to 0);
- *   "h_img":                       a big-tile primal forward sweep with layer 0's XG table and the gate weight
- *                                  images also writes each h(l, t) as the bf16-piece image of the gate GEMM's
- *                                  A tiles, which the next diagonal copies into LDS with direct-to-LDS loads
- *                                  instead of splitting f32 h in every workgroup (0, the default: measured
- *                                  slower, the image writes cost the forward more than the split they
- *                                  save; bitwise equal to 1).
+ *                                  (sample, step) holding it (1, the default; bitwise equal to 0).
  *   (Round 6 removed the options of arms that measured slower -- bptt_push, wgrad_ws, rowsum_side,
- *   gcn_side, reduce_side, wgrad_overlap, wgrad_min_kt, wgrad_threads; DESIGN.md keeps their A/B record.) */
+ *   gcn_side, reduce_side, wgrad_overlap, wgrad_min_kt, wgrad_threads, and its own h_img; DESIGN.md
+ *   keeps their A/B record.) */
 int smaml_set_option(smaml_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -14,7 +14,7 @@
 #   pmc_sq          SQ instruction-mix / MFMA-busy counters of the same workload (one --pmc pass)
 #   shares          one-GPU timings of rank 0's share at N = 2 / 4 / 8 (8 / 4 / 2 tasks)
 #   ab              A/B: AB_VARIANTS (words "lib:<file in the package dir>", "opt:<k=v[,k=v]>" or both as
-#                   "lib:<file>+opt:<k=v>", "base" =
+#                   "lib:<file>+opt:<k=v>", or "arg:<extra bench.py args, + for spaces>"; "base" =
 #                   the default library) each in its own process, AB_ROUNDS interleaved rounds of
 #                   bench.py $AB_ARGS                      -> gpurun_out/$TAG/ab.log
 # TAG names the output directory (default "session").
@@ -91,13 +91,15 @@ for s in "$@"; do
       : > "$O/ab.log"
       for round in $(seq 1 "${AB_ROUNDS:-2}"); do
         for v in ${AB_VARIANTS:-base}; do
+          extra=""
           case $v in
+            arg:*) envs=(); extra=${v#arg:}; extra=${extra//+/ } ;;
             lib:*+opt:*) l=${v#lib:}; envs=(SMAML_LIB=$PKG/${l%%+opt:*} SMAML_OPTIONS=${l#*+opt:}) ;;
             lib:*) envs=(SMAML_LIB=$PKG/${v#lib:}) ;;
             opt:*) envs=(SMAML_OPTIONS=${v#opt:}) ;;
             *) envs=() ;;
           esac
-          env "${envs[@]}" timeout -k 10 900 python bench.py ${AB_ARGS:---steps 3 --warmup 1 --cpu-sample-steps 0 --adapt-epochs 0 --cfg5-share-tasks 0} \
+          env "${envs[@]}" timeout -k 10 900 python bench.py ${AB_ARGS:---steps 3 --warmup 1 --cpu-sample-steps 0 --adapt-epochs 0 --cfg5-share-tasks 0} $extra \
             > "$O/ab_tmp.log" 2>&1
           ok $? "ab $v"
           echo "$v $(bench_json "$O/ab_tmp.log")" >> "$O/ab.log"

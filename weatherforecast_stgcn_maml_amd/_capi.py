@@ -32,7 +32,7 @@ GCN_RELU, GCN_PLAIN = 1, 2  # smaml_gcn_conv_ex / _backward flags
 # kernels.h enum Variant: launch counters per kernel tile configuration (smaml_variant_counts)
 VARIANTS = ("fwd", "fwd_drop", "fwd_split", "fwd_img", "fwd_dual", "fwd_dual_kept", "fwd_dual_img", "bwd_big", "bwd_small", "bwd_split",
             "bwd_dual_big", "bwd_dual_big_kept", "bwd_dual_small", "bwd_dual_small_kept", "wgrad", "wgrad_wide", "wgrad_pair",
-            "fwd_kw", "bwd_kw", "gcn_dedup", "xg_dedup", "wgrad_dedup", "f_compact", "fwd_himg")
+            "fwd_kw", "bwd_kw", "gcn_dedup", "xg_dedup", "wgrad_dedup", "f_compact")
 
 # api.cpp enum Cat: one kernel per category (the bench's roofline kernel is one symbol)
 TIMING_CATEGORIES = ("gcn_layer", "lstm_fwd_step", "lstm_fwd_dual", "head_loss", "head_dh", "lstm_bwd_step",

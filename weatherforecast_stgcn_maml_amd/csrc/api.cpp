@@ -221,7 +221,6 @@ static Knobs default_knobs() {
   k.bptt_streams = SMAML_BPTT_STREAMS_DEFAULT;
   k.fwd_streams = SMAML_FWD_STREAMS_DEFAULT;
   k.f_compact = SMAML_F_COMPACT_DEFAULT;
-  k.h_img = SMAML_H_IMG_DEFAULT;
   return k;
 }
 
@@ -293,8 +292,6 @@ struct smaml_ctx {
   int64_t xg_cap = 0;
   float* xgd_buf = nullptr;   // big-tile forward: layer 0's projection per distinct stream row (prep_xg_dedup)
   int64_t xgd_cap = 0;
-  char* himg_buf = nullptr;   // big-tile forward: pre-split h images, a ring of two steps per layer (prep_h_img)
-  int64_t himg_cap = 0;
   // grid-barrier state of the bookkeeping kernels (kernels.h GridBar): device words [3], the pinned
   // device-mapped error flag a timed-out waiter sets, the wait bound and the launch form
   unsigned* bar = nullptr;
@@ -988,35 +985,6 @@ bool prep_xg_dedup(smaml_ctx* c, hipStream_t s, bool consec, const float* theta,
   return true;
 }
 
-// Pre-split h images for this forward sweep (kernels.h HImgs, option h_img): only when EVERY diagonal runs
-// the big-tile gate kernel with the gate weight images and layer 0's XG table (so the input segment of
-// layer 0 never reads the images and every image's readers run after its writer). No room: off.
-bool prep_h_img(smaml_ctx* c, hipStream_t s, const float* theta, bool use_xgd) {
-  const Dims& d = c->d;
-  Work& w = c->w;
-  w.himg = HImgs{};
-  if (!c->kn.h_img || !use_xgd || w.drop.lstm() || !(w.gimg.th && w.gimg_src == theta) || d.H % 16) return false;
-  for (int diag = 0; diag < d.T + d.L - 1; ++diag)
-    if (!fwd_wave_big(d, w, c->po, diag)) return false;
-  const int64_t need = h_img_bytes(d.L, w.Z, w.M, d.H);
-  if (need > c->himg_cap) {
-    if (c->himg_buf) HIP_TRY(hipFree(c->himg_buf));
-    c->himg_buf = nullptr;
-    c->himg_cap = 0;
-    if (hipMalloc((void**)&c->himg_buf, need) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    c->himg_cap = need;
-    // (rows of a partial last tile are never written: zeros, so their unused products stay finite)
-    HIP_TRY(hipMemsetAsync(c->himg_buf, 0, need, s));
-  }
-  w.himg.p = c->himg_buf;
-  w.himg.ntm = (w.M + 255) / 256;
-  w.himg.Z = w.Z;
-  return true;
-}
-
 // LSTM forward over all layers and time steps from w.F (anti-diagonal wavefront). consec: every task
 // of this step reads B consecutive windows (layer 0's projection may then run once per stream row).
 int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, bool consec = false) {
@@ -1028,7 +996,6 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
   for (int diag = 0; xgd_ok && diag < d.T; ++diag) xgd_ok = fwd_wave_big(d, w, c->po, diag);
   const bool use_xgd = xgd_ok && prep_xg_dedup(c, s, true, theta, nullptr, tstride, true);
   if (w.fcompact && !use_xgd) return fail(SMAML_ESTATE, "compact features without the layer-0 projection table");
-  prep_h_img(c, s, theta, use_xgd);
   // Batch-1 sizes (the small-grid steps): layer 0's input projection F . W_ih0^T does not depend on the
   // recurrence, so it runs for all T steps as one throughput-bound GEMM before the wavefront and the
   // layer-0 steps' latency-bound K loops cover only the recurrent segment (kernels_small.hip).
@@ -1084,7 +1051,6 @@ int run_lstm(smaml_ctx* c, hipStream_t s, const float* theta, int64_t tstride, b
   w.xg = nullptr;
   w.xg_src = nullptr;
   w.xgd = XgDedup{};
-  w.himg = HImgs{};
   HIP_TRY(hipGetLastError());
   return SMAML_OK;
 }
@@ -1498,7 +1464,6 @@ int smaml_destroy(smaml_ctx* c) {
   if (c->bimg_buf) (void)hipFree(c->bimg_buf);
   if (c->xg_buf) (void)hipFree(c->xg_buf);
   if (c->xgd_buf) (void)hipFree(c->xgd_buf);
-  if (c->himg_buf) (void)hipFree(c->himg_buf);
   if (c->bar) (void)hipFree(c->bar);
   for (int i = 0; i < 4; ++i) {
     if (c->cs[i]) (void)hipStreamDestroy(c->cs[i]);
@@ -2130,8 +2095,6 @@ int smaml_set_option(smaml_ctx* c, const char* key, int64_t value) {
     c->kn.wgrad_dedup = (int)value;
   } else if (k == "bptt_streams" && value >= 1 && value <= 4) {
     c->kn.bptt_streams = (int)value;
-  } else if (k == "h_img" && (value == 0 || value == 1)) {
-    c->kn.h_img = (int)value;
   } else if (k == "f_compact" && (value == 0 || value == 1)) {
     c->kn.f_compact = (int)value;
   } else if (k == "fwd_streams" && value >= 0 && value <= 4) {

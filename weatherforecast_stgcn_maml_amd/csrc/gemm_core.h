@@ -420,9 +420,8 @@ struct BStage<C, LB, true> {
   __device__ __forceinline__ void store(char*) const {}
 };
 
-// A operand staging, the same two forms: f32 float4s split at the LDS store, or (DMA, loaders.h HImgA) a
-// pre-split image issued straight into the stage.
-template <class C, class LA, bool DMA = has_dma_image<LA>::value>
+// A operand staging: this thread's f32 float4s of the tile, split into the bf16 planes at the LDS store.
+template <class C, class LA>
 struct AStage {
   float4 r[C::A_F4];
   __device__ __forceinline__ void fetch(const LA& la, int m0, int k0, char*) {
@@ -431,14 +430,6 @@ struct AStage {
   __device__ __forceinline__ void store(char* img) const {
     store_tile_x6<C::BM, C::A_F4, C::NTH, C::A_KC, C::BK, C::MSW>(img, r);
   }
-};
-template <class C, class LA>
-struct AStage<C, LA, true> {
-  static_assert(C::X6S && C::X6S_NST == 2, "pre-split A images: two LDS stages (issued into the idle one)");
-  __device__ __forceinline__ void fetch(const LA& la, int m0, int k0, char* img) {
-    la.template issue<C::BM, C::A_KC, C::BK, C::NTH>(img, m0, k0);
-  }
-  __device__ __forceinline__ void store(char*) const {}
 };
 
 // The three pieces of the 32-row fragment at tile row `row` (this lane's row = row + (lane & 31)
@@ -508,9 +499,7 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
   char* st0 = reinterpret_cast<char*>(smem);
   const int nkt = (kend - kbeg + BKc - 1) / BKc;
   if (nkt <= 0) return;
-  constexpr bool DMA_A = has_dma_image<LA>::value;
-  constexpr bool DMA = DMA_A || has_dma_image<LB>::value;
-  static_assert(!DMA_A || !has_stage_a<Hook>::value, "a pre-split A image has no f32 staging for the hook");
+  constexpr bool DMA = has_dma_image<LB>::value;
   AStage<C, LA> ra;
   BStage<C, LB> rb;
   auto store = [&](char* st) {
@@ -554,90 +543,6 @@ __device__ __forceinline__ void gemm_mainloop_x6s(const LA& la, const LB& lb, in
       __builtin_amdgcn_s_setprio(0);
 #endif
       if (more) store(st0 + (cur ^ 1) * C::X6S_STAGE);
-    }
-    __syncthreads();
-  }
-}
-
-// Staggered staged mainloop (MI355X_MICROARCH "Two waves per SIMD", item 9). An 8-wave workgroup puts
-// waves w and w + NW/2 on one SIMD; in gemm_mainloop_x6s both run [MFMAs of tile k; split + LDS store of
-// tile k + 1] in lockstep, so the SIMD's matrix pipe idles through both waves' split VALU. Here the
-// second half of the waves runs each iteration the other way round -- [split + store of tile k + 1;
-// MFMAs of tile k] -- with tile k + 1's operands fetched one iteration earlier (the same number of
-// staging registers: each wave holds exactly one tile in flight), so on every SIMD one wave splits while
-// its partner issues MFMAs. Both orders are legal inside an iteration: tile k + 1 goes to the idle stage,
-// last read before the previous barrier. Same loads, splits and products per accumulator as
-// gemm_mainloop_x6s: bitwise-identical results. f32-staged operands only (a DMA image issued two
-// tiles ahead would land in the stage the current MFMAs read).
-template <class C, int IG, class LA, class LB, class Hook>
-__device__ __forceinline__ void gemm_mainloop_x6s_stag(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
-                                                       Acc<C>& acc, float* smem, Hook& hook) {
-  constexpr bool DMA_B = has_dma_image<LB>::value;
-  static_assert(C::X6S && C::X6S_NST == 2 && !has_dma_image<LA>::value, "staggered loop: staged f32 A, two stages");
-  static_assert(C::NTH == 512, "staggered loop: two waves per SIMD (8 waves)");
-  constexpr int BKc = C::BK;
-  constexpr int SA = C::AImg::BYTES;
-  char* st0 = reinterpret_cast<char*>(smem);
-  const int nkt = (kend - kbeg + BKc - 1) / BKc;
-  if (nkt <= 0) return;
-  const bool late = (threadIdx.x >> 6) >= 4;  // waves 4-7: store first, then the MFMAs
-  AStage<C, LA> ra;
-  BStage<C, LB> rb;
-  auto stage = [&](int kt) { return st0 + (kt & 1) * C::X6S_STAGE; };
-  // f32 operands go to registers; a DMA B image (pre-split weights) is issued straight into tile kt's
-  // stage -- only ever one tile ahead, into the idle stage, by early and late waves alike
-  auto fetch_a = [&](int kt) {
-    ra.fetch(la, m0, kbeg + kt * BKc, nullptr);
-    if constexpr (!DMA_B) rb.fetch(lb, n0, kbeg + kt * BKc, nullptr);
-  };
-  auto issue_b = [&](int kt) {
-    if constexpr (DMA_B) rb.fetch(lb, n0, kbeg + kt * BKc, stage(kt) + SA);
-  };
-  auto store = [&](int kt) {
-    if constexpr (has_stage_a<Hook>::value) hook.template stage_a<C::A_F4>(ra.r);
-    ra.store(stage(kt));
-    rb.store(stage(kt) + SA);
-  };
-  auto mma = [&](int kt) {
-#if SMAML_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
-    mma_tile_x6s<C, IG>(stage(kt), stage(kt) + SA, acc);
-#if SMAML_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-  };
-  fetch_a(0);
-  issue_b(0);
-  store(0);
-  if constexpr (DMA_B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (late && nkt > 1) fetch_a(1);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + 1 < nkt;
-    if (late) {
-      if (more) {
-        issue_b(kt + 1);
-        store(kt + 1);  // (tile kt + 1's f32 operands arrived under the previous iteration's MFMAs)
-      }
-      // (tile kt + 2's loads stay behind the image copies in issue order: the counted wait below)
-      if constexpr (DMA_B) asm volatile("" ::: "memory");
-      if (kt + 2 < nkt) fetch_a(kt + 2);
-      mma(kt);
-      if constexpr (DMA_B) {  // this wave's image chunks of tile kt + 1 landed (tile kt + 2's A loads may not)
-        if (kt + 2 < nkt)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::A_F4) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else {
-      if (more) {
-        fetch_a(kt + 1);
-        issue_b(kt + 1);
-      }
-      mma(kt);
-      if (more) store(kt + 1);
-      if constexpr (DMA_B) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
   }

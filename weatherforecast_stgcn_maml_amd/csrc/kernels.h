@@ -101,7 +101,6 @@ enum Variant {
   V_XG_DEDUP,        // k_xg_dedup: layer 0's input projection once per distinct stream row (big-tile forward)
   V_WGRAD_DEDUP,     // layer 0's input-weight gradient over distinct stream rows (k_dg_rowsum + gathered k_wgrad)
   V_F_COMPACT,       // GCN features stored once per distinct stream row (Work::fcompact)
-  V_FWD_HIMG,        // k_lstm_fwd_step with pre-split h images (HImgs; also counted as V_FWD, V_FWD_IMG)
   NVAR
 };
 
@@ -140,8 +139,6 @@ struct Knobs {
                                  // chunks on side streams (a chunk's rows depend on nothing else), so one
                                  // chunk's next diagonal fills the other's tail; weight gradients after the sweep
   int fwd_streams = 0;           // the same for the big-tile forward diagonals (primal and tangent); 0 = auto
-  int h_img = 0;                 // 1: the big-tile primal forward (with layer 0's XG table) hands h to the next
-                                 // diagonal as pre-split bf16 images (HImgs)
   int f_compact = 0;             // 1: where every reader of a step's features goes through the distinct stream rows
                                  // (xg_dedup forwards, wgrad_dedup backwards), the GCN stores only those rows
 };
@@ -165,9 +162,6 @@ struct Knobs {
 #endif
 #ifndef SMAML_BPTT_STREAMS_DEFAULT
 #define SMAML_BPTT_STREAMS_DEFAULT 2  // A/B (profiles/r05_ab_streams*.log): config 2 1653 -> 1618 ms, config-5 share 4453 -> 4308 ms
-#endif
-#ifndef SMAML_H_IMG_DEFAULT
-#define SMAML_H_IMG_DEFAULT 0  // A/B (profiles/r06_ab_h_img.log): forward 201.2 -> 207.6 ms with the images: off
 #endif
 #ifndef SMAML_F_COMPACT_DEFAULT
 #define SMAML_F_COMPACT_DEFAULT 1
@@ -198,28 +192,6 @@ struct GateImgs {
   int64_t tstride = 0;              // bytes per task
   int64_t off[MAX_LAYERS][2] = {};  // byte offset of (layer, W_ih | W_hh) in a task's images
 };
-// ---- pre-split h images (round 6; big-tile forward) ----
-// The big-tile forward's epilogue also stores each h(l, t) as the staged-split LDS image of the gate
-// GEMM's A tiles (X6Img<256, KC, 16>: 3 bf16 planes x 256 rows x 16 k = 24 KB per (row tile, K-tile)),
-// so the next diagonal's two readers of it -- layer l at t + 1 (recurrent segment) and layer l + 1 at t
-// (input segment) -- copy their A tiles into LDS with direct-to-LDS loads instead of loading f32 h and
-// splitting it in every workgroup (the split is deterministic: bitwise the same products). A ring of two
-// steps per layer: image (l, t) lives in slot t & 1 and is overwritten by step t + 2, two diagonals later,
-// after both readers ran (stream order; row chunks on side streams touch only their own row tiles).
-// Layout [L][2][Z][ntm][H / 16] images. The f32 h stays (BPTT, weight gradients, head, tangent forward).
-constexpr int H_IMG_BYTES = 3 * 256 * 16 * 2;
-struct HImgs {
-  char* p = nullptr;  // null: off (the gate kernels load and split f32 h)
-  int ntm = 0;        // 256-row tiles per (layer, slot, task)
-  int Z = 0;
-  // image block of (layer l, ring slot, task z): image (tm, kt) at + (tm * (H / 16) + kt) * H_IMG_BYTES
-  __host__ __device__ char* block(int l, int slot, int z, int H) const {
-    return p + ((int64_t)(l * 2 + slot) * Z + z) * ntm * (H / 16) * H_IMG_BYTES;
-  }
-};
-__host__ __device__ inline int64_t h_img_bytes(int L, int Z, int M, int H) {
-  return (int64_t)L * 2 * Z * ((M + 255) / 256) * (H / 16) * H_IMG_BYTES;
-}
 // ---- pre-split BPTT weight images (kernels_small.hip launch_split_bwd; small-grid BPTT) ----
 // Per task, for W_hh of every layer and W_ih of layers >= 1 (the [4H][H] matrices the BPTT step reads
 // as B[k][j]): per K-tile kt (16 gate rows) and unit tile tn (32 units) three bf16 planes of
@@ -262,7 +234,6 @@ struct Work {
   int fcompact = 0;                // F holds only the distinct rows of those windows, in XgDedup's row order
                                    // (rows [0, (2B + T - 2) N) of each task's slab): read through XgDedup only
   GateImgs gimg{};         // pre-split images of the weights the gate GEMMs read (launch_split_gate)
-  HImgs himg{};            // pre-split h images of the big-tile forward (run_lstm, option h_img)
   const float* gimg_src = nullptr; // the parameter vector gimg.th was split from (kernels use it only for that one)
   const float* gimg_u_src = nullptr;// ... and gimg.u (the sweep's tangent direction)
   int64_t* vcount = nullptr;       // [NVAR] launch counters (ctx-owned; may be null)

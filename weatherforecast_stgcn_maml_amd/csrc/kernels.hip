@@ -293,14 +293,10 @@ __device__ __forceinline__ void fwd_cell(const Acc<CfgGate>& acc, const float* _
 // one 16-B c_{t-1} load and six 16-B stores (i, f, g, o, c, h). XG: the pre-activations also get the
 // row's XgDedup entries (layer 0's input projection, xg = the step's block of window rows): four more
 // 16-B loads per item.
-// HIMG: h also goes to the pre-split image block himg (kernels.h HImgs; this step's layer, ring slot and
-// task): three 8-B plane stores per item at the staged split's LDS offsets of (tile row, unit).
-template <int H, class CG, bool XG = false, bool HIMG = false>
+template <int H, class CG, bool XG = false>
 __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __restrict__ th, const LayerOff& lo,
                                            float* __restrict__ Gz, float* __restrict__ Cz, float* __restrict__ Hz,
-                                           int m0, int ug, int t, int M, float* smem, const float* xg = nullptr,
-                                           char* __restrict__ himg = nullptr) {
-  static_assert(!HIMG || CG::BM == 256, "h images are 256-row tiles");
+                                           int m0, int ug, int t, int M, float* smem, const float* xg = nullptr) {
   const int j = ug * 32 + (int)(threadIdx.x & 31);
   float bsum[4];
 #pragma unroll
@@ -353,43 +349,20 @@ __device__ __forceinline__ void fwd_cell_t(const Acc<CG>& acc, const float* __re
         sto(Gz, og + 12u * H, go);
         sto(Cz, oh, c);
         sto(Hz, oh, hh);
-        if constexpr (HIMG) {
-          // split the STORED (rounded) h: without the barrier, fp-contract fuses o * tanh(c) into the split's
-          // first subtraction (an fma of the exact product) and the pieces would differ from those the
-          // readers' own split of the f32 h forms
-          float4 hv = hh;
-          asm volatile("" : "+v"(hv.x), "+v"(hv.y), "+v"(hv.z), "+v"(hv.w));
-          uint2 p0, p1, p2;
-          split4(hv, p0, p1, p2);
-          const int ki = (int)jq & 15;  // (H / 16 K-tiles of 16 units: K-tile jq >> 4 of the readers' h segment)
-          char* o = himg + ((int64_t)(m0 >> 8) * (H / 16) + (jq >> 4)) * H_IMG_BYTES + ml * 32 +
-                    16 * ((ki >> 3) ^ ((ml >> 3) & 1)) + 2 * (ki & 7);
-          constexpr int PL = H_IMG_BYTES / 3;
-          *reinterpret_cast<uint2*>(o) = p0;
-          *reinterpret_cast<uint2*>(o + PL) = p1;
-          *reinterpret_cast<uint2*>(o + 2 * PL) = p2;
-        }
       });
 }
 
 #ifndef SMAML_DIAG_FWD
 #define SMAML_DIAG_FWD 0  // timing diagnostics only (wrong results): 1 = forward step without its epilogue,
 #endif                    // 2 = without its GEMM
-#ifndef SMAML_GATE_STAGGER
-#define SMAML_GATE_STAGGER 0  // primal gate K loop on the staggered staged loop (gemm_mainloop_x6s_stag)
-#endif
 // XG (xg != null): layer 0's input projection of this step's windows comes from the XgDedup table
 // (launch_xg_dedup): the accumulators start from it and the K loop covers the recurrent segment only.
-// HIMG (with IMG and the XG table): A tiles as pre-split h images (kernels.h HImgs) -- x = h(l - 1, t) from
-// layer l - 1's ring slot t & 1, h_{t-1} from layer l's slot (t - 1) & 1 -- and h(l, t) written to slot t & 1.
-template <int H, bool DROP, bool IMG = false, bool HIMG = false>
+template <int H, bool DROP, bool IMG = false>
 __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                               float* __restrict__ CsAll, float* __restrict__ GsAll, int64_t lsz,
                                               const float* __restrict__ theta, int64_t tstride, FwdWave wv, int T,
                                               int M, const Drop& dr, float* smem, const GateImgs* gi = nullptr,
-                                              const float* xg = nullptr, int64_t xg_zstride = 0, int xg_N = 0,
-                                              const HImgs* hi = nullptr) {
-  static_assert(!HIMG || (IMG && !DROP), "h images: with the gate weight images, no dropout");
+                                              const float* xg = nullptr, int64_t xg_zstride = 0, int xg_N = 0) {
   int l, t, b0;
   LayerOff lo;
   const Blk bk = xcd_block();
@@ -422,10 +395,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
   const float* xgt = !DROP && xg && l == 0 ? xg + (int64_t)z * xg_zstride + xg_dedup_row0(t, M, xg_N) * (4 * H) : nullptr;
   if (xgt) kbeg = cin;
   if (SMAML_DIAG_FWD == 2) {  // timing diagnostic: cell epilogue only (no K loop)
-    if constexpr (HIMG)
-      fwd_cell_t<H, CfgGate, true, true>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt, hi->block(l, t & 1, z, H));
-    else
-      fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
+    fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
     return;
   }
   if (DROP && l > 0) {
@@ -446,16 +416,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
           o1 = gi->off[q][1];
         }
       const SegGateImg<2> lbi{{ib + o0, ib + o1}, {cin, H}};
-      if constexpr (HIMG) {  // (layer 0: the XG table covers the input segment, kbeg = cin)
-        const char* ph = hi->block(l, (t + 1) & 1, z, H);
-        const HImgA<2> lai{{l > 0 ? hi->block(l - 1, t & 1, z, H) : ph, ph}, {cin, H}};
-        gemm_mainloop<CfgGate>(lai, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
-      } else if constexpr (SMAML_GATE_STAGGER) {
-        NoHook nh;
-        gemm_mainloop_x6s_stag<CfgGate, -1>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem, nh);
-      } else {
-        gemm_mainloop<CfgGate>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
-      }
+      gemm_mainloop<CfgGate>(la, lbi, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
     } else {
       const SegGateBt<2> lbt{{th + lo.wih, th + lo.whh}, {cin, H}, H};
       gemm_mainloop<CfgGate>(la, lbt, m0, n0, kbeg, cin + (t > 0 ? H : 0), acc, smem);
@@ -471,9 +432,7 @@ __device__ __forceinline__ void lstm_fwd_step(const float* __restrict__ F, float
     if (sum == 12345.678f) Gz[threadIdx.x] = sum;  // (never true in practice; the MFMAs stay)
     return;
   }
-  if constexpr (HIMG) {
-    fwd_cell_t<H, CfgGate, true, true>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt, hi->block(l, t & 1, z, H));
-  } else if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1) {
+  if constexpr (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1) {
     fwd_cell_t<H, CfgGate, !DROP>(acc, th, lo, Gz, Cz, Hz, m0, ug, t, M, smem, xgt);
   } else {
     static_assert(!SMAML_XG_DEDUP_DEFAULT || (SMAML_FWD_EPI_T && CfgGate::WAVES_N == 1),
@@ -508,15 +467,14 @@ double fwd_wave(const Dims& d, const Work& w, const ParamOff& po, int diag, int 
 
 // The dropout variant holds the mask state beside the 4-gate tile: it gets the register budget
 // of 3 waves/SIMD instead of 4 (no spill).
-template <int H, bool IMG, bool HIMG = false>
+template <int H, bool IMG>
 __global__ SMAML_GATE_ATTR __launch_bounds__(CfgGate::NTH) void k_lstm_fwd_step(const float* __restrict__ F, float* __restrict__ HsAll,
                                                       float* __restrict__ CsAll, float* __restrict__ GsAll,
                                                       int64_t lsz, const float* __restrict__ theta, int64_t tstride,
-                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi, XgDedup xd,
-                                                      HImgs hi) {
+                                                      FwdWave wv, int T, int M, Drop dr, GateImgs gi, XgDedup xd) {
   __shared__ float smem[CfgGate::SMEM_FLOATS];
-  lstm_fwd_step<H, false, IMG, HIMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi, xd.xg,
-                                     xd.zstride, xd.N, &hi);
+  lstm_fwd_step<H, false, IMG>(F, HsAll, CsAll, GsAll, lsz, theta, tstride, wv, T, M, dr, smem, &gi, xd.xg, xd.zstride,
+                               xd.N);
 }
 
 // Layer 0's input projection of a step whose every task reads B consecutive windows, once per distinct
@@ -886,20 +844,13 @@ void launch_lstm_fwd_wave(hipStream_t s, const Dims& d, const Work& w, int diag,
   count_variant(w, V_FWD);
   XgDedup xd = w.xgd;
   if (xd.src != theta) xd.xg = nullptr;  // (a table of other weights is never read)
-  if (w.himg.p) {
-    // (run_lstm set the images for the whole sweep only with the gate images and the XG table of theta and
-    // every diagonal on these tiles: every reader of an image runs after its writer)
-    count_variant(w, V_FWD_IMG);
-    count_variant(w, V_FWD_HIMG);
-    SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, true, true><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd, w.himg)));
-  } else if (w.gimg.th && w.gimg_src == theta) {
+  if (w.gimg.th && w.gimg_src == theta) {
     count_variant(w, V_FWD_IMG);
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, true><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd, HImgs{})));
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd)));
   } else {
     SMAML_DISPATCH_H(d.H, (k_lstm_fwd_step<HT, false><<<grid, CfgGate::NTH, 0, s>>>(
-                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd, HImgs{})));
+                              w.F, w.Hs, w.Cs, w.Gs, lsz, theta, tstride, wv, d.T, w.M, w.drop, w.gimg, xd)));
   }
 }
 
@@ -1936,16 +1887,10 @@ constexpr int wgrad_smem_floats() {
 // Pair (A2 != null): slices [nsplit1, nsplit) of each task sum a second problem of the same shape,
 // A2^T [B1s | B2s] (the tangent weight gradient's dG^T [Rx | Rh] beside R(dG)^T [x | h]), into the
 // same partial slabs; its slices carry no bias column (zeros).
-#ifndef SMAML_WGRAD_STAGGER
-#define SMAML_WGRAD_STAGGER 0  // weight gradients on the staggered staged loop (gemm_mainloop_x6s_stag)
-#endif
 template <class C, class LA, class LB, class Hook>
 __device__ __forceinline__ void wgrad_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
                                                Acc<C>& acc, float* smem, Hook& hook) {
-  if constexpr (SMAML_WGRAD_STAGGER && C::X6S && C::X6S_NST == 2 && C::NTH == 512)
-    gemm_mainloop_x6s_stag<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
-  else
-    gemm_mainloop<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
+  gemm_mainloop<C, kWgradIG>(la, lb, m0, n0, kbeg, kend, acc, smem, hook);
 }
 
 struct WgPair {

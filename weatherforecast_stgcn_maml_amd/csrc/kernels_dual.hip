@@ -165,20 +165,6 @@ __device__ __forceinline__ void fwd_dual_tangent_epi_t(const Acc<CfgGateD>& at, 
       });
 }
 
-#ifndef SMAML_GATED_STAGGER
-#define SMAML_GATED_STAGGER 0  // tangent gate K loops (image path) on the staggered staged loop
-#endif
-template <class LA, class LB>
-__device__ __forceinline__ void gated_loop(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
-                                           Acc<CfgGateD>& acc, float* smem) {
-  if constexpr (SMAML_GATED_STAGGER && CfgGateD::X6S && CfgGateD::X6S_NST == 2 && CfgGateD::NTH == 512) {
-    NoHook nh;
-    gemm_mainloop_x6s_stag<CfgGateD, SMAML_IGLP>(la, lb, m0, n0, kbeg, kend, acc, smem, nh);
-  } else {
-    gemm_mainloop<CfgGateD, SMAML_IGLP>(la, lb, m0, n0, kbeg, kend, acc, smem);
-  }
-}
-
 // IMG: the weight tiles of theta and U come from their pre-split images (launch_split_gate).
 // xd.xg / xd.rxg (layer 0, set by the launcher only for this step's theta / U): layer 0's input
 // projections F W_ih0^T and F U_ih0^T of the step's consecutive windows (kernels.h XgDedup) start the
@@ -268,8 +254,8 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xdr}, lb, m0, n0, 0, cin + wh, ap, smem);
     else if constexpr (IMG)
-      gated_loop(SegKCt<2>{{xt, hp}, {cin, wh}, M}, SegGateImg<2>{{ith + io0, ith + io1}, {cin, wh}}, m0, n0, kb,
-                 cin + wh, ap, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M}, SegGateImg<2>{{ith + io0, ith + io1}, {cin, wh}},
+                                          m0, n0, kb, cin + wh, ap, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<2>{{xt, hp}, {cin, wh}, M},
                                           SegGateBt<2>{{th + lo.wih, th + lo.whh}, {cin, wh}, H}, m0, n0, kb,
@@ -315,9 +301,9 @@ __global__ SMAML_GATED_ATTR __launch_bounds__(CfgGateD::NTH) void k_lstm_fwd_dua
     if (DROP && l > 0)
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCDrop{la, xdr}, lb, m0, n0, 0, cin + wh + wrx + wh, at, smem);
     else if constexpr (IMG)
-      gated_loop(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
-                 SegGateImg<4>{{iu + io0, iu + io1, ith + io0, ith + io1}, {cin, wh, wrx, wh}}, m0, n0, kb,
-                 cin + wh + wrx + wh, at, smem);
+      gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
+                                          SegGateImg<4>{{iu + io0, iu + io1, ith + io0, ith + io1}, {cin, wh, wrx, wh}},
+                                          m0, n0, kb, cin + wh + wrx + wh, at, smem);
     else
       gemm_mainloop<CfgGateD, SMAML_IGLP>(SegKCt<4>{{xt, hp, rxt, rhp}, {cin, wh, wrx, wh}, M},
                                           SegGateBt<4>{{u + lo.wih, u + lo.whh, th + lo.wih, th + lo.whh},

@@ -376,34 +376,6 @@ struct SegGateImg {
   }
 };
 
-// Gate-GEMM A operand [x | h_{t-1}] as pre-split h images (kernels.h HImgs): segment s's image block at
-// p[s], image (row tile m0 / 256, K-tile kt) at + ((m0 >> 8) * (w[s] / 16) + kt) * H_IMG_BYTES, the exact
-// bytes of the staged split's LDS image; every wave copies its share of the 24 1-KB chunks with
-// global_load_lds_dwordx4 (64 lanes x 16 B, lane-contiguous in LDS).
-template <int NS>
-struct HImgA {
-  static constexpr bool kDmaImage = true;
-  const char* p[NS];
-  int w[NS];
-  template <int ROWS, bool KC, int BK, int NTH>
-  __device__ __forceinline__ void issue(char* dst, int m0, int k0) const {
-    static_assert(ROWS == 256 && KC && BK == 16, "h images: 256 rows x 16 k");
-    const char* b;
-    int ws, kk;
-    seg_pick<NS>(p, w, k0, b, ws, kk);
-    const char* src = b + ((int64_t)(m0 >> 8) * (ws / BK) + kk / BK) * H_IMG_BYTES;
-    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
-    constexpr int CH = H_IMG_BYTES / 1024, NW = NTH / 64;
-#pragma unroll
-    for (int c = 0; c < (CH + NW - 1) / NW; ++c) {
-      const int ch = wave + NW * c;
-      if (CH % NW == 0 || ch < CH)
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + ch * 1024 + 16 * lane), (lds_void_t*)(dst + ch * 1024),
-                                         16, 0, 0);
-    }
-  }
-};
-
 // Dropout mask on the x segment of an LSTM layer's input: x = drop(h_{l-1}) of one
 // (task, t) slab; element (m, k) has index base + m*H + k (kernels.h Drop, kind 2).
 struct XDrop {
