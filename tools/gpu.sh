@@ -12,6 +12,7 @@
 #                   --pmc FETCH_SIZE / WRITE_SIZE passes     -> gpurun_out/$TAG/prof_t$TASKS[_c5]/
 #                   (TASKS, default 15; CONFIG 2 or 5; tools/prof_summary.py reads the directory)
 #   pmc_sq          SQ instruction-mix / MFMA-busy counters of the same workload (one --pmc pass)
+#   pmc_clk         MFMA busy + effective clock (GRBM_GUI_ACTIVE) per kernel (tools/pmc_mfma_summary.py)
 #   shares          one-GPU timings of rank 0's share at N = 2 / 4 / 8 (8 / 4 / 2 tasks)
 #   ab              A/B: AB_VARIANTS (words "lib:<file in the package dir>", "opt:<k=v[,k=v]>" or both as
 #                   "lib:<file>+opt:<k=v>", or "arg:<extra bench.py args, + for spaces>"; "base" =
@@ -79,6 +80,14 @@ for s in "$@"; do
         SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA --kernel-include-regex "k_lstm|k_wgrad|k_gcn" \
         -f csv -d "$O/prof_pmc_sq" -o run -- python bench.py $PB > "$O/prof_pmc_sq.log" 2>&1
       ok $? pmc_sq ;;
+    pmc_clk)
+      # MFMA busy cycles and the effective clock (GRBM_GUI_ACTIVE / 8 over each dispatch's wall time)
+      W=$(workload_args)
+      PB="$W --steps 1 --warmup 0 --cpu-sample-steps 0 --adapt-epochs 0 --cfg5-share-tasks 0 --no-timing"
+      timeout -s KILL 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
+        --kernel-include-regex "k_lstm|k_wgrad|k_gcn|k_dg_rowsum|k_xg" -f csv -d "$O/prof_pmc_clk" -o run -- \
+        python bench.py $PB > "$O/prof_pmc_clk.log" 2>&1
+      ok $? pmc_clk ;;
     shares)
       : > "$O/shares.log"
       for T in 8 4 2; do
