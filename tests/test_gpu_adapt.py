@@ -152,3 +152,67 @@ def test_adaptation_cache_fill_batched_bitwise():
     for nb in (32, 3):
         assert np.array_equal(out[nb][0], out[0][0]), nb
         assert out[nb][1] == out[0][1] and out[nb][2] == out[0][2], nb
+
+
+def test_adapt_prepare_phases_and_cache_invalidation():
+    """smaml_adapt_prepare allocates the workspace and the per-window feature cache before any epoch
+    (adaptModel's set-up, adapt_hybrid_v5.py:163-181), so the epochs allocate nothing; the phase report
+    (smaml_adapt_phases) shows the batched cache fill in the first epoch only; a new set of GCN
+    parameters invalidates the cached windows without freeing them, and the next epoch refills them:
+    bitwise the same losses and parameters as a fresh context."""
+    from weatherforecast_stgcn_maml_amd import _capi, adapt as adapt_mod
+    from weatherforecast_stgcn_maml_amd.config import CONFIG2
+
+    d = CONFIG2
+    P = synth.init_params(25, d, gcn_bias_scale=0.1)
+    tr, gcn = _split(P)
+    lats, lons = synth.region_grid()
+    ei = build_spatial_graph(lats, lons, 4)[0]
+    feats = torch.from_numpy(np.ascontiguousarray(synth.make_features(3500, d.num_nodes, synth.t_total_for(24)))).cuda()
+    dev = torch.device("cuda:0")
+    stream = _capi.stream_ptr(torch)
+    order = np.random.default_rng(5).permutation(16).astype(np.int32).reshape(-1, 1)
+    lr_dev = torch.full((16,), 1e-3, device=dev)
+    gflat = params.pack({k: v for k, v in gcn.items() if k.startswith("base_stgcn.conv")}, d, which=1, device=dev)
+
+    def fresh_ctx():
+        ctx = _capi.Context(d, 0)
+        ctx.set_graph(ei)
+        ctx.set_gcn_params(gflat)
+        ctx.set_tasks([feats])
+        ctx.set_task_ids([0])
+        ctx.set_option("adapt_phase_sync", 1)
+        return ctx
+
+    def epoch(ctx, th, m, v, step):
+        losses = torch.empty(16, device=dev)
+        ctx.adapt_steps(stream, th, m, v, step, order, lr_dev, (0.9, 0.999), 1e-8, 0.0, adapt_mod.MAX_GRAD_NORM,
+                        losses)
+        torch.cuda.synchronize()
+        return losses.cpu().numpy(), ctx.adapt_phases()
+
+    th0 = params.pack(tr, d, which=0, device=dev)
+    ctx = fresh_ctx()
+    ctx.adapt_prepare(stream, 1)
+    prep = ctx.adapt_phases()
+    assert prep["cache_alloc_ms"] > 0.0
+    ctx.adapt_prepare(stream, 1)  # already prepared: nothing allocated (the phase is the timer's own cost)
+    assert ctx.adapt_phases()["cache_alloc_ms"] < 0.5
+    th, m, v = th0.clone(), torch.zeros_like(th0), torch.zeros_like(th0)
+    l1, ph1 = epoch(ctx, th, m, v, 0)
+    l2, ph2 = epoch(ctx, th, m, v, 16)
+    for ph in (ph1, ph2):
+        assert ph["reserve_ms"] < 0.5 and ph["cache_alloc_ms"] < 0.5 and ph["windows_filled_per_step"] == 0, ph
+    assert ph1["cache_fill_ms"] > ph2["cache_fill_ms"], (ph1, ph2)  # epoch 2 reads the cache
+    ctx.set_gcn_params(gflat)  # (same values, but the cache must not be trusted: refilled, not reallocated)
+    l3, ph3 = epoch(ctx, th, m, v, 32)
+    assert ph3["cache_alloc_ms"] < 0.5 and ph3["cache_fill_ms"] > ph2["cache_fill_ms"], (ph2, ph3)
+    got = (l1, l2, l3, th.cpu().numpy())
+    ctx.close()
+    # the same three epochs on a fresh context without adapt_prepare (the first call allocates)
+    ctx = fresh_ctx()
+    th, m, v = th0.clone(), torch.zeros_like(th0), torch.zeros_like(th0)
+    ref = [epoch(ctx, th, m, v, s)[0] for s in (0, 16, 32)] + [th.cpu().numpy()]
+    ctx.close()
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
