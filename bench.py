@@ -34,6 +34,8 @@ PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS  # dense BF16 MFMA = 16x the 
 # f32-accurate products as six bf16 piece products (gemm_core.h mfma_x6): 2516.8 / 6 = 419.5 TF of f32 work
 PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
+# bound on the N>1 C-ABI RCCL check after the timed region (its init alone waits up to 60 s)
+CAPI_COMM_WATCHDOG_S = 150.0
 # timing category -> GEMM family of smaml_build_info (product form of its contraction)
 CAT_FAMILY = {"gcn_layer": "gcn", "xg_proj": "gate", "lstm_fwd_step": "gate", "lstm_fwd_dual": "gate_dual", "lstm_bwd_step": "bptt",
               "lstm_bwd_dual": "bptt_dual", "wgrad": "wgrad", "head_dh": "bptt", "head_loss": "bptt"}
@@ -533,6 +535,7 @@ def main():
     qsum = float(res.losses[-1].sum().item()) if len(mine) else 0.0
     qmse = qsum / max(len(mine), 1)
     comm = None
+    hung = False  # the N>1 C-ABI RCCL check outlived its watchdog
     if world > 1:
         ar_ms, ar_n = ml.comm_time_collect()
         ml.comm_timing = False
@@ -546,14 +549,31 @@ def main():
         q = torch.tensor([qsum], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(q)
         qmse = float(q.item()) / args.tasks
-        if backend == "nccl" and os.environ.get("SMAML_BENCH_CAPI_COMM", "1") != "0":
+        capi_comm = os.environ.get("SMAML_BENCH_CAPI_COMM", "1")  # 0 = skip, force = also under gloo
+        if (backend == "nccl" and capi_comm != "0") or capi_comm == "force":
             # after the timed region: the C ABI's own RCCL communicator (smaml_comm_*) across
             # the same ranks, on a buffer the size of the meta-step's one all-reduce
+            # Its init is bounded by comm_timeout_ms, its collectives are not: run it on a daemon
+            # thread and, past CAPI_COMM_WATCHDOG_S, report the timeout in the line and leave
+            # without the (possibly blocked) teardown, so a hung check never costs the headline.
+            import threading
+
             from weatherforecast_stgcn_maml_amd.distributed import capi_comm_check
-            try:
-                comm["capi_comm_check"] = capi_comm_check(ml.ctx, ml.theta.numel() + 64)
-            except Exception as e:  # noqa: BLE001 - reported in the line; the headline is already measured
-                comm["capi_comm_check"] = {"status": f"error: {e}", "world": world}
+            box = {}
+
+            def check():
+                torch.cuda.set_device(local)
+                try:
+                    box["r"] = capi_comm_check(ml.ctx, ml.theta.numel() + 64)
+                except Exception as e:  # noqa: BLE001 - reported in the line; the headline is already measured
+                    box["r"] = {"status": f"error: {e}", "world": world}
+
+            th = threading.Thread(target=check, daemon=True)
+            th.start()
+            th.join(CAPI_COMM_WATCHDOG_S)
+            comm["capi_comm_check"] = box.get("r") or {
+                "status": f"error: no result within {CAPI_COMM_WATCHDOG_S} s (left without teardown)", "world": world}
+            hung = th.is_alive()
 
     ms_per_step = elapsed / args.steps * 1e3
     value = args.steps / elapsed
@@ -632,6 +652,10 @@ def main():
         out["config5_rank_share"] = config5_share_bench(args.cfg5_share_tasks, timing=not args.no_timing)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if hung:
+        # the check's thread is still inside a collective: a teardown could block on it
+        sys.stderr.flush()
+        os._exit(0)
     if world > 1:
         dist.destroy_process_group()
 
